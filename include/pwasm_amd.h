@@ -1,0 +1,187 @@
+/*
+ * pwasm_amd.h — C-ABI of the MI355X-native pafreport hot path (libpwasm_amd.so).
+ *
+ * The reference (gpertea/pwasm) has no FFI: its hot path is a set of C++ member functions
+ * called from pafreport's per-record loop.  Each entry point below replaces one of them;
+ * INTEGRATION.md shows the binding a maintainer would add to pafreport.cpp / GapAssem.cpp.
+ *
+ * Conventions: plain pointers + sizes, no torch or HIP C++ types in signatures (a stream is a
+ * `void*` holding a hipStream_t; NULL = the default stream); device buffers are caller-owned;
+ * every function returns 0 on success or a negative PW_E* status; launches are asynchronous
+ * on the given stream and never allocate or synchronise (graph-capture safe).
+ */
+#ifndef PWASM_AMD_H
+#define PWASM_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PW_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status codes */
+#define PW_OK 0
+#define PW_E_ARG (-1)     /* bad argument / shape */
+#define PW_E_HIP (-2)     /* HIP runtime error */
+#define PW_E_IO (-3)      /* host I/O */
+#define PW_E_NOMEM (-4)   /* host allocation */
+#define PW_E_NODEV (-5)   /* no gfx950 device */
+
+/* ---------------------------------------------------------------- packed cs op stream
+ * The CPU pre-pass (pw_pack_cs) turns a short-form cs string into 32-bit ops:
+ * bits 31..30 = type, bits 29..0 = length.  `:0` ops are dropped (they change nothing,
+ * pafreport.cpp:541-546).  Literal bytes go to a side array, upper-cased:
+ *   SUB: 2 bytes {target base, query base}   ('*tq', pafreport.cpp:547-578)
+ *   INS: len bytes (target-only bases)        ('-acg', pafreport.cpp:579-601 -> event 'I')
+ *   DEL: none (bases are taken from the query) ('+acg', pafreport.cpp:602-619 -> event 'D') */
+#define PW_OP_MATCH 0u
+#define PW_OP_SUB 1u
+#define PW_OP_INS 2u
+#define PW_OP_DEL 3u
+#define PW_OP_TYPE(w) ((uint32_t)(w) >> 30)
+#define PW_OP_LEN(w) ((uint32_t)(w)&0x3FFFFFFFu)
+#define PW_OP(type, len) (((uint32_t)(type) << 30) | ((uint32_t)(len)&0x3FFFFFFFu))
+
+/* One PAF record (= one PAFAlignment, pafreport.cpp:134-158), 32 bytes, device-resident. */
+typedef struct pw_aln_desc {
+  uint32_t op_begin;   /* first op in ops[] */
+  uint32_t n_ops;      /* ops of this record */
+  uint32_t lit_begin;  /* first literal byte in lits[] */
+  uint32_t ref;        /* bits 0..30 query index; bit 31 = reverse strand ('-') */
+  int32_t offset;      /* start on the aligned-strand query (pafreport.cpp:486-490) */
+  int32_t t_len;       /* tseq length implied by the cs string */
+  uint64_t text_begin; /* byte offset of this record's report slot in text[] */
+} pw_aln_desc;
+#define PW_REF_REVERSE 0x80000000u
+
+/* Per-record result written by pw_report_events, 32 bytes. */
+typedef struct pw_aln_result {
+  uint64_t text_off; /* first byte of the event lines in text[] */
+  uint32_t text_len; /* bytes of event lines (header excluded) */
+  uint32_t n_events; /* TDiffInfo records after S-merging */
+  int32_t err;       /* PW_REC_* */
+  int32_t err_a;     /* MISMATCH: q_pos          MODSEQ: modseq index */
+  int32_t err_b;     /* MISMATCH: query char     MODSEQ: evtsub index */
+  int32_t err_c;     /* MISMATCH: aligned-strand query char; MODSEQ: output line index */
+} pw_aln_result;
+
+#define PW_REC_OK 0
+#define PW_REC_MISMATCH 1 /* "Error: base mismatch ..." (pafreport.cpp:551-554) */
+#define PW_REC_MODSEQ 2   /* "Error: modseq[%d] not matching ..." (pafreport.cpp:812-813) */
+
+/* Arguments of pw_report_events (all pointers are device pointers). */
+typedef struct pw_report_args {
+  const pw_aln_desc* desc;  /* [n_alns] */
+  const uint32_t* ops;      /* packed ops */
+  const uint8_t* lits;      /* literal bytes */
+  const uint8_t* qseq;      /* forward upper-case query sequences, concatenated */
+  const uint64_t* qoff;     /* [n_queries] start of each query in qseq */
+  const int32_t* qlen;      /* [n_queries] */
+  const int32_t* next_stop; /* [sum qlen] from pw_stop_table_build; may be NULL if skip_codan */
+  uint8_t* text;            /* report slots, text_total bytes */
+  pw_aln_result* results;   /* [n_alns] */
+  uint64_t text_total;      /* end of the last slot */
+  uint32_t n_alns;
+  uint32_t skip_codan;      /* 1 = no codon impact column (pafreport.cpp:259-262, 915) */
+} pw_report_args;
+
+/* ---------------------------------------------------------------- device entry points */
+
+/* Replaces PAFAlignment::PAFAlignment (decode, pafreport.cpp:477-643) +
+ * PAFAlignment::printDiffInfo's event loop (classify, codon, format; pafreport.cpp:893-954)
+ * for a whole batch of records: one 64-lane wavefront per record. */
+int pw_report_events(const pw_report_args* args, void* stream);
+
+/* Per-query stop-codon lookahead used by the codon pass (replaces the forward scan of
+ * predictImpact, pafreport.cpp:854-870): next_stop[off+j] = smallest k >= j, k = j mod 3,
+ * k+2 < len, translateCodon(q+k) == '.', else INT32_MAX. */
+int pw_stop_table_build(const uint8_t* qseq, const uint64_t* qoff, const int32_t* qlen, uint32_t n_queries,
+                        int32_t* next_stop, void* stream);
+
+/* ---------------------------------------------------------------- GapAssem column consensus
+ * Packed MSA layout (GASeq rows, GapAssem.h:35-138): row r has its bases in
+ * seq[row_off[r] .. +row_len[r]) and the int16 gaps before each base (GASeq::ofs) at the same
+ * indices; col0[r] = offset - minoffset (GapAssem.cpp:568); clip_l/clip_r are the clip lengths
+ * already oriented by revcompl (GapAssem.cpp:557-564).  Rows are cut into 256-base chunks;
+ * pw_msa_slots() assigns each row ceil(len/256)+1 slots (the last one is the row's end). */
+typedef struct pw_msa_args {
+  const uint8_t* seq;       /* bases of all rows */
+  const int16_t* ofs;       /* gaps before each base */
+  const uint64_t* row_off;  /* [n_rows] first base of each row */
+  const int32_t* row_len;   /* [n_rows] */
+  const int32_t* col0;      /* [n_rows] offset - minoffset */
+  const int32_t* clip_l;    /* [n_rows] oriented left clip */
+  const int32_t* clip_r;    /* [n_rows] oriented right clip */
+  const int64_t* slot_base; /* [n_rows + 1] from pw_msa_slots */
+  int32_t* scratch;         /* [2 * n_slots] */
+  int32_t* counts;          /* [n_cols][6] A,C,G,T,N,- (GAlnColumn::counts order) */
+  uint8_t* consensus;       /* [n_cols] bestChar() per column ('-' for gap), 0 = no coverage */
+  int32_t* minmax;          /* [4]: mincol, maxcol, first out-of-range row, first zero column */
+  uint64_t n_slots;
+  uint32_t n_rows;
+  int32_t n_cols;           /* GSeqAlign::length */
+} pw_msa_args;
+
+/* Host helper: fills slot_base[n_rows + 1], returns n_slots. */
+uint64_t pw_msa_slots(const int32_t* row_len_host, uint32_t n_rows, int64_t* slot_base_host);
+
+/* Replaces GSeqAlign::buildMSA -> GASeq::toMSA -> GAlnColumn::addNuc/addGap and
+ * GAlnColumn::bestChar (GapAssem.cpp:551-591, 1048-1069, 1088-1106; GapAssem.h:295-337).
+ * minmax: INT_MAX / -1 sentinels when nothing is set. */
+int pw_msa_columns(const pw_msa_args* args, void* stream);
+
+/* ---------------------------------------------------------------- host pre-pass + CLI */
+
+/* Pack one cs string (CPU pre-pass).  offset/qlen/reverse locate it on the query.  Appends
+ * to caller arrays (capacity in *_cap, counts in/out in *_n).  Returns 0, or a PW_CS_* code
+ * with *err_pos = byte offset in cs where the reference would stop (pafreport.cpp:536-626). */
+#define PW_CS_OK 0
+#define PW_CS_PARSE 1     /* CS_ERROR (pafreport.cpp:542) */
+#define PW_CS_SPLICED 2   /* '~' (pafreport.cpp:620-622) */
+#define PW_CS_UNHANDLED 3 /* unknown op char (pafreport.cpp:623-624) */
+#define PW_CS_EMPTY 4     /* zero-length indel */
+#define PW_CS_BOUNDS 5    /* reads past the query */
+#define PW_CS_NOSPACE 6   /* caller arrays too small */
+typedef struct pw_cs_totals {
+  int32_t q_total, t_total; /* qpos / tpos after the last packed op */
+  uint32_t n_ops, n_lits;   /* appended */
+  uint32_t n_events_max;    /* upper bound of events (indels + substitutions) */
+  uint64_t text_bound;      /* upper bound of report bytes for these events */
+} pw_cs_totals;
+int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap, uint8_t* lits,
+               size_t lits_cap, pw_cs_totals* totals, int32_t* err_pos);
+
+/* The `pafreport` CLI (pafreport.cpp:175-460) on the HIP path; returns the process exit code
+ * the reference would produce (it prints exactly what the reference prints). */
+int pw_pafreport_main(int argc, char** argv);
+
+/* Host batch (the CLI's pre-pass), exposed so bench.py / tests can stage a batch on the
+ * device themselves.  Array pointers stay valid until pw_batch_free. */
+typedef struct pw_batch pw_batch;
+typedef struct pw_batch_view {
+  const pw_aln_desc* desc;
+  const uint32_t* ops;
+  const uint8_t* lits;
+  const uint8_t* qseq;
+  const uint64_t* qoff;
+  const int32_t* qlen;
+  uint64_t n_alns, n_ops, n_lits, qseq_len, n_queries, text_total, n_events_max;
+  uint64_t alg_bytes_in; /* algorithmic input bytes of one pass */
+  uint32_t skip_codan;
+} pw_batch_view;
+/* flags: bit0 = -G, bit1 = -F, bit2 = -C, bit3 = -N (same defaults as the CLI) */
+pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uint32_t flags, char* errbuf, size_t errlen);
+int pw_batch_view_get(const pw_batch* b, pw_batch_view* out);
+/* Render the report (headers + event text) for results of a finished batch into `path`. */
+int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
+                          const char* path);
+void pw_batch_free(pw_batch* b);
+
+const char* pw_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PWASM_AMD_H */
