@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""bench.py — pafreport hot path on MI355X: cs-events classified per second.
+
+A "step" = one pass of the hot path over one batch already resident in HBM: the next-stop
+table build (pw_stop_table_build) + the fused decode/classify/codon/render kernel
+(pw_report_events) over every record of the batch.  At N=1 the batch is BASELINE.json
+configs[1] (cfg2: 100k synthetic minimap2-style records, 1,000 CDS of 1-5 kb, ~1% ONT-style
+errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard (different
+seed = different target genomes; weak scaling, no data-path collective); the timed region is
+bracketed by barrier + synchronize, the max over ranks is reported.
+
+Also reported (rank 0): roofline of the dominant kernel (algorithmic bytes / its average HIP-
+event duration vs 8 TB/s) and the CPU baseline: the single-threaded oracle restatement
+(oracle/pafreport_oracle, kind "port") on a bounded sample of the same workload, 1 core.
+"""
+import argparse
+import json
+import os
+import pathlib
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (profiles/*.json)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pwasm_amd as pw
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    dev_name = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    # ---- data: this rank's shard (synthetic, seeded; generated outside the timed region)
+    tmp = tempfile.mkdtemp(prefix=f"pwbench{rank}_")
+    fa, paf = os.path.join(tmp, "q.fa"), os.path.join(tmp, "a.paf")
+    seed = 2 + 1000 * rank if args.config == 2 else args.config + 1000 * rank
+    t0 = time.time()
+    subprocess.run([str(REPO / "synth/build/pwsynth"), "paf", "--config", str(args.config), "--scale",
+                    str(args.scale), "--seed", str(seed), "--fa", fa, "--paf", paf], check=True,
+                   stderr=subprocess.DEVNULL)
+    flags = pw.FLAG_G | pw.FLAG_C if args.config in (1, 2, 3) else 0
+    batch = pw.HostBatch(fa, paf, flags)
+    v = batch.view
+    dev = pw.stage_batch(batch, dev_name)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] staged {v.n_alns} records, {v.n_ops} ops, {v.n_lits} literal bytes "
+        f"({time.time() - t0:.1f}s host prep)")
+
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def step(ev=None):
+        if not v.skip_codan:
+            rc = pw.lib().pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                              int(v.n_queries), dev["next_stop"].data_ptr(), sp)
+            assert rc == 0
+        a = pw.ReportArgs()
+        a.desc, a.ops, a.lits = dev["desc"].data_ptr(), dev["ops"].data_ptr(), dev["lits"].data_ptr()
+        a.qseq, a.qoff, a.qlen = dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr()
+        a.next_stop = 0 if v.skip_codan else dev["next_stop"].data_ptr()
+        a.text, a.results = dev["text"].data_ptr(), dev["results"].data_ptr()
+        a.text_total, a.n_alns, a.skip_codan = int(v.text_total), int(v.n_alns), int(v.skip_codan)
+        if ev is not None:
+            ev[0].record(stream)
+        rc = pw.lib().pw_report_events(pw.ctypes.byref(a), sp)
+        assert rc == 0
+        if ev is not None:
+            ev[1].record(stream)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    res = dev["results"].cpu().numpy().view(np.uint8).reshape(-1, 32)
+    n_events = int(res[:, 12:16].copy().view(np.uint32).sum())
+    errs = int((res[:, 16:20].copy().view(np.int32) != 0).sum())
+    text_bytes = int(res[:, 8:12].copy().view(np.uint32).astype(np.int64).sum())
+    assert errs == 0, f"{errs} records reported errors"
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    t_el = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    tot_events = n_events
+    max_el = t_el
+    if world > 1:
+        t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        max_el = float(t.item())
+        e = torch.tensor([n_events], dtype=torch.float64, device=dev_name)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        tot_events = int(e.item())
+
+    if rank == 0:
+        # algorithmic bytes of one launch: inputs + report text written
+        alg_bytes = int(v.alg_bytes_in) + text_bytes
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if args.traffic_json and os.path.exists(args.traffic_json):
+            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(fa, paf, args.cpu_sample, tmp)
+        out = {
+            "metric": "cs-events classified/sec (whole node) + achieved HBM GB/s, 1/2/4/8 MI355X",
+            "value": tot_events * args.steps / max_el,
+            "unit": "events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": max_el * 1000.0 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (pwsynth, seeded minimap2-style PAF with cs/cg tags)",
+            "config": {"workload": f"cfg{args.config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
+                                   f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU",
+                       "records_per_gpu": int(v.n_alns), "events_per_gpu": n_events, "scale": args.scale,
+                       "parallelism": f"shard-by-target x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "pw::report_kernel", "kernel_ms": round(kern_ms, 4),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(fa, paf, n_rec, tmp):
+    """Time the single-threaded oracle (C restatement of pafreport) on the first n_rec records."""
+    sample = os.path.join(tmp, "sample.paf")
+    with open(paf) as f, open(sample, "w") as g:
+        for i, line in enumerate(f):
+            if i >= n_rec:
+                break
+            g.write(line)
+    oracle = str(REPO / "oracle/build/pafreport_oracle")
+    outp = os.path.join(tmp, "cpu.txt")
+    cpu0 = sorted(os.sched_getaffinity(0))[0]
+    pin = ["taskset", "-c", str(cpu0)] if subprocess.run(["which", "taskset"], stdout=subprocess.DEVNULL).returncode == 0 else []
+    t0 = time.perf_counter()
+    subprocess.run(pin + [oracle, "-G", "-C", "-r", fa, sample, "-o", outp], check=True)
+    el = time.perf_counter() - t0
+    lines = hdr = 0
+    with open(outp, "rb") as f:
+        for line in f:
+            lines += 1
+            hdr += line.startswith(b">")
+    ev = lines - hdr
+    return {"value": ev / el, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": f"first {n_rec} records of the same batch ({ev} events, {el:.1f} s, pinned to cpu {cpu0})"}
+
+
+if __name__ == "__main__":
+    main()

@@ -153,6 +153,12 @@ typedef struct pw_cs_totals {
 int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap, uint8_t* lits,
                size_t lits_cap, pw_cs_totals* totals, int32_t* err_pos);
 
+/* GSeqAlign::refineMSA consensus of a packed layout file (PWL1, tests/pwl_format.md) on the HIP
+ * path, written as a PWC1 result; flags bit0 = MSAColumns::removeConsGaps, bit1 = disable
+ * MSAColumns::refineClipping.  Returns the reference's exit code (0, 1 bad index, 5 zero
+ * coverage) or 2 for I/O / device errors. */
+int pw_gapassem_run(const char* layout_path, const char* out_path, uint32_t flags);
+
 /* The `pafreport` CLI (pafreport.cpp:175-460) on the HIP path; returns the process exit code
  * the reference would produce (it prints exactly what the reference prints). */
 int pw_pafreport_main(int argc, char** argv);

@@ -1,0 +1,218 @@
+"""pwasm_amd — MI355X-native pafreport hot path (gpertea/pwasm), Python side.
+
+The product is native: libpwasm_amd.so (HIP kernels for gfx950 + C++ host pre-pass) and the
+`pafreport` / `gapassem_consensus` executables built on it.  This module only binds the C-ABI
+(include/pwasm_amd.h) with ctypes so bench.py and the tests can stage batches in device memory
+owned by PyTorch and launch the kernels on PyTorch's stream.  There is no Python or CPU
+implementation of the hot path here: if the library is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+import subprocess
+
+ROOT = pathlib.Path(__file__).resolve().parent
+REPO = ROOT.parent
+LIB_PATH = ROOT / "lib" / "libpwasm_amd.so"
+CLI_PATH = ROOT / "bin" / "pafreport"
+GA_CLI_PATH = ROOT / "bin" / "gapassem_consensus"
+
+PW_OP_MATCH, PW_OP_SUB, PW_OP_INS, PW_OP_DEL = 0, 1, 2, 3
+PW_CS_OK, PW_CS_PARSE, PW_CS_SPLICED, PW_CS_UNHANDLED, PW_CS_EMPTY, PW_CS_BOUNDS, PW_CS_NOSPACE = range(7)
+PW_REC_OK, PW_REC_MISMATCH, PW_REC_MODSEQ = 0, 1, 2
+
+# pafreport mode flags for pw_batch_from_files (same meaning as -G/-F/-C/-N)
+FLAG_G, FLAG_F, FLAG_C, FLAG_N = 1, 2, 4, 8
+
+
+class AlnDesc(ctypes.Structure):
+    _fields_ = [("op_begin", ctypes.c_uint32), ("n_ops", ctypes.c_uint32), ("lit_begin", ctypes.c_uint32),
+                ("ref", ctypes.c_uint32), ("offset", ctypes.c_int32), ("t_len", ctypes.c_int32),
+                ("text_begin", ctypes.c_uint64)]
+
+
+class AlnResult(ctypes.Structure):
+    _fields_ = [("text_off", ctypes.c_uint64), ("text_len", ctypes.c_uint32), ("n_events", ctypes.c_uint32),
+                ("err", ctypes.c_int32), ("err_a", ctypes.c_int32), ("err_b", ctypes.c_int32),
+                ("err_c", ctypes.c_int32)]
+
+
+class ReportArgs(ctypes.Structure):
+    _fields_ = [("desc", ctypes.c_void_p), ("ops", ctypes.c_void_p), ("lits", ctypes.c_void_p),
+                ("qseq", ctypes.c_void_p), ("qoff", ctypes.c_void_p), ("qlen", ctypes.c_void_p),
+                ("next_stop", ctypes.c_void_p), ("text", ctypes.c_void_p), ("results", ctypes.c_void_p),
+                ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32)]
+
+
+class CsTotals(ctypes.Structure):
+    _fields_ = [("q_total", ctypes.c_int32), ("t_total", ctypes.c_int32), ("n_ops", ctypes.c_uint32),
+                ("n_lits", ctypes.c_uint32), ("n_events_max", ctypes.c_uint32), ("text_bound", ctypes.c_uint64)]
+
+
+class BatchView(ctypes.Structure):
+    _fields_ = [("desc", ctypes.c_void_p), ("ops", ctypes.c_void_p), ("lits", ctypes.c_void_p),
+                ("qseq", ctypes.c_void_p), ("qoff", ctypes.c_void_p), ("qlen", ctypes.c_void_p),
+                ("n_alns", ctypes.c_uint64), ("n_ops", ctypes.c_uint64), ("n_lits", ctypes.c_uint64),
+                ("qseq_len", ctypes.c_uint64), ("n_queries", ctypes.c_uint64), ("text_total", ctypes.c_uint64),
+                ("n_events_max", ctypes.c_uint64), ("alg_bytes_in", ctypes.c_uint64),
+                ("skip_codan", ctypes.c_uint32)]
+
+
+class MsaArgs(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_void_p), ("ofs", ctypes.c_void_p), ("row_off", ctypes.c_void_p),
+                ("row_len", ctypes.c_void_p), ("col0", ctypes.c_void_p), ("clip_l", ctypes.c_void_p),
+                ("clip_r", ctypes.c_void_p), ("slot_base", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
+                ("counts", ctypes.c_void_p), ("consensus", ctypes.c_void_p), ("minmax", ctypes.c_void_p),
+                ("n_slots", ctypes.c_uint64), ("n_rows", ctypes.c_uint32), ("n_cols", ctypes.c_int32)]
+
+
+# every function declared in include/pwasm_amd.h (tests check the export table against it)
+_SIGS = {
+    "pw_report_events": (ctypes.c_int, [ctypes.POINTER(ReportArgs), ctypes.c_void_p]),
+    "pw_stop_table_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]),
+    "pw_msa_slots": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "pw_msa_columns": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
+    "pw_pack_cs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),
+                                  ctypes.POINTER(ctypes.c_int32)]),
+    "pw_pafreport_main": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]),
+    "pw_batch_from_files": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                              ctypes.c_size_t]),
+    "pw_batch_view_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatchView)]),
+    "pw_batch_write_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
+    "pw_batch_free": (None, [ctypes.c_void_p]),
+    "pw_version": (ctypes.c_char_p, []),
+    "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
+}
+
+_lib = None
+
+
+def build(jobs: int = 8) -> None:
+    """Compile the HIP library, CLIs, oracle and synth tool in-tree (make)."""
+    subprocess.run(["make", f"-j{jobs}"], cwd=str(REPO), check=True)
+
+
+def lib() -> ctypes.CDLL:
+    """The native library; raises if it was not built (there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"pwasm_amd: native library missing ({LIB_PATH}); run `make` / __graft_entry__.build()")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def pack_cs(cs: str, offset: int, qlen: int):
+    """CPU pre-pass on one cs string -> (rc, ops list, literal bytes, totals, err_pos)."""
+    L = lib()
+    n = len(cs) + 1
+    ops = (ctypes.c_uint32 * n)()
+    lits = (ctypes.c_uint8 * n)()
+    tot = CsTotals()
+    epos = ctypes.c_int32(0)
+    rc = L.pw_pack_cs(cs.encode(), offset, qlen, ops, n, lits, n, ctypes.byref(tot), ctypes.byref(epos))
+    return rc, list(ops[:tot.n_ops]), bytes(lits[:tot.n_lits]), tot, epos.value
+
+
+class HostBatch:
+    """A PAF batch packed by the C++ pre-pass (pw_batch_from_files), arrays viewable as numpy."""
+
+    def __init__(self, fasta: str, paf: str, flags: int = 0):
+        L = lib()
+        err = ctypes.create_string_buffer(4096)
+        h = L.pw_batch_from_files(fasta.encode(), paf.encode(), flags, err, 4096)
+        if not h:
+            raise RuntimeError("pw_batch_from_files: " + err.value.decode(errors="replace"))
+        self._h = h
+        self.view = BatchView()
+        if L.pw_batch_view_get(h, ctypes.byref(self.view)) != 0:
+            raise RuntimeError("pw_batch_view_get failed")
+
+    def array(self, name: str):
+        import numpy as np
+        v = self.view
+        spec = {"desc": (v.desc, v.n_alns * ctypes.sizeof(AlnDesc), np.uint8),
+                "ops": (v.ops, v.n_ops, np.uint32), "lits": (v.lits, v.n_lits, np.uint8),
+                "qseq": (v.qseq, v.qseq_len, np.uint8), "qoff": (v.qoff, v.n_queries, np.uint64),
+                "qlen": (v.qlen, v.n_queries, np.int32)}[name]
+        ptr, n, dt = spec
+        if n == 0:
+            return np.zeros(0, dtype=dt)
+        ct = np.ctypeslib.as_ctypes_type(dt)
+        buf = (ct * int(n)).from_address(int(ptr))
+        return np.ctypeslib.as_array(buf).copy()
+
+    def write_report(self, text_host, results_host, path: str) -> int:
+        """Headers + event text for a finished batch (numpy arrays on the host)."""
+        return lib().pw_batch_write_report(self._h, text_host.ctypes.data, results_host.ctypes.data, path.encode())
+
+    def close(self):
+        if self._h:
+            lib().pw_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
+    """Launch pw_stop_table_build (unless -F/-N) + pw_report_events on device tensors in `dev`."""
+    L = lib()
+    v = batch.view
+    if not v.skip_codan:
+        rc = L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                   int(v.n_queries), dev["next_stop"].data_ptr(), stream_ptr)
+        if rc != 0:
+            raise RuntimeError(f"pw_stop_table_build: {rc}")
+    a = ReportArgs()
+    a.desc = dev["desc"].data_ptr()
+    a.ops = dev["ops"].data_ptr()
+    a.lits = dev["lits"].data_ptr()
+    a.qseq = dev["qseq"].data_ptr()
+    a.qoff = dev["qoff"].data_ptr()
+    a.qlen = dev["qlen"].data_ptr()
+    a.next_stop = 0 if v.skip_codan else dev["next_stop"].data_ptr()
+    a.text = dev["text"].data_ptr()
+    a.results = dev["results"].data_ptr()
+    a.text_total = int(v.text_total)
+    a.n_alns = int(v.n_alns)
+    a.skip_codan = int(v.skip_codan)
+    rc = L.pw_report_events(ctypes.byref(a), stream_ptr)
+    if rc != 0:
+        raise RuntimeError(f"pw_report_events: {rc}")
+
+
+def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
+    """Copy a packed batch into device tensors (inputs resident in HBM) + output buffers."""
+    import numpy as np
+    import torch
+    v = batch.view
+    dev = {}
+    for name in ("desc", "ops", "lits", "qseq", "qoff", "qlen"):
+        arr = batch.array(name)
+        if arr.size == 0:
+            arr = np.zeros(1, dtype=arr.dtype)
+        if arr.dtype == np.uint64:  # torch only needs the bytes
+            arr = arr.view(np.uint8)
+        dev[name] = torch.from_numpy(arr).to(device)
+    dev["next_stop"] = torch.empty(max(int(v.qseq_len), 1), dtype=torch.int32, device=device)
+    dev["text"] = torch.empty(max(int(v.text_total), 1), dtype=torch.uint8, device=device)
+    dev["results"] = torch.empty(max(int(v.n_alns), 1) * ctypes.sizeof(AlnResult), dtype=torch.uint8,
+                                 device=device)
+    return dev
+
+
+def version() -> str:
+    return lib().pw_version().decode()

@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Writes the hand-derived known-answer tests (KATs) under tests/golden/kat/<name>/.
+
+The reference (gpertea/pwasm pafreport) cannot be built in this image (gclib is absent), so
+every expected output below was derived BY HAND from the reference source and is written
+here as a literal.  Derivations (line refs into /root/reference/pafreport.cpp):
+  kat1_forward  - SURVEY.md §8(a) KAT: S merge-free substitution (:547-573), I event (:579-601),
+                  setTContext (:120-128), getRefContext (:721-733), predictImpact S/I (:801-883).
+  kat2_reverse  - '-' strand: offset = r_len - r_alnend (:488-490), D/I rloc transforms
+                  (:597,615), S kept on the aligned strand then flipped (:634-640),
+                  tloc = |tseq| - tloc (:633), revcomp tctx (:631), tdiffs.Reverse (:643),
+                  merged S run "GC"/"TA" (:556-560), getRefContext end-of-query quirk (:726-729).
+  kat3_status   - homopolymer (:735-748), motif list order (:41,751-763), AA0 quirk for
+                  rloc<3 (:829), stop introduced by S (:834-837), "[15]" + abbreviated tctx
+                  (:920-934), aa4 containing '.', in-frame deletion scanned to the natural stop,
+                  rlabel = qname with 2 FASTA records (:366-379), duplicate q~t warning
+                  (:319-333), self alignment skipped (:314-317), '#' comment (:304).
+  kat4_fullgenome - -F: rlabel "q:start-end" (:368-372), codon analysis skipped (:259,915)
+                  so each line ends with a tab.
+  err_*         - the reference's error messages (format strings copied from the source
+                  lines cited in each case), exit code 1, and report lines printed before it.
+Each case dir holds: q.fa, in.paf, args.json ({"args": [...], "rc": N}), stdout, stderr.
+Run: python3 tests/golden/make_kats.py   (idempotent)
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "kat")
+
+CDS = "ATGAAACCCGGGTTTAAACCCGGGTTTTAA"
+FA1 = ">cds\n" + CDS + "\n"
+G1 = "ATGGCCTGGAAAAAGATCCCTACGGTACTTGCATAA"
+FA3 = ">g1 first gene\n" + G1 + "\n>g2\n" + CDS + "\n"
+
+USAGE = (
+    "Usage:\n"
+    " pafreport <paf_with_cg_cs> -r <refseq.fa> [-s <summary.txt>]\n"
+    "    [-o <diff_report.dfa>][-w <outfile.mfa>] [-G|-F|-C|-N]\n"
+    "    \n"
+    "   <paf_with_cg_cs> is the input PAF file with high quality query sequence(s)\n"
+    "      aligned to many target sequences using minimap2 --cs\n"
+    "   -r provide the fasta file with query sequence(s) (required)\n"
+    "   -o write difference data for each alignment into <diff_report.dfa>\n"
+    "   -s write event summary counts into <summary.txt>\n"
+    "   -w write MSA as multifasta into <outfile.mfa>\n"
+    "   -G gene CDS analysis mode (default for query<100K; assumes -C)\n"
+    "   -F full genome alignment mode (default for query>100Kb; assumes -N)\n"
+    "   -C perform codon impact analysis\n"
+    "   -N skip codon impact analysis\n"
+)
+
+
+def paf(*cols):
+    return "\t".join(str(c) for c in cols) + "\n"
+
+
+K1 = paf("cds", 30, 0, 30, "+", "asm1", 100, 10, 41, 29, 31, 60, "NM:i:2", "AS:i:50", "cg:Z:15M1D15M",
+         "cs:Z::4*ga:10-t:15")
+K1_OUT = (">asm1:10-41+ coverage:100.00 score=50 edit_distance=2\n"
+          "S\t5\t2(K)\tA:G\t5\tATGAgACCCG\tATGAAACCC\t[unknown]\tAA2|K:R\n"
+          "I\t16\t6(K)\t:T\t16\tGGTTTtAAACC\tGTTTAAACC\t[unknown]\tpremature stop at AA6\n")
+
+K2 = paf("cds", 30, 0, 30, "-", "asm2", 500, 100, 131, 25, 33, 60, "NM:i:5", "AS:i:40", "cg:Z:9M1I9M2D11M",
+         "cs:Z::3*ga:5+g:4*gt*ca:3-aa:11")
+K2_OUT = (">asm2:100-131- coverage:100.00 score=40 edit_distance=5\n"
+          "I\t12\t4(G)\t:TT\t14\tCCCGGttGTTgc\tCCGGGTTTA\t[unknown]\tframe shift GFKP+:GCLN+\n"
+          "S\t15\t5(F)\tTA:GC\t19\ttGTTgcAACCG\tGGTTTAAAC\t[unknown]\tAA5|F:L, AA6|K:Q\n"
+          "D\t21\t7(P)\tC:\t23\tcAACCGGGTT\tAACCCGGGT\t[unknown]\tframe shift PGF+:PGF+\n"
+          "S\t27\t9(F)\tT:C\t29\tGGGTTcTAA\tGGGTTTTAA\t[unknown]\tsynonymous\n")
+
+K3A = paf("g1", 36, 0, 36, "+", "tA", 1000, 200, 251, 30, 51, 60, "NM:i:19", "AS:i:10",
+          "cg:Z:11M1D5M1I7M15D12M", "cs:Z::1*ct:6*ag:2-a:5+t:7-acgtacgtacgtacg:12")
+K3 = ("# comment\n" + K3A +
+      paf("g1", 36, 0, 36, "+", "g1", 36, 0, 36, 36, 36, 60, "NM:i:0", "AS:i:72", "cg:Z:36M", "cs:Z::36") +
+      K3A +
+      paf("g2", 30, 0, 30, "+", "tB", 800, 10, 37, 24, 30, 60, "NM:i:3", "AS:i:20", "cg:Z:6M3I21M",
+          "cs:Z::6+ccc:21") +
+      paf("g2", 30, 10, 25, "+", "tC", 100, 0, 15, 15, 15, 60, "NM:i:0", "AS:i:30", "cg:Z:15M", "cs:Z::15"))
+K3_OUT = (">g1--tA:200-251+ coverage:100.00 score=10 edit_distance=19\n"
+          "S\t2\t1(M)\tT:C\t2\tAcGGCCT\tATGGCCTGG\tmotif CCTGG\tAA0|M:T\n"
+          "S\t9\t3(W)\tG:A\t9\tGCCTGaAAaAA\tCCTGGAAAA\tmotif CCTGG\tAA3|W:.|premature stop at AA3\n"
+          "I\t12\t4(K)\t:A\t12\tTGaAAaAAAGA\tGGAAAAAGA\thomopolymer\tframe shift KKIP+:KKDP+\n"
+          "D\t17\t6(I)\tT:\t18\tAAAGACCCTA\tAAGATCCCT\tmotif GATC\tframe shift IPTV+:TLRY+\n"
+          "I\t25\t9(V)\t:[15]\t25\tCTACG[15]GTACT\tTACGGTACT\tmotif GTAC\tpremature stop at AA17\n"
+          ">g2--tB:10-37+ coverage:100.00 score=20 edit_distance=3\n"
+          "D\t7\t3(P)\tCCC:\t7\tTGAAAGGGTT\tGAAACCCGG\t[unknown]\tpremature stop at AA9\n"
+          ">g2--tC:0-15+ coverage:50.00 score=30 edit_distance=0\n")
+K3_ERR = "Warning: alignment g1 to tA already seen, ignoring \n"
+
+K4_OUT = (">cds:0-30--asm1:10-41+ coverage:100.00 score=50 edit_distance=2\n"
+          "S\t5\t2(K)\tA:G\t5\tATGAgACCCG\tATGAAACCC\t[unknown]\t\n"
+          "I\t16\t6(K)\t:T\t16\tGGTTTtAAACC\tGTTTAAACC\t[unknown]\t\n")
+
+
+def line(s):
+    return s.rstrip("\n")
+
+
+CASES = {
+    "kat1_forward": (FA1, K1, ["-r", "q.fa", "in.paf"], 0, K1_OUT, ""),
+    "kat1_outfile": (FA1, K1, ["in.paf", "-r", "q.fa", "-o", "out.txt"], 0, "", ""),
+    "kat2_reverse": (FA1, K2, ["-r", "q.fa", "in.paf"], 0, K2_OUT, ""),
+    "kat3_status": (FA3, K3, ["-r", "q.fa", "in.paf"], 0, K3_OUT, K3_ERR),
+    "kat4_fullgenome": (FA1, K1, ["-F", "-r", "q.fa", "in.paf"], 0, K4_OUT, ""),
+    "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
+                       K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
+    # pafreport.cpp:551-553 base check; records before the failing one are already reported
+    "err_mismatch": (FA1, K1 + K1.replace("asm1", "asm9").replace("*ga", "*gc"), ["-r", "q.fa", "in.paf"], 1,
+                     K1_OUT,
+                     "Error: base mismatch C != qstr[4] (A) at line\n" +
+                     line(K1.replace("asm1", "asm9").replace("*ga", "*gc")) + "\n"),
+    # :620-622
+    "err_spliced": (FA1, K1.replace(":4*ga:10-t:15", ":4~gt10ag:26"), ["-r", "q.fa", "in.paf"], 1, "",
+                    "Error: spliced alignments not supported! at line:\n" +
+                    line(K1.replace(":4*ga:10-t:15", ":4~gt10ag:26")) + "\n"),
+    # :542 CS_ERROR (:474) with the cs position string
+    "err_cs_parse": (FA1, K1.replace(":4*ga:10-t:15", ":4*ga:x10-t:15"), ["-r", "q.fa", "in.paf"], 1, "",
+                     "Error parsing cs string from line: " + line(K1.replace(":4*ga:10-t:15", ":4*ga:x10-t:15")) +
+                     " (cs position: x10-t:15)\n"),
+    # :623-624
+    "err_cs_op": (FA1, K1.replace(":4*ga:10-t:15", ":4*ga:10=t:15"), ["-r", "q.fa", "in.paf"], 1, "",
+                  "Error: unhandled event at t:15 in cs, line:\n" +
+                  line(K1.replace(":4*ga:10-t:15", ":4*ga:10=t:15")) + "\n"),
+    # :715-716
+    "err_tlen": (FA1, K1.replace("\t10\t41\t", "\t10\t42\t"), ["-r", "q.fa", "in.paf"], 1, "",
+                 "Error: tseq alignment length mismatch (31 vs 32(42-10)) at line:" +
+                 line(K1.replace("\t10\t41\t", "\t10\t42\t")) + "\n"),
+    # :717-718 (cs/CIGAR consistent, PAF query span not)
+    "err_qlen": (FA1, K1.replace("cds\t30\t0\t30", "cds\t30\t0\t29"), ["-r", "q.fa", "in.paf"], 1, "",
+                 "Error: ref alignment length mismatch (30 vs 29-0) at line:" +
+                 line(K1.replace("cds\t30\t0\t30", "cds\t30\t0\t29")) + "\n"),
+    # :308-309
+    "err_fields": (FA1, K1 + "cds\t30\t0\t30\t+\n", ["-r", "q.fa", "in.paf"], 1, K1_OUT,
+                   "Error: invalid PAF fline (num. fields=5):\ncds\t30\t0\t30\t+\n"),
+    # :356-358
+    "err_rlen": (FA1, K1.replace("cds\t30\t", "cds\t31\t"), ["-r", "q.fa", "in.paf"], 1, "",
+                 "Error: ref seq len in this PAF line (31) differs from loaded sequence length(30)!\n" +
+                 line(K1.replace("cds\t30\t", "cds\t31\t")) + "\n"),
+    # :347
+    "err_noquery": (FA1, K1.replace("cds\t", "cdsX\t", 1), ["-r", "q.fa", "in.paf"], 1, "",
+                    "Error: could not retrieve sequence for cdsX !\n"),
+    # :711
+    "err_cigar_op": (FA1, K1.replace("15M1D15M", "15M1Z15M"), ["-r", "q.fa", "in.paf"], 1, "",
+                     "Error: unhandled cigar_op Z (len 1) in " + line(K1.replace("15M1D15M", "15M1Z15M")) + "\n"),
+    # :521 with a NULL position string
+    "err_nocigar": (FA1, K1.replace("cg:Z:15M1D15M", "xx:Z:15M1D15M"), ["-r", "q.fa", "in.paf"], 1, "",
+                    "Error parsing cigar string from line: " + line(K1.replace("cg:Z:15M1D15M", "xx:Z:15M1D15M")) +
+                    " (cigar position: (null))\n"),
+    # :675-679 soft clip warning, then the report
+    "warn_softclip": (FA1, K1.replace("cg:Z:15M1D15M", "cg:Z:2S13M3D15M"), ["-r", "q.fa", "in.paf"], 0,
+                      K1_OUT, "Warning: soft clipping shouldn't be found in this application!\n" +
+                      line(K1.replace("cg:Z:15M1D15M", "cg:Z:2S13M3D15M")) + "\n"),
+    # CLI (:177-197, 251-252)
+    "cli_no_r": (FA1, K1, ["in.paf"], 1, "", "Error: query FASTA file (-r) is required!\n"),
+    "cli_G_F": (FA1, K1, ["-G", "-F", "-r", "q.fa", "in.paf"], 1, "", USAGE + " Error: cannot use both -G and -F!\n"),
+    "cli_C_N": (FA1, K1, ["-C", "-N", "-r", "q.fa", "in.paf"], 1, "", USAGE + " Error: cannot use both -N and -C!\n"),
+    "cli_bad_opt": (FA1, K1, ["-h", "-r", "q.fa", "in.paf"], 1, "", USAGE + "\nInvalid argument: -h\n"),
+}
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    for name, (fa, pafs, args, rc, out, err) in CASES.items():
+        d = os.path.join(OUT, name)
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "q.fa"), "w") as f:
+            f.write(fa)
+        with open(os.path.join(d, "in.paf"), "w") as f:
+            f.write(pafs)
+        spec = {"args": args, "rc": rc}
+        if name == "kat1_outfile":
+            spec["outfile"] = "out.txt"
+            spec["outfile_expected"] = K1_OUT
+        with open(os.path.join(d, "args.json"), "w") as f:
+            json.dump(spec, f, indent=1)
+        with open(os.path.join(d, "stdout"), "w") as f:
+            f.write(out)
+        with open(os.path.join(d, "stderr"), "w") as f:
+            f.write(err)
+    print(f"wrote {len(CASES)} cases to {OUT}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+"""GPU parity: the HIP path (pwasm_amd/bin/pafreport -> libpwasm_amd.so kernels) against the
+oracle on the same inputs — byte-identical stdout, stderr and exit code.
+
+Inputs: the hand-derived KATs (tests/golden/kat), seeded synthetic PAF for every config shape
+ at sizes the oracle finishes in seconds, injected errors at random records,
+all -G/-F/-C/-N modes, the torch-stream batch API, and the GapAssem column consensus.
+Parity bar: bit-exact (integer/byte work only)."""
+import os
+import random
+import shutil
+import struct
+
+import numpy as np
+import pytest
+
+import pwasm_amd as pw
+from conftest import CLI, GA_CLI, GA_ORACLE, KAT_DIR, ORACLE, SYNTH, run, synth_paf
+from test_oracle_kat import read_pwc, run_case, write_pwl
+
+pytestmark = pytest.mark.gpu
+
+CASES = sorted(d for d in os.listdir(KAT_DIR) if os.path.isdir(KAT_DIR / d))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_kat_on_gpu(built, case, tmp_path):
+    run_case(CLI, case, tmp_path)
+
+
+def same(args, cwd=None, timeout=900):
+    """Run oracle and product with the same args; compare everything the reference prints."""
+    ro, oo, eo = run([ORACLE, *args], cwd=cwd, timeout=timeout)
+    rp, op, ep = run([CLI, *args], cwd=cwd, timeout=timeout)
+    assert rp == ro, (rp, ro, ep[-2000:], eo[-2000:])
+    if op != oo:
+        a, b = oo.decode(errors="replace").splitlines(), op.decode(errors="replace").splitlines()
+        for i, (x, y) in enumerate(zip(a, b)):
+            if x != y:
+                pytest.fail(f"first difference at line {i}:\noracle: {x!r}\nhip:    {y!r}")
+        pytest.fail(f"length differs: oracle {len(a)} lines, hip {len(b)} lines")
+    assert ep == eo
+    return oo
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
+def test_edge_mix(built, tmp_path, seed):
+    fa, paf = synth_paf(tmp_path, 0, seed=seed)
+    out = same(["-r", fa, paf])
+    assert out.count(b"\n") > 100
+
+
+@pytest.mark.parametrize("flags", [[], ["-C"], ["-N"], ["-G"], ["-F"], ["-G", "-C"], ["-F", "-C"]])
+def test_modes(built, tmp_path, flags):
+    fa, paf = synth_paf(tmp_path, 0, seed=11)
+    same([*flags, "-r", fa, paf])
+
+
+def test_cfg1_plumbing(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 1)
+    out = same(["-r", fa, paf])
+    assert out.count(b">") == 20
+
+
+def test_cfg2_subsample(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 2, scale=0.05)
+    same(["-G", "-C", "-r", fa, paf])
+
+
+def test_cfg3_subsample(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 3, scale=0.0004)
+    same(["-G", "-C", "-r", fa, paf])
+
+
+def test_cfg4_long_contigs_full_genome_mode(built, tmp_path):
+    # dense cs over long queries (auto -F: FASTA > 120 kB); contigs shortened so the oracle's
+    # O(L) per-event suffix copy (pafreport.cpp:908) stays within seconds
+    fa, paf = synth_paf(tmp_path, 4, extra=["--ncds", 2, "--len-min", 150000, "--len-max", 250000, "--recs", 3,
+                                            "--err", 0.02])
+    assert os.path.getsize(fa) > 120000
+    out = same(["-r", fa, paf])
+    assert out.count(b"\n") > 5000
+
+
+def test_long_indels_and_runs(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 0, seed=21, extra=["--longindel", 0.5, "--subrun", 0.6, "--err", 0.05])
+    same(["-r", fa, paf])
+
+
+def test_reverse_only_and_forward_only(built, tmp_path):
+    for rev in (0.0, 1.0):
+        fa, paf = synth_paf(tmp_path, 0, seed=31, extra=["--rev", rev])
+        same(["-r", fa, paf])
+
+
+def _inject(paf, tmp_path, kind, seed):
+    lines = open(paf).read().splitlines(keepends=True)
+    rng = random.Random(seed)
+    idx = [i for i, l in enumerate(lines) if not l.startswith("#") and "*" in l]
+    k = rng.choice(idx[len(idx) // 3:])
+    f = lines[k].rstrip("\n").split("\t")
+    cs = [i for i, x in enumerate(f) if x.startswith("cs:Z:")][0]
+    if kind == "mismatch":  # flip the query base of one '*' op
+        s = f[cs]
+        j = s.index("*", 5)
+        q = s[j + 2]
+        f[cs] = s[:j + 2] + ("c" if q != "c" else "g") + s[j + 3:]
+    elif kind == "bounds":
+        f[cs] = f[cs] + ":1000000"
+    elif kind == "cigar":
+        cg = [i for i, x in enumerate(f) if x.startswith("cg:Z:")][0]
+        f[cg] = f[cg] + "3Q"
+    lines[k] = "\t".join(f) + "\n"
+    out = os.path.join(tmp_path, f"inj_{kind}.paf")
+    open(out, "w").write("".join(lines))
+    return out
+
+
+@pytest.mark.parametrize("kind", ["mismatch", "bounds", "cigar"])
+def test_error_midway(built, tmp_path, kind):
+    fa, paf = synth_paf(tmp_path, 0, seed=41)
+    bad = _inject(paf, tmp_path, kind, seed=5)
+    same(["-r", fa, bad])
+
+
+def test_empty_and_comment_only_input(built, tmp_path):
+    fa, _ = synth_paf(tmp_path, 1)
+    p = tmp_path / "c.paf"
+    p.write_text("# nothing here\n")
+    same(["-r", fa, str(p)])
+    p2 = tmp_path / "e.paf"
+    p2.write_text("")
+    same(["-r", fa, str(p2)])
+
+
+def test_stdin_input(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 1)
+    import subprocess
+    a = subprocess.run([str(ORACLE), "-r", fa], stdin=open(paf), stdout=subprocess.PIPE).stdout
+    b = subprocess.run([str(CLI), "-r", fa], stdin=open(paf), stdout=subprocess.PIPE).stdout
+    assert a == b and len(a) > 0
+
+
+def test_batch_api_on_torch_stream(built, tmp_path):
+    """Stage a packed batch in torch device memory, launch on torch's stream, render the
+    report from the device results: must equal the CLI output."""
+    import torch
+    fa, paf = synth_paf(tmp_path, 0, seed=3)
+    b = pw.HostBatch(fa, paf, 0)
+    dev = pw.stage_batch(b, "cuda:0")
+    pw.run_report(b, dev, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    text = dev["text"].cpu().numpy()
+    res = dev["results"].cpu().numpy()
+    outp = str(tmp_path / "batch.txt")
+    rc = b.write_report(text, res, outp)
+    assert rc == 0
+    _, want, _ = run([ORACLE, "-r", fa, paf])
+    assert open(outp, "rb").read() == want
+    r = res.view(np.uint8).reshape(-1, 32)
+    n_events = r[:, 12:16].copy().view(np.uint32).sum()
+    assert n_events == want.count(b"\n") - want.count(b">")
+
+
+# ---------------------------------------------------------------- GapAssem consensus
+def ga_same(layout, tmp_path, extra=()):
+    ro, _, eo = run([GA_ORACLE, layout, tmp_path / "o.pwc", *extra])
+    rp, _, ep = run([GA_CLI, layout, tmp_path / "p.pwc", *extra])
+    assert rp == ro, (rp, ro, ep, eo)
+    assert ep == eo
+    if ro == 0:
+        assert open(tmp_path / "p.pwc", "rb").read() == open(tmp_path / "o.pwc", "rb").read()
+    return ro
+
+
+def test_gapassem_hand_layouts(built, tmp_path):
+    lay = tmp_path / "l.pwl"
+    write_pwl(lay, [(0, "ACGT", [0, 0, 1, 0], 0, 0, 0), (1, "CNGA", [0, 0, 1, 0], 0, 0, 0),
+                    (2, "-G", [0, 0], 0, 0, 0)])
+    assert ga_same(lay, tmp_path) == 0
+    assert read_pwc(tmp_path / "p.pwc")["cons"] == "AC*GGA"
+    lay2 = tmp_path / "z.pwl"
+    write_pwl(lay2, [(0, "ACG", [0, 0, 0], 0, 0, 0), (4, "TT", [0, 0], 0, 0, 0)])
+    assert ga_same(lay2, tmp_path) == 5
+
+
+def test_gapassem_clipped_rows(built, tmp_path):
+    rng = random.Random(7)
+    rows = []
+    for r in range(12):
+        n = rng.randint(20, 60)
+        seq = "".join(rng.choice("ACGTN") for _ in range(n))
+        ofs = [0] + [rng.choice([0, 0, 0, 1, 2, -1]) for _ in range(n - 1)]
+        rows.append((rng.randint(0, 30), seq, ofs, rng.randint(0, 4), rng.randint(0, 4), r % 2))
+    lay = tmp_path / "c.pwl"
+    write_pwl(lay, rows)
+    ga_same(lay, tmp_path, ["--no-refine-clipping"])
+
+
+@pytest.mark.parametrize("scale", [0.0005, 0.002, 0.01])
+def test_gapassem_synthetic(built, tmp_path, scale):
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", scale, "--out", lay])
+    assert rc == 0, err
+    assert ga_same(lay, tmp_path) == 0
+
+
+def test_gapassem_tile_boundaries(built, tmp_path):
+    # rows long enough to cross several 2048-column tiles and 256-base chunks with gaps
+    lay = tmp_path / "b.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.02, "--rows", 40, "--out", lay])
+    assert rc == 0, err
+    assert ga_same(lay, tmp_path) == 0
