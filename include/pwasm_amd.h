@@ -71,7 +71,9 @@ typedef struct pw_aln_result {
 #define PW_REC_MISMATCH 1 /* "Error: base mismatch ..." (pafreport.cpp:551-554) */
 #define PW_REC_MODSEQ 2   /* "Error: modseq[%d] not matching ..." (pafreport.cpp:812-813) */
 
-/* Arguments of pw_report_events (all pointers are device pointers). */
+/* Arguments of pw_report_events (all pointers are device pointers).  qseq and lits must stay
+ * readable for PW_DEV_PAD bytes past their last element (16-byte LDS staging loads). */
+#define PW_DEV_PAD 256
 typedef struct pw_report_args {
   const pw_aln_desc* desc;  /* [n_alns] */
   const uint32_t* ops;      /* packed ops */

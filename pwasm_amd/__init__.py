@@ -23,6 +23,8 @@ PW_OP_MATCH, PW_OP_SUB, PW_OP_INS, PW_OP_DEL = 0, 1, 2, 3
 PW_CS_OK, PW_CS_PARSE, PW_CS_SPLICED, PW_CS_UNHANDLED, PW_CS_EMPTY, PW_CS_BOUNDS, PW_CS_NOSPACE = range(7)
 PW_REC_OK, PW_REC_MISMATCH, PW_REC_MODSEQ = 0, 1, 2
 
+DEV_PAD = 256  # readable bytes required past the end of the device query / literal arrays
+
 # pafreport mode flags for pw_batch_from_files (same meaning as -G/-F/-C/-N)
 FLAG_G, FLAG_F, FLAG_C, FLAG_N = 1, 2, 4, 8
 
@@ -206,6 +208,8 @@ def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
             arr = np.zeros(1, dtype=arr.dtype)
         if arr.dtype == np.uint64:  # torch only needs the bytes
             arr = arr.view(np.uint8)
+        if name in ("lits", "qseq"):  # the kernel reads up to 256 bytes past the end (16-byte staging loads)
+            arr = np.concatenate([arr, np.zeros(DEV_PAD, dtype=arr.dtype)])
         dev[name] = torch.from_numpy(arr).to(device)
     dev["next_stop"] = torch.empty(max(int(v.qseq_len), 1), dtype=torch.int32, device=device)
     dev["text"] = torch.empty(max(int(v.text_total), 1), dtype=torch.uint8, device=device)

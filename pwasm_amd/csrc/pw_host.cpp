@@ -50,6 +50,10 @@ bool parse_int(const char*& p, int& out) {
 inline bool is_alpha(unsigned char c) { return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'); }
 inline unsigned char up(unsigned char c) { return (c >= 'a' && c <= 'z') ? (unsigned char)(c - 32) : c; }
 
+// Device copies of the query and literal arrays carry this many readable bytes past their end:
+// the report kernel stages them into LDS with 16-byte loads (pw_report.hip).
+constexpr size_t kDevPad = 256;
+
 // Per-event report-line byte bounds (see DESIGN.md §Text slots): the kernel never writes past them.
 constexpr uint64_t kBoundSub = 190, kBoundIndel = 140;
 
@@ -537,7 +541,7 @@ struct Device {
     }
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     nq = (uint32_t)q.len.size();
-    if (!qseq.ensure(q.seq.size() + 1) || !qoff.ensure(nq + 1) || !qlen.ensure(nq + 1) ||
+    if (!qseq.ensure(q.seq.size() + kDevPad) || !qoff.ensure(nq + 1) || !qlen.ensure(nq + 1) ||
         (!skip_codan && !next_stop.ensure(q.seq.size() + 1))) {
       fprintf(stderr, "pafreport: device allocation failed\n");
       return false;
@@ -560,7 +564,7 @@ struct Device {
     res_h.resize(na);
     text_h.resize(b.text_total);
     if (na == 0) return true;
-    if (!desc.ensure(na) || !ops.ensure(b.ops.size() + 1) || !lits.ensure(b.lits.size() + 1) ||
+    if (!desc.ensure(na) || !ops.ensure(b.ops.size() + 1) || !lits.ensure(b.lits.size() + kDevPad) ||
         !text.ensure(b.text_total + 1) || !res.ensure(na)) {
       fprintf(stderr, "pafreport: device allocation failed\n");
       return false;

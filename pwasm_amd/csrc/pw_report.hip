@@ -10,18 +10,27 @@
 //   event line        printDiffInfo (event loop)           pafreport.cpp:893-954
 //
 // Layout: one 64-lane wavefront (= one 64-thread workgroup) owns one PAF record at a time and
-// walks its packed op stream in chunks of 64 ops, one op per lane:
-//   1. wave prefix-scan of (q, t, literal) advances -> each op's query/target/literal start;
-//   2. ballot of SUB ops -> S-run heads (pafreport merges directly consecutive '*' ops,
+// walks its packed op stream in SEGMENTS of up to 128 ops (2 per lane):
+//   1. coalesced load of the segment's op words; wave prefix-scan of (query, target, literal)
+//      advances -> every op's start coordinates;
+//   2. the segment is cut where its query span or literal span would overflow the LDS windows,
+//      then staged in LDS with 16-byte loads: op words (+16-op halo each side), per-op starts,
+//      the literal bytes and the forward-query window its events can touch (span + 64 bytes
+//      each side).  Byte accesses hit LDS; one outside a window (long indels at a segment edge)
+//      falls back to the global copy, so windows change speed, never results;
+//   3. ballot of SUB ops -> S-run heads (pafreport merges directly consecutive '*' ops,
 //      pafreport.cpp:556-560; `:0` ops are dropped by the pre-pass so "consecutive" is exact);
-//   3. each head lane owns one event: final coordinates, target context (gathered from the
-//      op stream + query, never materialising tseq), 9-nt query context, status, amino acid,
-//      codon consequence (O(1) per indel via the next-stop table), and renders its report line
-//      twice (count, then write) into a per-wave LDS staging window;
-//   4. the wave copies the window to the record's text slot (events of '-' records are written
-//      back-to-front, which is the reference's tdiffs.Reverse(), pafreport.cpp:643).
-// Workgroups are persistent (grid-stride over records) so the 4.6 KB of byte tables are
-// staged into LDS once per workgroup.
+//      heads are compacted into an event list, one event per lane;
+//   4. each lane computes its event and writes the report line, field by field as the values
+//      become known, into its own 144-byte LDS line buffer (stores are unconditional: a
+//      masked-off character goes to the lane's junk byte, so there is no per-character branch);
+//   5. a wave prefix-scan of line lengths places the lines in the record's text slot (events of
+//      '-' records back-to-front = the reference's tdiffs.Reverse(), pafreport.cpp:643) and the
+//      lines are gathered 16 bytes per lane into full-width global stores.
+// A line longer than its buffer (an S run with many changed codons) is flagged and re-emitted
+// straight to global memory by long_lines_kernel, launched behind the main kernel.
+// Workgroups are persistent (grid-stride over records): the 4.6 KB of byte tables are staged
+// into LDS once per workgroup.
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -31,18 +40,43 @@
 
 namespace pw {
 
+// LDS pointers carry their address space explicitly: a generic pointer here makes hipcc merge
+// "LDS hit ? lds[o] : global[i]" into one flat load (global latency + vmcnt waits).
+#define LDS __attribute__((address_space(3)))
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // 16-byte copies
+
 __constant__ Tables c_tables = build_tables();
 
 constexpr int kWave = 64;
-constexpr int kStage = 4096;  // LDS staging window per wave (bytes)
-constexpr int kCtx = 24;      // per-lane target-context scratch (bytes)
-constexpr int kMaxEv = 12;    // MAX_EVLEN, pafreport.cpp:919
+constexpr int kSegOps = 128;    // ops per segment (2 per lane)
+constexpr int kOpHalo = 16;     // op words staged before / after a segment
+constexpr int kQW = 4096;       // forward-query window per wave (bytes)
+constexpr int kQPad = 64;       // context reach beyond a segment's query span
+constexpr int kLW = 1024;       // literal window per wave (bytes)
+constexpr int kLPad = 64;
+constexpr int kLine = 144;      // per-lane report-line buffer (bytes)
+constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
+constexpr int32_t kLongFlag = 0x100;  // results[].err bit: a line left for long_lines_kernel
+
+struct WaveLds {
+  uint8_t line[kWave * kLine];  // per-lane line buffers
+  uint8_t qw[kQW];
+  uint8_t lw[kLW];
+  uint8_t ctx[kWave * 24];      // per-lane target-context scratch
+  uint32_t opw[kSegOps + 2 * kOpHalo];
+  int32_t qs[kSegOps];
+  int32_t ts[kSegOps];
+  uint32_t ls[kSegOps];
+  uint32_t ostart[kWave + 1];   // line starts in output order
+  uint8_t junk[kWave];
+  uint8_t olane[kWave];         // lane of the k-th line in output order
+  uint16_t evl[kSegOps];
+};
 
 struct Lds {
-  Tables tab;                        // 4608 B
-  uint8_t stage[kStage];             // 4096 B
-  uint8_t ctx[kWave * kCtx];         // 1536 B
+  Tables tab;
+  WaveLds w;
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -55,31 +89,53 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
   return v;
 }
 __device__ __forceinline__ uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, kWave); }
+// LDS written by some lanes and read by others of the same (single-wave) workgroup
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }
 
 // ------------------------------------------------------------------ record context
 struct Rec {
-  const uint32_t* ops;   // this record's ops
-  const uint8_t* lits;   // global literal array
-  const uint8_t* R;      // forward query
-  const int32_t* NS;     // next-stop table of this query (or null)
-  int L;                 // query length
-  int offset;            // start on the aligned strand
-  int T;                 // tseq length
+  const uint32_t* ops;      // this record's ops (global)
+  const uint8_t* lits;      // global literal array
+  const uint8_t* R;         // forward query (global)
+  const int32_t* NS;        // next-stop table of this query (or null)
+  const LDS Tables* tab;    // LDS tables
+  const LDS uint8_t* qw;    // LDS forward-query window
+  const LDS uint8_t* lw;    // LDS literal window
+  const LDS uint32_t* opw;  // LDS op words
+  int L;                    // query length
+  int offset;               // start on the aligned strand
+  int T;                    // tseq length
   uint32_t n_ops;
+  int qlo;                  // forward position of qw[0]
+  uint32_t l_lo, l_n;       // literal window [l_lo, l_lo + l_n)
+  int op_lo;                // record op index of opw[0]
+  uint32_t op_n;
   bool rev;
 };
 
-__device__ __forceinline__ uint8_t Rc(const Rec& r, int x) { return (x >= 0 && x < r.L) ? r.R[x] : 0; }
+__device__ __forceinline__ uint8_t Rc(const Rec& r, int x) {
+  if ((unsigned)x >= (unsigned)r.L) return 0;
+  const unsigned o = (unsigned)(x - r.qlo);
+  return o < (unsigned)kQW ? r.qw[o] : r.R[x];
+}
+__device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
+  const uint32_t o = i - r.l_lo;
+  return o < r.l_n ? r.lw[o] : r.lits[i];
+}
+__device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
+  const unsigned o = (unsigned)((int)j - r.op_lo);
+  return o < r.op_n ? r.opw[o] : r.ops[j];
+}
 
 // aligned-strand query char at p (refseq_rc for '-' records, pafreport.cpp:352-362); p == L
 // reads the NUL terminator as the reference does.
-__device__ __forceinline__ uint8_t aligned_char(const Rec& r, const Lds& s, int p) {
-  if (p < 0 || p >= r.L) return 0;
-  return r.rev ? s.tab.comp[r.R[r.L - 1 - p]] : r.R[p];
+__device__ __forceinline__ uint8_t aligned_char(const Rec& r, int p) {
+  if ((unsigned)p >= (unsigned)r.L) return 0;
+  return r.rev ? r.tab->comp[Rc(r, r.L - 1 - p)] : Rc(r, p);
 }
 
-__device__ __forceinline__ uint8_t translate(const Lds& s, uint8_t a, uint8_t b, uint8_t c) {
-  return s.tab.codon[(s.tab.nt[a] << 8) | (s.tab.nt[b] << 4) | s.tab.nt[c]];
+__device__ __forceinline__ uint8_t translate(const LDS Tables* t, uint8_t a, uint8_t b, uint8_t c) {
+  return t->codon[(t->nt[a] << 8) | (t->nt[b] << 4) | t->nt[c]];
 }
 
 __device__ __forceinline__ uint32_t op_tadv(uint32_t w) {
@@ -94,54 +150,41 @@ __device__ __forceinline__ uint32_t op_ladv(uint32_t w) {
   uint32_t t = w >> 30, n = w & 0x3FFFFFFFu;
   return t == PW_OP_SUB ? 2u : (t == PW_OP_INS ? n : 0u);
 }
-
-// ------------------------------------------------------------------ one event (head lane)
-struct Event {
-  uint32_t type;   // PW_OP_SUB / INS / DEL
-  int n;           // evtbases length (S-run length, I/D length)
-  int q_pos;       // offset + qpos at creation (aligned strand)
-  uint32_t ls;     // literal start of the head op
-  int rloc, tloc;  // final (printed - 1)
-  int ctx_len;     // tctx length before abbreviation
-  int rctx0, rctx_loc;
-  int status;      // 0 unknown, 1 homopolymer, 2..5 motif
-  uint8_t aa;
-  int aapos;       // printed aapos (rloc/3 + 1)
-  int r_trloc;
-  // I/D impact (computed once)
-  int imp_kind;    // 0 none, 1 stop, 2 frame shift, 3 empty
-  int imp_val;
-  uint32_t aa4, maa4;
-  int aa4n, maa4n;
-};
-
-// evtbases[i] in final orientation, upper case (pafreport.cpp:563,594-596,612-614,637,895)
-__device__ __forceinline__ uint8_t ev_base(const Rec& r, const Lds& s, const Event& e, int i) {
-  if (e.type == PW_OP_SUB) {
-    return r.rev ? s.tab.comp[r.lits[e.ls + 2 * (e.n - 1 - i)]] : r.lits[e.ls + 2 * i];
-  } else if (e.type == PW_OP_INS) {
-    return r.rev ? s.tab.comp[r.lits[e.ls + (e.n - 1 - i)]] : r.lits[e.ls + i];
-  }
-  return r.rev ? s.tab.comp[s.tab.comp[Rc(r, e.rloc + i)]] : Rc(r, e.q_pos + i);
-}
-// evtsub[i] (S only)
-__device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Lds& s, const Event& e, int i) {
-  return r.rev ? s.tab.comp[r.lits[e.ls + 2 * (e.n - 1 - i) + 1]] : r.lits[e.ls + 2 * i + 1];
-}
 __device__ __forceinline__ uint8_t to_upper(uint8_t c) { return (c >= 'a' && c <= 'z') ? c - 32 : c; }
 __device__ __forceinline__ uint8_t to_lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
 
-// Gather tseq[p0, p1) (tseq = the target segment, pafreport.cpp:543,575,588) by walking the op
-// stream from the event's head op; writes into dst[0..).
+// ------------------------------------------------------------------ event
+struct Event {
+  uint32_t type;  // PW_OP_SUB / INS / DEL
+  int n;          // evtbases length (S-run length, I/D length)
+  int q_pos;      // offset + qpos at creation (aligned strand)
+  uint32_t ls;    // literal start of the head op
+  int rloc;       // final (printed - 1)
+  int r_trloc;
+};
+
+// evtbases[i] in final orientation, upper case (pafreport.cpp:563,594-596,612-614,637,895)
+__device__ __forceinline__ uint8_t ev_base(const Rec& r, const Event& e, int i) {
+  if (e.type == PW_OP_SUB) return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i))] : litb(r, e.ls + 2 * i);
+  if (e.type == PW_OP_INS) return r.rev ? r.tab->comp[litb(r, e.ls + (e.n - 1 - i))] : litb(r, e.ls + i);
+  return r.rev ? r.tab->comp[r.tab->comp[Rc(r, e.rloc + i)]] : Rc(r, e.q_pos + i);
+}
+// evtsub[i] (S only)
+__device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
+  return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i) + 1)] : litb(r, e.ls + 2 * i + 1);
+}
+
+// Gather tseq[p0, p1) (the target segment, pafreport.cpp:543,575,588) by walking the op
+// stream from the event's head op.
 struct Cursor {
   uint32_t j;
   int ts, qs;
   uint32_t ls, w;
 };
-__device__ void gather_tseq(const Rec& r, const Lds& s, Cursor c, int p0, int p1, uint8_t* dst) {
+__device__ __forceinline__ void gather_tseq(const Rec& r, Cursor c, int p0, int p1, LDS uint8_t* dst) {
   while (c.ts > p0 && c.j > 0) {  // step back to the op holding p0
     c.j--;
-    c.w = r.ops[c.j];
+    c.w = opword(r, c.j);
     c.ts -= (int)op_tadv(c.w);
     c.qs -= (int)op_qadv(c.w);
     c.ls -= op_ladv(c.w);
@@ -153,166 +196,81 @@ __device__ void gather_tseq(const Rec& r, const Lds& s, Cursor c, int p0, int p1
       c.qs += (int)op_qadv(c.w);
       c.ls += op_ladv(c.w);
       c.j++;
-      c.w = r.ops[c.j];
+      c.w = opword(r, c.j);
     }
-    uint32_t t = c.w >> 30;
-    int off = p - c.ts;
+    const uint32_t t = c.w >> 30;
+    const int off = p - c.ts;
     uint8_t ch;
-    if (t == PW_OP_MATCH) ch = aligned_char(r, s, r.offset + c.qs + off);
-    else if (t == PW_OP_SUB) ch = to_lower(r.lits[c.ls]);
-    else ch = to_lower(r.lits[c.ls + off]);
+    if (t == PW_OP_MATCH) ch = aligned_char(r, r.offset + c.qs + off);
+    else if (t == PW_OP_SUB) ch = to_lower(litb(r, c.ls));
+    else ch = to_lower(litb(r, c.ls + off));
     dst[k++] = ch;
   }
 }
 
-// ------------------------------------------------------------------ rendering sinks
-struct CountSink {
-  int n = 0;
-  __device__ __forceinline__ void put(uint8_t) { n++; }
-};
-struct WriteSink {
-  uint8_t* buf;
-  int pos, lo, hi;
+// ------------------------------------------------------------------ line sinks
+// LineSink writes into the lane's LDS line buffer; a store past the buffer or a masked-off
+// character goes to the lane's junk byte (no branch).  GlobalSink (long_lines_kernel) writes
+// the line straight to its place in the text slot.
+struct LineSink {
+  LDS uint8_t* buf;
+  LDS uint8_t* junk;
+  int pos;
   __device__ __forceinline__ void put(uint8_t c) {
-    if (pos >= lo && pos < hi) buf[pos - lo] = c;
+    *(pos < kLine ? buf + pos : junk) = c;
     pos++;
   }
+  __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
+    *((pred && pos < kLine) ? buf + pos : junk) = c;
+    pos += pred ? 1 : 0;
+  }
 };
-template <class S>
-__device__ __forceinline__ void put_str(S& k, const char* p) {
-  while (*p) k.put((uint8_t)*p++);
-}
-template <class S>
-__device__ __forceinline__ void put_int(S& k, int v) {
-  if (v < 0) {
-    k.put('-');
-    v = -v;  // values here are > INT_MIN
+struct GlobalSink {
+  uint8_t* p;
+  int pos;
+  __device__ __forceinline__ void put(uint8_t c) { p[pos++] = c; }
+  __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
+    if (pred) p[pos++] = c;
   }
-  char b[11];
-  int n = 0;
-  do {
-    b[n++] = (char)('0' + v % 10);
-    v /= 10;
-  } while (v);
-  while (n) k.put((uint8_t)b[--n]);
-}
+};
 
-__constant__ char kMotif[4][6] = {"CCTGG", "CCAGG", "GATC", "GTAC"};  // pafreport.cpp:41
-
+// "%d" of a non-negative int
 template <class S>
-__device__ void put_bases(S& k, const Rec& r, const Lds& s, const Event& e, bool sub) {
-  if (e.n > kMaxEv) {
-    k.put('[');
-    put_int(k, e.n);
-    k.put(']');
-    return;
+__device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
+  if (v >= 100000u) {
+    for (uint32_t P = 1000000000u; P >= 100000u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   }
-  for (int i = 0; i < e.n; i++) k.put(sub ? ev_sub(r, s, e, i) : ev_base(r, s, e, i));
-}
-
-// S consequence: predictImpact substitution branch (pafreport.cpp:804-841)
-template <class S>
-__device__ void put_sub_impact(S& k, const Rec& r, const Lds& s, const Event& e) {
-  int p0 = e.rloc - e.r_trloc;
-  int first = p0 / 3, last = (p0 + e.n - 1) / 3;
-  bool any = false;
-  for (int ao = first; ao <= last; ao++) {
-    uint8_t m[3], o[3];
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-      int pos = 3 * ao + j;
-      o[j] = Rc(r, e.r_trloc + pos);
-      m[j] = (pos >= p0 && pos < p0 + e.n) ? ev_base(r, s, e, pos - p0) : o[j];
-    }
-    uint8_t aa = translate(s, o[0], o[1], o[2]);
-    uint8_t maa = translate(s, m[0], m[1], m[2]);
-    if (aa != maa) {
-      if (any) put_str(k, ", ");
-      put_str(k, "AA");
-      int aapos = ao + e.rloc / 3;
-      put_int(k, aapos);
-      k.put('|');
-      k.put(aa);
-      k.put(':');
-      k.put(maa);
-      any = true;
-      if (maa == '.') {
-        put_str(k, "|premature stop at AA");
-        put_int(k, aapos);
-      }
-    }
-  }
-  if (!any) put_str(k, "synonymous");
+  for (uint32_t P = 10000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
+  k.put((uint8_t)('0' + v % 10u));
+}
+template <class S, int N>
+__device__ __forceinline__ void wr_lit(S& k, const char (&s)[N]) {
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) k.put((uint8_t)s[i]);
 }
 
+// S consequence, one codon of modseq (predictImpact, pafreport.cpp:811-826)
+__device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, uint8_t& aa, uint8_t& maa) {
+  const int p0 = e.rloc - e.r_trloc;
+  uint8_t m[3], o[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const int pos = 3 * ao + j;
+    o[j] = Rc(r, e.r_trloc + pos);
+    m[j] = (pos >= p0 && pos < p0 + e.n) ? ev_base(r, e, pos - p0) : o[j];
+  }
+  aa = translate(r.tab, o[0], o[1], o[2]);
+  maa = translate(r.tab, m[0], m[1], m[2]);
+}
+
+// Indel consequence: predictImpact insert/cut + stop scan (pafreport.cpp:843-882), written to
+// the sink.  modseq = Q[r_trloc, rloc) + X + Q[s, L) with X the inserted bases (I) or nothing
+// (D; s = rloc + len).  Codons touching the prefix / X / the first five codons are translated
+// explicitly; past that, modseq codons are query codons and the first stop is one lookup in the
+// next-stop table.
 template <class S>
-__device__ void render(S& k, const Rec& r, const Lds& s, const Event& e, const uint8_t* ctx, bool skip_codan) {
-  k.put(e.type == PW_OP_SUB ? 'S' : (e.type == PW_OP_INS ? 'I' : 'D'));
-  k.put('\t');
-  put_int(k, e.rloc + 1);
-  k.put('\t');
-  put_int(k, e.aapos);
-  k.put('(');
-  k.put(e.aa);
-  k.put(')');
-  k.put('\t');
-  if (e.type == PW_OP_SUB) {
-    put_bases(k, r, s, e, true);
-    k.put(':');
-    put_bases(k, r, s, e, false);
-  } else if (e.type == PW_OP_INS) {
-    k.put(':');
-    put_bases(k, r, s, e, false);
-  } else {
-    put_bases(k, r, s, e, false);
-    k.put(':');
-  }
-  k.put('\t');
-  put_int(k, e.tloc + 1);
-  k.put('\t');
-  const int l = e.ctx_len;  // tctx, abbreviated past 22 (pafreport.cpp:918-927)
-  if (l <= 10 + kMaxEv) {
-    for (int j = 0; j < l; j++) k.put(r.rev ? s.tab.comp[ctx[l - 1 - j]] : ctx[j]);
-  } else {
-    for (int j = 0; j < 5; j++) k.put(r.rev ? s.tab.comp[ctx[9 - j]] : ctx[j]);
-    k.put('[');
-    put_int(k, l - 10);
-    k.put(']');
-    for (int j = 0; j < 5; j++) k.put(r.rev ? s.tab.comp[ctx[4 - j]] : ctx[5 + j]);
-  }
-  k.put('\t');
-  for (int j = 0; j < 9; j++) k.put(r.R[e.rctx0 + j]);
-  k.put('\t');
-  if (e.status == 0) put_str(k, "[unknown]");
-  else if (e.status == 1) put_str(k, "homopolymer");
-  else {
-    put_str(k, "motif ");
-    put_str(k, kMotif[e.status - 2]);
-  }
-  k.put('\t');
-  if (!skip_codan) {
-    if (e.type == PW_OP_SUB) put_sub_impact(k, r, s, e);
-    else if (e.imp_kind == 1) {
-      put_str(k, "premature stop at AA");
-      put_int(k, e.imp_val);
-    } else if (e.imp_kind == 2) {
-      put_str(k, "frame shift ");
-      for (int j = 0; j < e.aa4n; j++) k.put((uint8_t)(e.aa4 >> (8 * j)));
-      k.put('+');
-      k.put(':');
-      for (int j = 0; j < e.maa4n; j++) k.put((uint8_t)(e.maa4 >> (8 * j)));
-      k.put('+');
-    }
-  }
-  k.put('\n');
-}
-
-// Indel consequence: predictImpact insert/cut + stop scan (pafreport.cpp:843-882).  The
-// modified sequence is modseq = Q[r_trloc, rloc) + X + Q[s, L) with X the inserted bases
-// (I) or nothing (D; s = rloc + len).  Codons touching the prefix / X / the first five codons
-// are translated explicitly; past that, modseq codons are query codons and the first stop is
-// one lookup in the next-stop table.
-__device__ void indel_impact(const Rec& r, const Lds& s, Event& e) {
+__device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e) {
   const int a = e.rloc - e.r_trloc;
   const int x = (e.type == PW_OP_INS) ? e.n : 0;
   const int dl = (e.type == PW_OP_DEL) ? e.n : 0;
@@ -322,50 +280,261 @@ __device__ void indel_impact(const Rec& r, const Lds& s, Event& e) {
   int E = a + x;
   if (E < 15) E = 15;
   int stop_i = -1;
-  e.aa4 = e.maa4 = 0;
-  e.aa4n = e.maa4n = 0;
+  uint32_t aa4 = 0, maa4 = 0;
+  int aa4n = 0, maa4n = 0;
   int i = 0;
   for (; i + 2 < M && i < E; i += 3) {
     uint8_t m[3];
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      int p = i + j;
-      m[j] = (p < a) ? Rc(r, e.r_trloc + p) : (p < a + x ? ev_base(r, s, e, p - a) : Rc(r, sfx + p - a - x));
+      const int p = i + j;
+      m[j] = (p < a) ? Rc(r, e.r_trloc + p) : (p < a + x ? ev_base(r, e, p - a) : Rc(r, sfx + p - a - x));
     }
-    uint8_t mm = translate(s, m[0], m[1], m[2]);
+    const uint8_t mm = translate(r.tab, m[0], m[1], m[2]);
     if (mm == '.') {
       stop_i = i;
       break;
     }
-    if (i > 0 && e.maa4n < 4) {
+    if (i > 0 && maa4n < 4) {
       if (i + 2 < trlen) {
-        e.aa4 |= (uint32_t)translate(s, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1), Rc(r, e.r_trloc + i + 2))
-                 << (8 * e.aa4n);
-        e.aa4n++;
+        aa4 |= (uint32_t)translate(r.tab, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1), Rc(r, e.r_trloc + i + 2))
+               << (8 * aa4n);
+        aa4n++;
       }
-      e.maa4 |= (uint32_t)mm << (8 * e.maa4n);
-      e.maa4n++;
+      maa4 |= (uint32_t)mm << (8 * maa4n);
+      maa4n++;
     }
   }
   if (stop_i < 0 && i + 2 < M && r.NS) {
-    int k0 = sfx + (i - a - x);
+    const int k0 = sfx + (i - a - x);
     if (k0 >= 0 && k0 < r.L) {
-      int st = r.NS[k0];
+      const int st = r.NS[k0];
       if (st != kNoStop) stop_i = st - sfx + a + x;
     }
   }
   if (stop_i >= 0) {
-    e.imp_kind = 1;
-    e.imp_val = 1 + (stop_i + e.r_trloc) / 3;
-  } else if (e.aa4n > 0 && e.maa4n > 0) {
-    e.imp_kind = 2;
-  } else {
-    e.imp_kind = 3;
+    wr_lit(k, "premature stop at AA");
+    wr_dig(k, (uint32_t)(1 + (stop_i + e.r_trloc) / 3));
+  } else if (aa4n > 0 && maa4n > 0) {
+    wr_lit(k, "frame shift ");
+#pragma unroll
+    for (int q = 0; q < 4; q++) k.put_if(q < aa4n, (uint8_t)(aa4 >> (8 * q)));
+    k.put('+');
+    k.put(':');
+#pragma unroll
+    for (int q = 0; q < 4; q++) k.put_if(q < maa4n, (uint8_t)(maa4 >> (8 * q)));
+    k.put('+');
   }
 }
 
+// Compute the event whose head op is `j` (record op index), segment slot `idx`, and write its
+// report line (printDiffInfo, pafreport.cpp:886-953) to the sink as the fields become known.
+// Returns the evtsub index failing the modseq check (pafreport.cpp:811-814), or -1; `rel`
+// receives rloc - r_trloc for the error message.
+template <class S>
+__device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds* w, uint32_t idx, uint32_t j,
+                                          bool skip, LDS uint8_t* ctx, int& rel) {
+  Event e;
+  const uint32_t wd = w->opw[kOpHalo + idx];
+  const uint32_t typ = wd >> 30;
+  const int qs = w->qs[idx], ts = w->ts[idx];
+  const uint32_t ls = w->ls[idx];
+  const int qp = r.offset + qs;
+  e.type = typ;
+  e.q_pos = qp;
+  e.ls = ls;
+  if (typ == PW_OP_SUB) {  // run of directly consecutive '*' ops (pafreport.cpp:556-560)
+    int n = 1;
+    uint32_t kk = j + 1;
+    while (kk < r.n_ops && (opword(r, kk) >> 30) == PW_OP_SUB) {
+      n++;
+      kk++;
+    }
+    e.n = n;
+  } else {
+    e.n = (int)(wd & 0x3FFFFFFFu);
+  }
+  const int evtlen = typ == PW_OP_SUB ? 1 : e.n;  // merged S keeps evtlen 1 (pafreport.cpp:562)
+  int tloc;
+  if (!r.rev) {
+    e.rloc = qp;
+    tloc = ts;
+  } else {  // pafreport.cpp:597, 615, 633, 639
+    e.rloc = (typ == PW_OP_INS) ? r.L - qp : r.L - qp - e.n;
+    tloc = r.T - ts;
+  }
+  // amino acid at the event (pafreport.cpp:897-899)
+  const int aap0 = e.rloc / 3;
+  const uint8_t aa = translate(r.tab, Rc(r, 3 * aap0), Rc(r, 3 * aap0 + 1), Rc(r, 3 * aap0 + 2));
+  e.r_trloc = aap0 > 0 ? 3 * (aap0 - 1) : 0;  // 3*(aapos-2), clipped at 0
+  rel = e.rloc - e.r_trloc;
+
+  // ---- "E\trloc\taapos(aa)\t"
+  k.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
+  k.put('\t');
+  wr_dig(k, (uint32_t)(e.rloc + 1));
+  k.put('\t');
+  wr_dig(k, (uint32_t)(aap0 + 1));
+  k.put('(');
+  k.put(aa);
+  k.put(')');
+  k.put('\t');
+  // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity
+  const bool big = e.n > kMaxEv;
+  if (typ == PW_OP_SUB) {
+    if (big) {
+      k.put('[');
+      wr_dig(k, (uint32_t)e.n);
+      k.put(']');
+    } else {
+      for (int i = 0; i < e.n; i++) k.put(ev_sub(r, e, i));
+    }
+  }
+  if (typ != PW_OP_DEL) k.put(':');
+  const uint8_t b0 = ev_base(r, e, 0);
+  bool same = true;
+  if (big) {
+    k.put('[');
+    wr_dig(k, (uint32_t)e.n);
+    k.put(']');
+    for (int i = 1; i < e.n; i++) same = same && ev_base(r, e, i) == b0;
+  } else {
+    for (int i = 0; i < e.n; i++) {
+      const uint8_t b = ev_base(r, e, i);
+      same = same && b == b0;
+      k.put(b);
+    }
+  }
+  if (typ == PW_OP_DEL) k.put(':');
+  k.put('\t');
+  wr_dig(k, (uint32_t)(tloc + 1));
+  k.put('\t');
+  // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
+  {
+    int tcs = ts - 5;
+    if (tcs < 0) tcs = 0;
+    int tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
+    if (tce >= r.T) tce = r.T - 1;
+    int cl = tce - tcs;
+    if (cl < 0) cl = 0;
+    Cursor cur;
+    cur.j = j;
+    cur.ts = ts;
+    cur.qs = qs;
+    cur.ls = ls;
+    cur.w = wd;
+    const bool abbr = cl > 10 + kMaxEv;
+    if (!abbr) {
+      gather_tseq(r, cur, tcs, tce, ctx);
+      for (int q = 0; q < cl; q++) k.put(r.rev ? r.tab->comp[ctx[cl - 1 - q]] : ctx[q]);
+    } else {
+      gather_tseq(r, cur, tcs, tcs + 5, ctx);
+      gather_tseq(r, cur, tce - 5, tce, ctx + 5);
+#pragma unroll
+      for (int q = 0; q < 5; q++) k.put(r.rev ? r.tab->comp[ctx[9 - q]] : ctx[q]);
+      k.put('[');
+      wr_dig(k, (uint32_t)(cl - 10));
+      k.put(']');
+#pragma unroll
+      for (int q = 0; q < 5; q++) k.put(r.rev ? r.tab->comp[ctx[4 - q]] : ctx[5 + q]);
+    }
+  }
+  k.put('\t');
+  // ---- query context (getRefContext, pafreport.cpp:721-733) + status
+  int c0 = e.rloc - 4, eloc = 4;
+  if (c0 < 0) {
+    eloc += c0;
+    c0 = 0;
+  } else if (c0 + 8 >= r.L) {
+    eloc += r.L - c0 - 9;
+    c0 = r.L - 9;
+  }
+  if (c0 < 0) c0 = 0;  // L < 9 is reported by the host
+  uint32_t rw0 = 0, rw1 = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint8_t c = Rc(r, c0 + q);
+    k.put(c);
+    rw0 |= (uint32_t)c << (8 * q);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint8_t c = Rc(r, c0 + 4 + q);
+    k.put(c);
+    rw1 |= (uint32_t)c << (8 * q);
+  }
+  const uint32_t rw2 = Rc(r, c0 + 8);
+  k.put((uint8_t)rw2);
+  k.put('\t');
+  {
+    // homopolymer seed "cccc": first occurrence in the context (hpolyCheck, :742-746); motifs:
+    // first in list order anywhere in it (mmotifCheck, :751-763)
+    const uint64_t lo = (uint64_t)rw0 | ((uint64_t)rw1 << 32);
+    int l = -1;
+    bool m0 = false, m1 = false, m2 = false, m3 = false;
+#pragma unroll
+    for (int p = 5; p >= 0; p--) {
+      const uint32_t v4 = p <= 4 ? (uint32_t)(lo >> (8 * p)) : ((rw1 >> 8) | (rw2 << 24));
+      const uint32_t c4 = p < 4 ? (uint32_t)(lo >> (8 * (p + 4))) & 0xFFu : (p == 4 ? rw2 : 0u);
+      if (v4 == 0x01010101u * b0) l = p;
+      m0 = m0 || (v4 == 0x47544343u && c4 == 'G');  // "CCTGG"
+      m1 = m1 || (v4 == 0x47414343u && c4 == 'G');  // "CCAGG"
+      m2 = m2 || v4 == 0x43544147u;                 // "GATC"
+      m3 = m3 || v4 == 0x43415447u;                 // "GTAC"
+    }
+    const int st = (same && l >= 0 && l <= eloc && l + 4 >= eloc) ? 1 : (m0 ? 2 : (m1 ? 3 : (m2 ? 4 : (m3 ? 5 : 0))));
+    switch (st) {
+      case 0: wr_lit(k, "[unknown]"); break;
+      case 1: wr_lit(k, "homopolymer"); break;
+      case 2: wr_lit(k, "motif CCTGG"); break;
+      case 3: wr_lit(k, "motif CCAGG"); break;
+      case 4: wr_lit(k, "motif GATC"); break;
+      default: wr_lit(k, "motif GTAC"); break;
+    }
+  }
+  k.put('\t');
+  // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
+  int modseq_err = -1;
+  if (!skip) {
+    if (typ == PW_OP_SUB) {
+      for (int i = 0; i < e.n; i++)
+        if (modseq_err < 0 && to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, e, i))) modseq_err = i;
+      const int p0 = e.rloc - e.r_trloc;
+      bool any = false;
+      for (int ao = p0 / 3; ao <= (p0 + e.n - 1) / 3; ao++) {
+        uint8_t caa, cmaa;
+        sub_codon(r, e, ao, caa, cmaa);
+        if (caa != cmaa) {
+          if (any) wr_lit(k, ", ");
+          wr_lit(k, "AA");
+          const uint32_t ap = (uint32_t)(ao + e.rloc / 3);
+          wr_dig(k, ap);
+          k.put('|');
+          k.put(caa);
+          k.put(':');
+          k.put(cmaa);
+          if (cmaa == '.') {
+            wr_lit(k, "|premature stop at AA");
+            wr_dig(k, ap);
+          }
+          any = true;
+        }
+      }
+      if (!any) wr_lit(k, "synonymous");
+    } else {
+      indel_impact(k, r, e);
+    }
+  }
+  k.put('\n');
+  return modseq_err;
+}
+
 // ------------------------------------------------------------------ per-record driver
-__device__ void process_record(const pw_report_args& A, Lds& s, uint32_t ai, int lane) {
+// kLong: long_lines_kernel instance — only flagged records, only lines longer than kLine,
+// written straight to the text slot.
+template <bool kLong>
+__device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds* S, uint32_t ai, int lane) {
+  LDS WaveLds* w = &S->w;
   const pw_aln_desc d = A.desc[ai];
   const uint32_t qi = d.ref & 0x7FFFFFFFu;
   Rec r;
@@ -374,6 +543,10 @@ __device__ void process_record(const pw_report_args& A, Lds& s, uint32_t ai, int
   r.R = A.qseq + A.qoff[qi];
   r.L = A.qlen[qi];
   r.NS = A.next_stop ? A.next_stop + A.qoff[qi] : nullptr;
+  r.tab = &S->tab;
+  r.qw = w->qw;
+  r.lw = w->lw;
+  r.opw = w->opw;
   r.offset = d.offset;
   r.T = d.t_len;
   r.n_ops = d.n_ops;
@@ -385,203 +558,207 @@ __device__ void process_record(const pw_report_args& A, Lds& s, uint32_t ai, int
 
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
-  bool prev_sub = false;
-  uint32_t ev_base_idx = 0;
+  bool prev_sub = false, any_long = false;
+  uint32_t ev_idx = 0;
   int me_first = INT_MAX, me_last = -1, me_fa = 0, me_fb = 0, me_la = 0, me_lb = 0;  // modseq errors
-  uint8_t* ctx = s.ctx + lane * kCtx;
+  LDS uint8_t* ctx = w->ctx + lane * 24;
+  LDS uint8_t* my_line = w->line + lane * kLine;
 
-  for (uint32_t base = 0; base < r.n_ops; base += kWave) {
-    const uint32_t k = base + lane;
-    const bool valid = k < r.n_ops;
-    const uint32_t w = valid ? r.ops[k] : 0u;
-    const uint32_t typ = w >> 30, len = w & 0x3FFFFFFFu;
-    const uint32_t qadv = op_qadv(w), tadv = op_tadv(w), ladv = op_ladv(w);
-    const uint32_t qi_ = wave_incl_scan(qadv, lane);
-    const uint32_t ti_ = wave_incl_scan(tadv, lane);
-    const uint32_t li_ = wave_incl_scan(ladv, lane);
-    const int qs = qc + (int)(qi_ - qadv);
-    const int ts = tc + (int)(ti_ - tadv);
-    const uint32_t ls = lc + (li_ - ladv);
-    const bool is_sub = valid && typ == PW_OP_SUB;
-    const uint64_t submask = __ballot(is_sub);
-    const bool prevsub = lane == 0 ? prev_sub : ((submask >> (lane - 1)) & 1ull) != 0;
-    const bool head = valid && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub));
-
-    // base check of every '*' op (pafreport.cpp:550-554)
-    bool bad = false;
-    uint8_t qch = 0, rch = 0;
-    const int qp = r.offset + qs;
-    if (is_sub) {
-      qch = r.lits[ls + 1];
-      rch = aligned_char(r, s, qp);
-      bad = qch != rch;
+  for (uint32_t sb = 0; sb < r.n_ops;) {
+    // ---- 1. op words + scan (2 ops per lane, op sb + 64k + lane)
+    uint32_t wd[2], qa[2], ta[2], la[2];
+    int qs[2], ts[2];
+    uint32_t ls[2];
+    uint32_t qtot = 0, ttot = 0, ltot = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t j = sb + 64 * k + lane;
+      wd[k] = j < r.n_ops ? r.ops[j] : 0u;
+      qa[k] = op_qadv(wd[k]);
+      ta[k] = op_tadv(wd[k]);
+      la[k] = op_ladv(wd[k]);
+      const uint32_t qi_ = wave_incl_scan(qa[k], lane), ti_ = wave_incl_scan(ta[k], lane),
+                     li_ = wave_incl_scan(la[k], lane);
+      qs[k] = qc + (int)(qtot + qi_ - qa[k]);
+      ts[k] = tc + (int)(ttot + ti_ - ta[k]);
+      ls[k] = lc + ltot + li_ - la[k];
+      qtot += bcast(qi_, 63);
+      ttot += bcast(ti_, 63);
+      ltot += bcast(li_, 63);
     }
-    const uint64_t badmask = __ballot(bad);
-    if (badmask) {
-      const int fl = __builtin_ctzll(badmask);
-      if (lane == fl) {
+    // ---- 2. segment length: query / literal spans must fit the windows
+    uint32_t nseg = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t j = sb + 64 * k + lane;
+      const bool fits = j < r.n_ops && (uint32_t)(qs[k] + (int)qa[k] - qc) <= (uint32_t)(kQW - 2 * kQPad - 16) &&
+                        (ls[k] + la[k] - lc) <= (uint32_t)(kLW - 2 * kLPad - 16);
+      nseg += (uint32_t)__popcll(__ballot(fits));
+    }
+    if (nseg == 0) nseg = 1;
+    // ---- 3. stage op words (+halo), starts
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t idx = 64 * k + lane;
+      if (idx < nseg) {
+        w->opw[kOpHalo + idx] = wd[k];
+        w->qs[idx] = qs[k];
+        w->ts[idx] = ts[k];
+        w->ls[idx] = ls[k];
+      }
+    }
+    if (lane < 2 * kOpHalo) {
+      const int j = lane < kOpHalo ? (int)sb - kOpHalo + lane : (int)(sb + nseg) + (lane - kOpHalo);
+      const uint32_t v = (j >= 0 && (uint32_t)j < r.n_ops) ? r.ops[j] : 0u;
+      w->opw[lane < kOpHalo ? lane : kOpHalo + nseg + (lane - kOpHalo)] = v;
+    }
+    r.op_lo = (int)sb - kOpHalo;
+    r.op_n = nseg + 2 * kOpHalo;
+    uint32_t sq = 0, st = 0, sl = 0;  // segment totals
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const bool in = (uint32_t)(64 * k + lane) < nseg;
+      sq += in ? qa[k] : 0u;
+      st += in ? ta[k] : 0u;
+      sl += in ? la[k] : 0u;
+    }
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+      sq += __shfl_xor(sq, dd, kWave);
+      st += __shfl_xor(st, dd, kWave);
+      sl += __shfl_xor(sl, dd, kWave);
+    }
+    // ---- 4. forward-query window: aligned span [offset+qc-pad, offset+qc+sq+pad)
+    {
+      const int a0q = r.offset + qc - kQPad, a1q = r.offset + qc + (int)sq + kQPad;
+      int f0 = r.rev ? r.L - a1q : a0q;
+      if (f0 < 0) f0 = 0;
+      if (f0 > r.L) f0 = r.L;
+      const uintptr_t abs0 = (uintptr_t)(r.R + f0) & ~(uintptr_t)15;
+      r.qlo = (int)((intptr_t)abs0 - (intptr_t)r.R);
+      const intptr_t avail = (intptr_t)(r.R + r.L) - (intptr_t)abs0;  // bytes up to the query end
+      int nbytes = (int)((avail + 15) & ~(intptr_t)15);
+      if (nbytes > kQW) nbytes = kQW;
+      for (int o = lane * 16; o < nbytes; o += kWave * 16)
+        *reinterpret_cast<LDS v4u*>(w->qw + o) = *reinterpret_cast<const v4u*>(abs0 + o);
+    }
+    // ---- 5. literal window [lc - pad, lc + sl + pad)
+    {
+      const uint32_t l0 = lc > (uint32_t)kLPad ? lc - kLPad : 0u;
+      const uintptr_t abs0 = (uintptr_t)(r.lits + l0) & ~(uintptr_t)15;
+      r.l_lo = (uint32_t)((const uint8_t*)abs0 - r.lits);
+      uint32_t nbytes = (lc + sl + kLPad - r.l_lo + 15) & ~15u;
+      if (nbytes > (uint32_t)kLW) nbytes = kLW;
+      r.l_n = nbytes;
+      for (uint32_t o = lane * 16; o < nbytes; o += kWave * 16)
+        *reinterpret_cast<LDS v4u*>(w->lw + o) = *reinterpret_cast<const v4u*>(abs0 + o);
+    }
+    wave_sync();
+
+    // ---- 6. base check of every '*' op (pafreport.cpp:550-554) and S-run heads
+    uint64_t hm[2];
+    uint32_t sm_prev = prev_sub ? 1u : 0u;
+    int bad_idx = INT_MAX;
+    int bad_qp = 0, bad_q = 0, bad_r = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t idx = 64 * k + lane;
+      const bool in = idx < nseg;
+      const uint32_t typ = wd[k] >> 30;
+      const bool is_sub = in && typ == PW_OP_SUB;
+      const uint64_t subm = __ballot(is_sub);
+      const bool prevsub = lane == 0 ? sm_prev != 0 : ((subm >> (lane - 1)) & 1ull) != 0;
+      sm_prev = (uint32_t)((subm >> 63) & 1ull);
+      hm[k] = __ballot(in && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub)));
+      bool bad = false;
+      uint8_t qch = 0, rch = 0;
+      const int qp = r.offset + qs[k];
+      if (is_sub) {
+        qch = litb(r, ls[k] + 1);
+        rch = aligned_char(r, qp);
+        bad = qch != rch;
+      }
+      const uint64_t bm = __ballot(bad);
+      if (bm && bad_idx == INT_MAX) {
+        const int fl = __builtin_ctzll(bm);
+        bad_idx = 64 * k + fl;
+        bad_qp = __shfl(qp, fl, kWave);
+        bad_q = __shfl((int)qch, fl, kWave);
+        bad_r = __shfl((int)rch, fl, kWave);
+      }
+    }
+    if (bad_idx != INT_MAX) {
+      if (lane == 0 && !kLong) {
         pw_aln_result res;
         res.text_off = slot_lo;
         res.text_len = 0;
         res.n_events = 0;
         res.err = PW_REC_MISMATCH;
-        res.err_a = qp;
-        res.err_b = qch;
-        res.err_c = rch;
+        res.err_a = bad_qp;
+        res.err_b = bad_q;
+        res.err_c = bad_r;
         A.results[ai] = res;
       }
       return;
     }
-
-    // ---- event fields (head lanes)
-    Event e;
-    int linelen = 0;
-    if (head) {
-      e.type = typ;
-      e.q_pos = qp;
-      e.ls = ls;
-      if (is_sub) {
-        int n = 1;
-        const uint64_t after = (lane == 63) ? 0ull : (submask >> (lane + 1));
-        const int avail = 63 - lane;
-        const int ones = (int)__builtin_ctzll(~after);  // consecutive SUB lanes after this one
-        n += ones < avail ? ones : avail;
-        if (lane + n == kWave) {  // run reaches the chunk end: continue in the op stream
-          uint32_t j = base + kWave;
-          while (j < r.n_ops && (r.ops[j] >> 30) == PW_OP_SUB) {
-            n++;
-            j++;
-          }
-        }
-        e.n = n;
-      } else {
-        e.n = (int)len;
-      }
-      // final coordinates (pafreport.cpp:562,593-598,611-616,630-640)
-      const int evtlen = is_sub ? 1 : e.n;
-      if (!r.rev) {
-        e.rloc = qp;
-        e.tloc = ts;
-      } else {
-        e.rloc = (typ == PW_OP_INS) ? r.L - qp : r.L - qp - e.n;
-        e.tloc = r.T - ts;
-      }
-      // target context (setTContext, pafreport.cpp:120-128)
-      int tcs = ts - 5;
-      if (tcs < 0) tcs = 0;
-      int tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
-      if (tce >= r.T) tce = r.T - 1;
-      int cl = tce - tcs;
-      if (cl < 0) cl = 0;
-      e.ctx_len = cl;
-      Cursor cur;
-      cur.j = k;
-      cur.ts = ts;
-      cur.qs = qs;
-      cur.ls = ls;
-      cur.w = w;
-      if (cl <= 10 + kMaxEv) {
-        gather_tseq(r, s, cur, tcs, tce, ctx);
-      } else {
-        gather_tseq(r, s, cur, tcs, tcs + 5, ctx);
-        gather_tseq(r, s, cur, tce - 5, tce, ctx + 5);
-      }
-      // query context (getRefContext, pafreport.cpp:721-733)
-      int c0 = e.rloc - 4, eloc = 4;
-      if (c0 < 0) {
-        eloc += c0;
-        c0 = 0;
-      } else if (c0 + 8 >= r.L) {
-        eloc += r.L - c0 - 9;
-        c0 = r.L - 9;
-      }
-      if (c0 < 0) c0 = 0;  // L < 9 is rejected on the host
-      e.rctx0 = c0;
-      e.rctx_loc = eloc;
-      uint8_t rc9[9];
-#pragma unroll
-      for (int j = 0; j < 9; j++) rc9[j] = Rc(r, c0 + j);
-      // homopolymer (hpolyCheck, pafreport.cpp:735-748)
-      const uint8_t b0 = ev_base(r, s, e, 0);
-      bool same = true;
-      for (int i = 1; i < e.n && same; i++) same = ev_base(r, s, e, i) == b0;
-      e.status = 0;
-      if (same) {
-        int l = -1;
-        for (int p = 0; p + 4 <= 9 && l < 0; p++)
-          if (rc9[p] == b0 && rc9[p + 1] == b0 && rc9[p + 2] == b0 && rc9[p + 3] == b0) l = p;
-        if (l >= 0 && l <= eloc && l + 4 >= eloc) e.status = 1;
-      }
-      if (e.status == 0) {  // mmotifCheck: first motif in list order found anywhere
-        for (int m = 0; m < 4 && e.status == 0; m++) {
-          const char* mo = kMotif[m];
-          const int ml = (m < 2) ? 5 : 4;
-          for (int p = 0; p + ml <= 9; p++) {
-            bool hit = true;
-            for (int q = 0; q < ml; q++) hit = hit && rc9[p + q] == (uint8_t)mo[q];
-            if (hit) {
-              e.status = 2 + m;
-              break;
-            }
-          }
-        }
-      }
-      // amino acid at the event (pafreport.cpp:897-899)
-      const int aap0 = e.rloc / 3;
-      e.aa = translate(s, Rc(r, 3 * aap0), Rc(r, 3 * aap0 + 1), Rc(r, 3 * aap0 + 2));
-      e.aapos = aap0 + 1;
-      e.r_trloc = 3 * (e.aapos - 2);
-      if (e.r_trloc < 0) e.r_trloc = 0;
-      e.imp_kind = 0;
-      if (!skip) {
-        if (is_sub) {  // modseq check (pafreport.cpp:811-814)
-          for (int i = 0; i < e.n; i++) {
-            if (to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, s, e, i))) {
-              e.imp_kind = -1 - i;  // failing evtsub index, resolved after the chunk scan
-              break;
-            }
-          }
-        } else {
-          indel_impact(r, s, e);
-        }
-      }
-      CountSink cnt;
-      render(cnt, r, s, e, ctx, skip);
-      linelen = cnt.n;
-    }
-
-    // ---- chunk block placement
-    const uint64_t headmask = __ballot(head);
-    const uint32_t nh = (uint32_t)__popcll(headmask);
-    const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
-    const uint32_t B = bcast(incl, kWave - 1);
-    const int my_off = r.rev ? (int)(B - incl) : (int)(incl - (uint32_t)linelen);
-    // modseq errors: keep the first / last failing event index
+    // compact the heads into the event list
+    const uint32_t n0 = (uint32_t)__popcll(hm[0]);
+    const uint32_t nev = n0 + (uint32_t)__popcll(hm[1]);
     {
-      int fail_i = (head && e.type == PW_OP_SUB && e.imp_kind < 0) ? (-1 - e.imp_kind) : -1;
-      const uint64_t fm = __ballot(fail_i >= 0);
-      if (fm) {
-        const int lo = __builtin_ctzll(fm), hi = 63 - __builtin_clzll(fm);
-        const int gi_lo = (int)ev_base_idx + (int)__popcll(headmask & ((1ull << lo) - 1ull));
-        const int gi_hi = (int)ev_base_idx + (int)__popcll(headmask & ((1ull << hi) - 1ull));
-        const int fi_lo = __shfl(fail_i, lo, kWave), fi_hi = __shfl(fail_i, hi, kWave);
-        const int rl_lo = __shfl(head ? e.rloc : 0, lo, kWave), rl_hi = __shfl(head ? e.rloc : 0, hi, kWave);
-        const int tr_lo = __shfl(head ? e.r_trloc : 0, lo, kWave), tr_hi = __shfl(head ? e.r_trloc : 0, hi, kWave);
-        if (gi_lo < me_first) {
-          me_first = gi_lo;
-          me_fa = rl_lo - tr_lo + fi_lo;
-          me_fb = fi_lo;
-        }
-        if (gi_hi > me_last) {
-          me_last = gi_hi;
-          me_la = rl_hi - tr_hi + fi_hi;
-          me_lb = fi_hi;
+      const uint64_t lt = (1ull << lane) - 1ull;
+      if ((hm[0] >> lane) & 1ull) w->evl[__popcll(hm[0] & lt)] = (uint16_t)lane;
+      if ((hm[1] >> lane) & 1ull) w->evl[n0 + __popcll(hm[1] & lt)] = (uint16_t)(64 + lane);
+    }
+    wave_sync();
+    prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;  // carry into the next segment
+
+    // ---- 7. events, 64 per round: each lane writes its line into its LDS line buffer
+    for (uint32_t e0 = 0; e0 < nev; e0 += kWave) {
+      const uint32_t ei = e0 + lane;
+      const bool act = ei < nev;
+      const uint32_t idx = act ? w->evl[ei] : 0u;
+      int linelen = 0, merr = -1, rel = 0;
+      if (act) {
+        LineSink k;
+        k.buf = my_line;
+        k.junk = w->junk + lane;
+        k.pos = 0;
+        merr = emit_event(k, r, w, idx, sb + idx, skip, ctx, rel);
+        linelen = k.pos;
+      }
+      // modseq errors: first / last failing event of the record (in creation order)
+      {
+        const uint64_t fm = __ballot(merr >= 0);
+        if (fm) {
+          const int lo = __builtin_ctzll(fm), hi = 63 - __builtin_clzll(fm);
+          const int fi_lo = __shfl(merr, lo, kWave), fi_hi = __shfl(merr, hi, kWave);
+          const int rl_lo = __shfl(rel, lo, kWave), rl_hi = __shfl(rel, hi, kWave);
+          const int gi_lo = (int)(ev_idx + e0) + lo, gi_hi = (int)(ev_idx + e0) + hi;
+          if (gi_lo < me_first) {
+            me_first = gi_lo;
+            me_fa = rl_lo + fi_lo;
+            me_fb = fi_lo;
+          }
+          if (gi_hi > me_last) {
+            me_last = gi_hi;
+            me_la = rl_hi + fi_hi;
+            me_lb = fi_hi;
+          }
         }
       }
-      if (head && e.type == PW_OP_SUB && e.imp_kind < 0) e.imp_kind = 0;
-    }
-
-    if (B > 0) {
+      const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
+      const uint32_t B = bcast(incl, kWave - 1);
+      const uint32_t my_off = r.rev ? (B - incl) : (incl - (uint32_t)linelen);
+      if (B == 0) continue;
+      if (out_hi - out_lo < B) {  // host slot bound violated: report, never write outside the slot
+        if (lane == 0 && !kLong) {
+          pw_aln_result res = {};
+          res.text_off = slot_lo;
+          res.err = 3;
+          A.results[ai] = res;
+        }
+        return;
+      }
       uint64_t g0;
       if (!r.rev) {
         g0 = out_lo;
@@ -590,40 +767,81 @@ __device__ void process_record(const pw_report_args& A, Lds& s, uint32_t ai, int
         out_hi -= B;
         g0 = out_hi;
       }
-      for (uint32_t w0 = 0; w0 < B; w0 += kStage) {
-        const uint32_t wn = (B - w0) < (uint32_t)kStage ? (B - w0) : (uint32_t)kStage;
-        if (head && (uint32_t)(my_off + linelen) > w0 && (uint32_t)my_off < w0 + wn) {
-          WriteSink ws;
-          ws.buf = s.stage;
-          ws.pos = my_off;
-          ws.lo = (int)w0;
-          ws.hi = (int)(w0 + wn);
-          render(ws, r, s, e, ctx, skip);
+      const bool is_long = act && linelen > kLine;
+      if (kLong) {  // second pass: rewrite the long lines in place
+        if (is_long) {
+          GlobalSink gk;
+          gk.p = A.text + g0 + my_off;
+          gk.pos = 0;
+          int rl2;
+          emit_event(gk, r, w, idx, sb + idx, skip, ctx, rl2);
         }
-        __syncthreads();
-        uint8_t* dst = A.text + g0 + w0;
-        for (uint32_t i = lane; i < wn; i += kWave) dst[i] = s.stage[i];
-        __syncthreads();
+        continue;
       }
+      any_long = any_long || (__ballot(is_long) != 0ull);
+      // line starts in output order (k-th line = lane k, or lane 63-k for '-' records)
+      {
+        const int kk = r.rev ? kWave - 1 - lane : lane;
+        w->ostart[kk] = my_off;
+        w->olane[kk] = (uint8_t)lane;
+        if (lane == 0) w->ostart[kWave] = B;
+      }
+      wave_sync();
+      // gather: each lane builds 16 output bytes from the line buffers, one 16-byte store
+      uint8_t* const dst = A.text + g0;
+      const uint32_t shift = (uint32_t)((uintptr_t)dst & 15);
+      uint8_t* const gb = dst - shift;  // 16-byte aligned
+      const uint32_t end = shift + B;
+      for (uint32_t c = (uint32_t)lane * 16; c < end; c += kWave * 16) {
+        const uint32_t b0 = c < shift ? 0u : c - shift;  // first output byte of this chunk
+        int kk = 0;  // last line with ostart <= b0
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+          if (kk + step <= kWave - 1 && w->ostart[kk + step] <= b0) kk += step;
+        uint32_t v[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          // output byte; before the slot (chunk 0) it is clamped to 0 so kk never runs ahead
+          const uint32_t b = (c + q < shift) ? 0u : c + q - shift;
+          while (kk < kWave - 1 && w->ostart[kk + 1] <= b) kk++;
+          const uint32_t ln = w->olane[kk];
+          uint32_t o = b - w->ostart[kk];
+          if (o >= (uint32_t)kLine) o = kLine - 1;  // long line: long_lines_kernel rewrites it
+          const uint8_t ch = w->line[ln * kLine + o];
+          v[q >> 2] |= (uint32_t)ch << (8 * (q & 3));
+        }
+        if (c >= shift && c + 16 <= end) {
+          v4u vv;
+          vv.x = v[0];
+          vv.y = v[1];
+          vv.z = v[2];
+          vv.w = v[3];
+          *reinterpret_cast<v4u*>(gb + c) = vv;
+        } else {
+          const uint32_t lo = c < shift ? shift : c, hi = (c + 16 < end) ? c + 16 : end;
+          for (uint32_t bb = lo; bb < hi; bb++) gb[bb] = (uint8_t)(v[(bb - c) >> 2] >> (8 * ((bb - c) & 3)));
+        }
+      }
+      wave_sync();
     }
 
-    // ---- carries
-    qc += (int)bcast(qi_, kWave - 1);
-    tc += (int)bcast(ti_, kWave - 1);
-    lc += bcast(li_, kWave - 1);
-    prev_sub = ((submask >> 63) & 1ull) != 0;
-    ev_base_idx += nh;
+    // ---- 8. carries
+    qc += (int)sq;
+    tc += (int)st;
+    lc += sl;
+    ev_idx += nev;
+    sb += nseg;
   }
 
-  if (lane == 0) {
+  if (lane == 0 && !kLong) {
     pw_aln_result res;
     res.text_off = r.rev ? out_hi : slot_lo;
     res.text_len = (uint32_t)(r.rev ? (slot_hi - out_hi) : (out_lo - slot_lo));
-    res.n_events = ev_base_idx;
-    res.err = PW_REC_OK;
+    res.n_events = ev_idx;
+    res.err = any_long ? kLongFlag : PW_REC_OK;
     res.err_a = res.err_b = res.err_c = 0;
     if (me_last >= 0) {  // first failing event in OUTPUT order
-      res.err = PW_REC_MODSEQ;
+      res.err |= PW_REC_MODSEQ;
       if (!r.rev) {
         res.err_a = me_fa;
         res.err_b = me_fb;
@@ -631,25 +849,48 @@ __device__ void process_record(const pw_report_args& A, Lds& s, uint32_t ai, int
       } else {
         res.err_a = me_la;
         res.err_b = me_lb;
-        res.err_c = (int)ev_base_idx - 1 - me_last;
+        res.err_c = (int)ev_idx - 1 - me_last;
       }
     }
     A.results[ai] = res;
   }
 }
 
+__device__ __forceinline__ void stage_tables(LDS Lds* sp, int lane) {
+  const v4u* src = reinterpret_cast<const v4u*>(&c_tables);
+  LDS v4u* dst = reinterpret_cast<LDS v4u*>(&sp->tab);
+  for (int i = lane; i < (int)(sizeof(Tables) / 16); i += kWave) dst[i] = src[i];
+}
+
 __global__ __launch_bounds__(kWave) void report_kernel(pw_report_args A) {
   __shared__ __attribute__((aligned(16))) Lds s;
+  LDS Lds* sp = (LDS Lds*)&s;
   const int lane = threadIdx.x;
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tables);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&s.tab);
-    for (int i = lane; i < (int)(sizeof(Tables) / 4); i += kWave) dst[i] = src[i];
-  }
+  stage_tables(sp, lane);
   __syncthreads();
   for (uint32_t ai = blockIdx.x; ai < A.n_alns; ai += gridDim.x) {
-    process_record(A, s, ai, lane);
+    process_record<false>(A, sp, ai, lane);
     __syncthreads();
+  }
+}
+
+// Second pass over records flagged by report_kernel: lines longer than kLine are written to
+// their (already reserved) place in the text slot, then the flag is cleared.
+__global__ __launch_bounds__(kWave) void long_lines_kernel(pw_report_args A) {
+  __shared__ __attribute__((aligned(16))) Lds s;
+  LDS Lds* sp = (LDS Lds*)&s;
+  const int lane = threadIdx.x;
+  bool staged = false;
+  for (uint32_t ai = blockIdx.x; ai < A.n_alns; ai += gridDim.x) {
+    if (!(A.results[ai].err & kLongFlag)) continue;
+    if (!staged) {
+      stage_tables(sp, lane);
+      __syncthreads();
+      staged = true;
+    }
+    process_record<true>(A, sp, ai, lane);
+    __syncthreads();
+    if (lane == 0) A.results[ai].err &= ~kLongFlag;
   }
 }
 
@@ -725,6 +966,8 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
   const uint32_t max_blocks = (uint32_t)ncu * 16u;
   const uint32_t grid = args->n_alns < max_blocks ? args->n_alns : max_blocks;
   hipLaunchKernelGGL(pw::report_kernel, dim3(grid), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
+  const uint32_t grid2 = args->n_alns < 1024u ? args->n_alns : 1024u;
+  hipLaunchKernelGGL(pw::long_lines_kernel, dim3(grid2), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
