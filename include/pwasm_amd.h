@@ -185,6 +185,13 @@ int pw_batch_view_get(const pw_batch* b, pw_batch_view* out);
 /* Render the report (headers + event text) for results of a finished batch into `path`. */
 int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                           const char* path);
+/* Shard output for a multi-GPU run: the same bytes as pw_batch_write_report, cut
+ * into items tagged with their 0-based input line ("PWI1", then per item {u64 line, i32 status
+ * (-1 = continue, else the exit code the reference ends with), u32 n_stdout, u32 n_stderr,
+ * stdout bytes, stderr bytes}).  Merging the items of all shards by global line, up to the
+ * first item with status >= 0, reproduces the single-process output (pwasm_amd/shard.py). */
+int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
+                         const char* path);
 void pw_batch_free(pw_batch* b);
 
 const char* pw_version(void);

@@ -31,18 +31,56 @@
 #include <sys/stat.h>
 
 /* ------------------------------------------------------------------ errors */
-/* gclib GError: message to stderr, exit(1).  GMessage: message to stderr. */
+/* gclib GError: message to stderr, exit(1).  GMessage: message to stderr.
+ * With --items <path> (test tooling for the multi-GPU shard merge) everything a
+ * non-comment input line prints goes into one PWI1 item tagged with its 0-based line number. */
+static FILE* g_errf;   /* stderr, or the current item's stderr buffer */
+static FILE* g_items;  /* --items output */
+static FILE* g_item_out;
+static uint64_t g_item_line;
+static char *g_ob, *g_eb;
+static size_t g_on, g_en;
+
+static void item_begin(uint64_t line) {
+  g_item_line = line;
+  g_item_out = open_memstream(&g_ob, &g_on);
+  g_errf = open_memstream(&g_eb, &g_en);
+}
+static void item_end(int32_t status) {
+  if (!g_items || !g_item_out) return;
+  fclose(g_item_out);
+  fclose(g_errf);
+  uint32_t no = (uint32_t)g_on, ne = (uint32_t)g_en;
+  if (no || ne || status >= 0) {
+    fwrite(&g_item_line, 8, 1, g_items);
+    fwrite(&status, 4, 1, g_items);
+    fwrite(&no, 4, 1, g_items);
+    fwrite(&ne, 4, 1, g_items);
+    fwrite(g_ob, 1, no, g_items);
+    fwrite(g_eb, 1, ne, g_items);
+  }
+  free(g_ob);
+  free(g_eb);
+  g_ob = g_eb = NULL;
+  g_item_out = NULL;
+  g_errf = stderr;
+}
 static void gerror(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
-  vfprintf(stderr, fmt, ap);
+  vfprintf(g_errf ? g_errf : stderr, fmt, ap);
   va_end(ap);
+  if (g_items) {
+    item_end(1);
+    fclose(g_items);
+    g_items = NULL;
+  }
   exit(1);
 }
 static void gmessage(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
-  vfprintf(stderr, fmt, ap);
+  vfprintf(g_errf ? g_errf : stderr, fmt, ap);
   va_end(ap);
 }
 
@@ -910,6 +948,14 @@ static char* get_line(FILE* f, gstr* buf) {
 
 int main(int argc, char* argv[]) {
   comp_init();
+  g_errf = stderr;
+  const char* items_path = NULL;
+  if (argc > 2 && strcmp(argv[1], "--items") == 0) { /* test tooling, not a pafreport option */
+    items_path = argv[2];
+    argv[2] = argv[0];
+    argc -= 2;
+    argv += 2;
+  }
   gargs args;
   gargs_parse(&args, argc, argv, "DGFCNvd:p:r:o:m:w:c:s:");
   if (args.err > 0) {
@@ -988,7 +1034,17 @@ int main(int argc, char* argv[]) {
   fa_rec* refseq = NULL;
   char* refseq_rc = NULL; /* reverse complement of the current query */
   char* line;
-  while ((line = get_line(inf, &lbuf)) != NULL) { /* :303-436 */
+  if (items_path) {
+    g_items = fopen(items_path, "wb");
+    if (!g_items) gerror("Cannot open file %s for writing!\n", items_path);
+    fwrite("PWI1", 1, 4, g_items);
+  }
+  uint64_t line_no = 0;
+  for (; (line = get_line(inf, &lbuf)) != NULL; line_no++, item_end(-1)) { /* :303-436 */
+    if (g_items) {
+      item_begin(line_no);
+      freport = g_item_out;
+    }
     if (line[0] == '#') continue;
     gs_set(&lstr, line);
     int numt = strsplit_tab(line, &t, &tcap);
@@ -1053,7 +1109,11 @@ int main(int argc, char* argv[]) {
     print_diff_info(freport, rlabel.s, tlabel.s, &al, alnscore, edist, &tdiffs, refseq->seq, refseq->len);
     td_free(&tdiffs);
   }
-  if (freport != stdout) fclose(freport);
+  if (g_items) {
+    fclose(g_items);
+  } else if (freport != stdout) {
+    fclose(freport);
+  }
   if (inf != stdin) fclose(inf);
   return 0;
 }

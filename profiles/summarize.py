@@ -13,7 +13,9 @@ import sys
 def main(src, out, alg_bytes=None):
     stats = list(csv.DictReader(open(f"{src}/trace/run_kernel_stats.csv")))
     pmc = collections.defaultdict(list)
-    for part in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    import glob
+    import os
+    for part in sorted(os.path.basename(p) for p in glob.glob(f"{src}/pmc_*") if os.path.isdir(p)):
         try:
             for r in csv.DictReader(open(f"{src}/{part}/run_counter_collection.csv")):
                 if "report_kernel" in r["Kernel_Name"]:

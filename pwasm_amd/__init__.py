@@ -15,7 +15,8 @@ import subprocess
 
 ROOT = pathlib.Path(__file__).resolve().parent
 REPO = ROOT.parent
-LIB_PATH = ROOT / "lib" / "libpwasm_amd.so"
+# PWASM_LIB selects another in-tree build of the same library (experiment builds, tools/exp_build.sh)
+LIB_PATH = pathlib.Path(os.environ["PWASM_LIB"]) if os.environ.get("PWASM_LIB") else ROOT / "lib" / "libpwasm_amd.so"
 CLI_PATH = ROOT / "bin" / "pafreport"
 GA_CLI_PATH = ROOT / "bin" / "gapassem_consensus"
 
@@ -85,6 +86,7 @@ _SIGS = {
                                               ctypes.c_size_t]),
     "pw_batch_view_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatchView)]),
     "pw_batch_write_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
+    "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
     "pw_batch_free": (None, [ctypes.c_void_p]),
     "pw_version": (ctypes.c_char_p, []),
     "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
@@ -156,6 +158,10 @@ class HostBatch:
     def write_report(self, text_host, results_host, path: str) -> int:
         """Headers + event text for a finished batch (numpy arrays on the host)."""
         return lib().pw_batch_write_report(self._h, text_host.ctypes.data, results_host.ctypes.data, path.encode())
+
+    def write_items(self, text_host, results_host, path: str) -> int:
+        """The same output cut into line-tagged items (PWI1) for the multi-GPU shard merge."""
+        return lib().pw_batch_write_items(self._h, text_host.ctypes.data, results_host.ctypes.data, path.encode())
 
     def close(self):
         if self._h:

@@ -252,6 +252,7 @@ struct RecHost {
 struct LogItem {
   uint8_t kind;  // 0 message, 1 record, 2 fatal
   uint32_t idx;
+  uint64_t line;  // 0-based input line it came from (shard merge order)
 };
 
 struct Batch {
@@ -281,9 +282,10 @@ struct Batch {
     msgs.push_back(std::move(m));
     return (uint32_t)msgs.size() - 1;
   }
-  void log_msg(std::string m) { log.push_back({0, add_msg(std::move(m))}); }
+  uint64_t cur_line = 0;  // input line being packed
+  void log_msg(std::string m) { log.push_back({0, add_msg(std::move(m)), cur_line}); }
   void log_fatal(std::string m) {
-    log.push_back({2, add_msg(std::move(m))});
+    log.push_back({2, add_msg(std::move(m)), cur_line});
     fatal = true;
   }
 };
@@ -296,9 +298,11 @@ struct Packer {
   Options opt;
   std::unordered_map<std::string, int> alnpairs;  // q~t (gene mode), persists across batches
   std::vector<char*> t;
+  uint64_t n_lines = 0;  // input lines seen (across batches)
 
   // Handle one input line (pafreport.cpp:304-382).  Returns false after a fatal error.
   bool add_line(Batch& b, const char* line0, size_t n) {
+    b.cur_line = n_lines++;
     if (n > 0 && line0[0] == '#') return true;
     const uint32_t loff = (uint32_t)b.text.size();
     b.text.append(line0, n);
@@ -486,7 +490,7 @@ struct Packer {
     b.hdr += hdr;
     b.desc.push_back(d);
     b.recs.push_back(rh);
-    b.log.push_back({1, (uint32_t)b.recs.size() - 1});
+    b.log.push_back({1, (uint32_t)b.recs.size() - 1, b.cur_line});
     return true;
   }
 };
@@ -602,68 +606,76 @@ struct Device {
   }
 };
 
+// Print what the reference prints for one log item; returns -1 to continue, else the exit code
+// the reference ends with at this item.
+int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_aln_result* res, FILE* out,
+              FILE* err) {
+  if (it.kind == 0) {
+    fputs(b.msgs[it.idx].c_str(), err);
+    return -1;
+  }
+  if (it.kind == 2) {
+    fflush(out);
+    fputs(b.msgs[it.idx].c_str(), err);
+    return 1;
+  }
+  const RecHost& rh = b.recs[it.idx];
+  const pw_aln_result& r = res[it.idx];
+  const char* lstr = b.text.data() + rh.line_off;
+  if (rh.pre_msg >= 0) {
+    fputs(b.msgs[rh.pre_msg].c_str(), err);
+    return 1;
+  }
+  if (r.err == PW_REC_MISMATCH) {
+    fprintf(err, "Error: base mismatch %c != qstr[%d] (%c) at line\n%s\n", (char)r.err_b, r.err_a, (char)r.err_c,
+            lstr);
+    return 1;
+  }
+  if (rh.cs_msg >= 0) {
+    fputs(b.msgs[rh.cs_msg].c_str(), err);
+    return 1;
+  }
+  for (int k = 0; k < rh.n_softclip; k++)
+    fprintf(err, "Warning: soft clipping shouldn't be found in this application!\n%s\n", lstr);
+  if (rh.post_msg >= 0) {
+    fputs(b.msgs[rh.post_msg].c_str(), err);
+    return 1;
+  }
+  if (r.err == 3) {
+    fprintf(err, "pafreport: internal error: report slot overflow\n");
+    return 2;
+  }
+  fwrite(b.hdr.data() + rh.hdr_off, 1, rh.hdr_len, out);
+  uint32_t nlines = r.n_events;
+  std::string post;
+  if (rh.qlen < 9 && r.n_events > 0) {
+    nlines = 0;
+    post = "Error: query sequence too short for a 9-nt context\n";
+  } else if (r.err == PW_REC_MODSEQ) {
+    nlines = (uint32_t)r.err_c;
+    post = strf("Error: modseq[%d] not matching di.evtsub[%d] !\n", r.err_a, r.err_b);
+  }
+  const uint8_t* tx = text + r.text_off;
+  if (nlines == r.n_events) {
+    fwrite(tx, 1, r.text_len, out);
+    return -1;
+  }
+  uint32_t pos = 0, seen = 0;
+  while (seen < nlines && pos < r.text_len) {
+    if (tx[pos] == '\n') seen++;
+    pos++;
+  }
+  fwrite(tx, 1, pos, out);
+  fflush(out);
+  fputs(post.c_str(), err);
+  return 1;
+}
+
 // Print what the reference prints for this batch; returns -1 to continue, else an exit code.
 int emit(const Batch& b, const uint8_t* text, const pw_aln_result* res, FILE* out) {
   for (const LogItem& it : b.log) {
-    if (it.kind == 0) {
-      fputs(b.msgs[it.idx].c_str(), stderr);
-      continue;
-    }
-    if (it.kind == 2) {
-      fflush(out);
-      fputs(b.msgs[it.idx].c_str(), stderr);
-      return 1;
-    }
-    const RecHost& rh = b.recs[it.idx];
-    const pw_aln_result& r = res[it.idx];
-    const char* lstr = b.text.data() + rh.line_off;
-    if (rh.pre_msg >= 0) {
-      fputs(b.msgs[rh.pre_msg].c_str(), stderr);
-      return 1;
-    }
-    if (r.err == PW_REC_MISMATCH) {
-      fprintf(stderr, "Error: base mismatch %c != qstr[%d] (%c) at line\n%s\n", (char)r.err_b, r.err_a, (char)r.err_c,
-              lstr);
-      return 1;
-    }
-    if (rh.cs_msg >= 0) {
-      fputs(b.msgs[rh.cs_msg].c_str(), stderr);
-      return 1;
-    }
-    for (int k = 0; k < rh.n_softclip; k++)
-      fprintf(stderr, "Warning: soft clipping shouldn't be found in this application!\n%s\n", lstr);
-    if (rh.post_msg >= 0) {
-      fputs(b.msgs[rh.post_msg].c_str(), stderr);
-      return 1;
-    }
-    if (r.err == 3) {
-      fprintf(stderr, "pafreport: internal error: report slot overflow\n");
-      return 2;
-    }
-    fwrite(b.hdr.data() + rh.hdr_off, 1, rh.hdr_len, out);
-    uint32_t nlines = r.n_events;
-    std::string post;
-    if (rh.qlen < 9 && r.n_events > 0) {
-      nlines = 0;
-      post = "Error: query sequence too short for a 9-nt context\n";
-    } else if (r.err == PW_REC_MODSEQ) {
-      nlines = (uint32_t)r.err_c;
-      post = strf("Error: modseq[%d] not matching di.evtsub[%d] !\n", r.err_a, r.err_b);
-    }
-    const uint8_t* tx = text + r.text_off;
-    if (nlines == r.n_events) {
-      fwrite(tx, 1, r.text_len, out);
-    } else {
-      uint32_t pos = 0, seen = 0;
-      while (seen < nlines && pos < r.text_len) {
-        if (tx[pos] == '\n') seen++;
-        pos++;
-      }
-      fwrite(tx, 1, pos, out);
-      fflush(out);
-      fputs(post.c_str(), stderr);
-      return 1;
-    }
+    const int rc = emit_item(b, it, text, res, out, stderr);
+    if (rc >= 0) return rc;
   }
   return -1;
 }
@@ -987,6 +999,45 @@ extern "C" int pw_batch_write_report(const pw_batch* bt, const uint8_t* text_hos
   int rc = emit(bt->b, text_host, res_host, f);
   fclose(f);
   return rc < 0 ? 0 : rc;
+}
+
+// Item stream of a shard (PWI1): per log item {u64 line, i32 status, u32 n_out,
+// u32 n_err, stdout bytes, stderr bytes}; ends after the first item with status >= 0.
+extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                                    const char* path) {
+  if (!bt || !path) return PW_E_ARG;
+  FILE* f = fopen(path, "wb");
+  if (!f) return PW_E_IO;
+  fwrite("PWI1", 1, 4, f);
+  char *ob = nullptr, *eb = nullptr;
+  size_t on = 0, en = 0;
+  int ret = PW_OK;
+  for (const LogItem& it : bt->b.log) {
+    FILE* o = open_memstream(&ob, &on);
+    FILE* e = open_memstream(&eb, &en);
+    if (!o || !e) {
+      ret = PW_E_NOMEM;
+      if (o) fclose(o);
+      if (e) fclose(e);
+      break;
+    }
+    const int32_t st = emit_item(bt->b, it, text_host, res_host, o, e);
+    fclose(o);
+    fclose(e);
+    const uint32_t no = (uint32_t)on, ne = (uint32_t)en;
+    fwrite(&it.line, 8, 1, f);
+    fwrite(&st, 4, 1, f);
+    fwrite(&no, 4, 1, f);
+    fwrite(&ne, 4, 1, f);
+    fwrite(ob, 1, on, f);
+    fwrite(eb, 1, en, f);
+    free(ob);
+    free(eb);
+    ob = eb = nullptr;
+    if (st >= 0) break;
+  }
+  if (fclose(f) != 0 && ret == PW_OK) ret = PW_E_IO;
+  return ret;
 }
 
 extern "C" void pw_batch_free(pw_batch* bt) { delete bt; }

@@ -54,16 +54,20 @@ constexpr int kQW = 4096;       // forward-query window per wave (bytes)
 constexpr int kQPad = 64;       // context reach beyond a segment's query span
 constexpr int kLW = 1024;       // literal window per wave (bytes)
 constexpr int kLPad = 64;
-constexpr int kLine = 144;      // per-lane report-line buffer (bytes)
+constexpr int kLine = 112;      // per-lane report-line buffer (bytes)
+constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries (rounds without long lines)
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
-constexpr int32_t kLongFlag = 0x100;  // results[].err bit: a line left for long_lines_kernel
+constexpr int32_t kLongFlag = 0x100;
+// Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
+#ifndef PW_ABL
+#define PW_ABL 0
+#endif  // results[].err bit: a line left for long_lines_kernel
 
 struct WaveLds {
   uint8_t line[kWave * kLine];  // per-lane line buffers
   uint8_t qw[kQW];
   uint8_t lw[kLW];
-  uint8_t ctx[kWave * 24];      // per-lane target-context scratch
   uint32_t opw[kSegOps + 2 * kOpHalo];
   int32_t qs[kSegOps];
   int32_t ts[kSegOps];
@@ -71,6 +75,7 @@ struct WaveLds {
   uint32_t ostart[kWave + 1];   // line starts in output order
   uint8_t junk[kWave];
   uint8_t olane[kWave];         // lane of the k-th line in output order
+  uint8_t cmap[kMap];           // 16-byte output chunk -> output index of its first line
   uint16_t evl[kSegOps];
 };
 
@@ -134,7 +139,15 @@ __device__ __forceinline__ uint8_t aligned_char(const Rec& r, int p) {
   return r.rev ? r.tab->comp[Rc(r, r.L - 1 - p)] : Rc(r, p);
 }
 
+// translateCodon: three bases of {A,C,G,T} in either case take one lookup in codon64 (no
+// dependent table reads); anything else goes through the IUPAC mask tables.
+__device__ __forceinline__ bool is_acgt(uint32_t c) {
+  // letters 0x40-0x7F whose low 5 bits are 1 (A), 3 (C), 7 (G) or 20 (T)
+  return (c & 0xC0u) == 0x40u && ((0x0010008Au >> (c & 0x1Fu)) & 1u);
+}
 __device__ __forceinline__ uint8_t translate(const LDS Tables* t, uint8_t a, uint8_t b, uint8_t c) {
+  if (is_acgt(a) && is_acgt(b) && is_acgt(c))
+    return t->codon64[((a >> 1) & 3u) << 4 | ((b >> 1) & 3u) << 2 | ((c >> 1) & 3u)];
   return t->codon[(t->nt[a] << 8) | (t->nt[b] << 4) | t->nt[c]];
 }
 
@@ -152,6 +165,8 @@ __device__ __forceinline__ uint32_t op_ladv(uint32_t w) {
 }
 __device__ __forceinline__ uint8_t to_upper(uint8_t c) { return (c >= 'a' && c <= 'z') ? c - 32 : c; }
 __device__ __forceinline__ uint8_t to_lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+// comp[comp[c]] without the tables: the IUPAC complement is an involution except U/u -> A/a -> T/t
+__device__ __forceinline__ uint8_t comp2(uint8_t c) { return (c | 0x20) == 'u' ? (uint8_t)(c - 1) : c; }
 
 // ------------------------------------------------------------------ event
 struct Event {
@@ -167,45 +182,11 @@ struct Event {
 __device__ __forceinline__ uint8_t ev_base(const Rec& r, const Event& e, int i) {
   if (e.type == PW_OP_SUB) return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i))] : litb(r, e.ls + 2 * i);
   if (e.type == PW_OP_INS) return r.rev ? r.tab->comp[litb(r, e.ls + (e.n - 1 - i))] : litb(r, e.ls + i);
-  return r.rev ? r.tab->comp[r.tab->comp[Rc(r, e.rloc + i)]] : Rc(r, e.q_pos + i);
+  return r.rev ? comp2(Rc(r, e.rloc + i)) : Rc(r, e.q_pos + i);
 }
 // evtsub[i] (S only)
 __device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
   return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i) + 1)] : litb(r, e.ls + 2 * i + 1);
-}
-
-// Gather tseq[p0, p1) (the target segment, pafreport.cpp:543,575,588) by walking the op
-// stream from the event's head op.
-struct Cursor {
-  uint32_t j;
-  int ts, qs;
-  uint32_t ls, w;
-};
-__device__ __forceinline__ void gather_tseq(const Rec& r, Cursor c, int p0, int p1, LDS uint8_t* dst) {
-  while (c.ts > p0 && c.j > 0) {  // step back to the op holding p0
-    c.j--;
-    c.w = opword(r, c.j);
-    c.ts -= (int)op_tadv(c.w);
-    c.qs -= (int)op_qadv(c.w);
-    c.ls -= op_ladv(c.w);
-  }
-  int k = 0;
-  for (int p = p0; p < p1; p++) {
-    while (p >= c.ts + (int)op_tadv(c.w) && c.j + 1 < r.n_ops) {
-      c.ts += (int)op_tadv(c.w);
-      c.qs += (int)op_qadv(c.w);
-      c.ls += op_ladv(c.w);
-      c.j++;
-      c.w = opword(r, c.j);
-    }
-    const uint32_t t = c.w >> 30;
-    const int off = p - c.ts;
-    uint8_t ch;
-    if (t == PW_OP_MATCH) ch = aligned_char(r, r.offset + c.qs + off);
-    else if (t == PW_OP_SUB) ch = to_lower(litb(r, c.ls));
-    else ch = to_lower(litb(r, c.ls + off));
-    dst[k++] = ch;
-  }
 }
 
 // ------------------------------------------------------------------ line sinks
@@ -224,6 +205,7 @@ struct LineSink {
     *((pred && pos < kLine) ? buf + pos : junk) = c;
     pos += pred ? 1 : 0;
   }
+  __device__ __forceinline__ void put_at(int i, uint8_t c) { *(i < kLine ? buf + i : junk) = c; }
 };
 struct GlobalSink {
   uint8_t* p;
@@ -232,11 +214,63 @@ struct GlobalSink {
   __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
     if (pred) p[pos++] = c;
   }
+  __device__ __forceinline__ void put_at(int i, uint8_t c) { p[i] = c; }
 };
+
+// Write tseq[p0, p1) (the target segment, pafreport.cpp:543,575,588 — never materialised) to
+// line positions base.. : in order for '+' records, reverse-complemented for '-' records
+// (revCompl of tctx, pafreport.cpp:631).  Walks the op stream run by run from the cursor.
+struct Cursor {
+  uint32_t j;
+  int ts, qs;
+  uint32_t ls, w;
+};
+template <class S>
+__device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, int p1, int base) {
+  while (c.ts > p0 && c.j > 0) {  // step back to the op holding p0
+    c.j--;
+    c.w = opword(r, c.j);
+    c.ts -= (int)op_tadv(c.w);
+    c.qs -= (int)op_qadv(c.w);
+    c.ls -= op_ladv(c.w);
+  }
+  int p = p0;
+  while (p < p1) {
+    const int tl = (int)op_tadv(c.w);
+    if (p >= c.ts + tl && c.j + 1 < r.n_ops) {
+      c.ts += tl;
+      c.qs += (int)op_qadv(c.w);
+      c.ls += op_ladv(c.w);
+      c.j++;
+      c.w = opword(r, c.j);
+      continue;
+    }
+    int pe = c.ts + tl;
+    if (pe > p1 || pe <= p) pe = p1;  // (pe <= p: past the last op; cannot happen on valid input)
+    const uint32_t t = c.w >> 30;
+    for (; p < pe; p++) {
+      const int off = p - c.ts;
+      uint8_t ch;
+      if (t == PW_OP_MATCH) {
+        const int x = r.offset + c.qs + off;  // aligned-strand query position
+        ch = r.rev ? comp2(Rc(r, r.L - 1 - x)) : Rc(r, x);
+        if (x >= r.L) ch = 0;
+      } else {
+        ch = to_lower(litb(r, t == PW_OP_SUB ? c.ls : c.ls + off));
+        if (r.rev) ch = r.tab->comp[ch];
+      }
+      k.put_at(r.rev ? base + (p1 - 1 - p) : base + (p - p0), ch);
+    }
+  }
+}
 
 // "%d" of a non-negative int
 template <class S>
 __device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
+#if PW_ABL & 8
+  k.put('1'); k.put('2'); k.put('3'); k.put((uint8_t)('0' + (v & 7)));
+  return;
+#endif
   if (v >= 100000u) {
     for (uint32_t P = 1000000000u; P >= 100000u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   }
@@ -333,7 +367,7 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e)
 // receives rloc - r_trloc for the error message.
 template <class S>
 __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds* w, uint32_t idx, uint32_t j,
-                                          bool skip, LDS uint8_t* ctx, int& rel) {
+                                          bool skip, int& rel) {
   Event e;
   const uint32_t wd = w->opw[kOpHalo + idx];
   const uint32_t typ = wd >> 30;
@@ -381,6 +415,11 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
   k.put('\t');
   // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity
   const bool big = e.n > kMaxEv;
+#if PW_ABL & 32
+  const uint8_t b0 = 'A';
+  const bool same = e.n == 1;
+  k.put('A'); k.put(':'); k.put('C');
+#else
   if (typ == PW_OP_SUB) {
     if (big) {
       k.put('[');
@@ -406,10 +445,14 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
     }
   }
   if (typ == PW_OP_DEL) k.put(':');
+#endif
   k.put('\t');
   wr_dig(k, (uint32_t)(tloc + 1));
   k.put('\t');
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
+#if PW_ABL & 1
+  wr_lit(k, "acgtaCGTACG");
+#else
   {
     int tcs = ts - 5;
     if (tcs < 0) tcs = 0;
@@ -423,24 +466,27 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
     cur.qs = qs;
     cur.ls = ls;
     cur.w = wd;
-    const bool abbr = cl > 10 + kMaxEv;
-    if (!abbr) {
-      gather_tseq(r, cur, tcs, tce, ctx);
-      for (int q = 0; q < cl; q++) k.put(r.rev ? r.tab->comp[ctx[cl - 1 - q]] : ctx[q]);
-    } else {
-      gather_tseq(r, cur, tcs, tcs + 5, ctx);
-      gather_tseq(r, cur, tce - 5, tce, ctx + 5);
-#pragma unroll
-      for (int q = 0; q < 5; q++) k.put(r.rev ? r.tab->comp[ctx[9 - q]] : ctx[q]);
+    if (cl <= 10 + kMaxEv) {
+      emit_tseq(k, r, cur, tcs, tce, k.pos);
+      k.pos += cl;
+    } else {  // first5[len-10]last5 of the (oriented) context
+      emit_tseq(k, r, cur, r.rev ? tce - 5 : tcs, r.rev ? tce : tcs + 5, k.pos);
+      k.pos += 5;
       k.put('[');
       wr_dig(k, (uint32_t)(cl - 10));
       k.put(']');
-#pragma unroll
-      for (int q = 0; q < 5; q++) k.put(r.rev ? r.tab->comp[ctx[4 - q]] : ctx[5 + q]);
+      emit_tseq(k, r, cur, r.rev ? tcs : tce - 5, r.rev ? tcs + 5 : tce, k.pos);
+      k.pos += 5;
     }
   }
+#endif
   k.put('\t');
   // ---- query context (getRefContext, pafreport.cpp:721-733) + status
+#if PW_ABL & 4
+  wr_lit(k, "ACGTACGTA\t[unknown]");
+  (void)same;
+  (void)b0;
+#else
   int c0 = e.rloc - 4, eloc = 4;
   if (c0 < 0) {
     eloc += c0;
@@ -492,10 +538,16 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
       default: wr_lit(k, "motif GTAC"); break;
     }
   }
+#endif
   k.put('\t');
   // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
   int modseq_err = -1;
+#if PW_ABL & 2
+  if (!skip) wr_lit(k, "synonymous");
+  if (false) {
+#else
   if (!skip) {
+#endif
     if (typ == PW_OP_SUB) {
       for (int i = 0; i < e.n; i++)
         if (modseq_err < 0 && to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, e, i))) modseq_err = i;
@@ -561,7 +613,6 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
   bool prev_sub = false, any_long = false;
   uint32_t ev_idx = 0;
   int me_first = INT_MAX, me_last = -1, me_fa = 0, me_fb = 0, me_la = 0, me_lb = 0;  // modseq errors
-  LDS uint8_t* ctx = w->ctx + lane * 24;
   LDS uint8_t* my_line = w->line + lane * kLine;
 
   for (uint32_t sb = 0; sb < r.n_ops;) {
@@ -723,7 +774,7 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
         k.buf = my_line;
         k.junk = w->junk + lane;
         k.pos = 0;
-        merr = emit_event(k, r, w, idx, sb + idx, skip, ctx, rel);
+        merr = emit_event(k, r, w, idx, sb + idx, skip, rel);
         linelen = k.pos;
       }
       // modseq errors: first / last failing event of the record (in creation order)
@@ -774,41 +825,74 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
           gk.p = A.text + g0 + my_off;
           gk.pos = 0;
           int rl2;
-          emit_event(gk, r, w, idx, sb + idx, skip, ctx, rl2);
+          emit_event(gk, r, w, idx, sb + idx, skip, rl2);
         }
         continue;
       }
       any_long = any_long || (__ballot(is_long) != 0ull);
-      // line starts in output order (k-th line = lane k, or lane 63-k for '-' records)
-      {
-        const int kk = r.rev ? kWave - 1 - lane : lane;
-        w->ostart[kk] = my_off;
-        w->olane[kk] = (uint8_t)lane;
-        if (lane == 0) w->ostart[kWave] = B;
-      }
-      wave_sync();
-      // gather: each lane builds 16 output bytes from the line buffers, one 16-byte store
+      // line starts in output order (k-th line = lane k, or lane 63-k for '-' records) and the
+      // chunk map: 16-byte chunk ci of the aligned destination -> line holding its first byte
       uint8_t* const dst = A.text + g0;
       const uint32_t shift = (uint32_t)((uintptr_t)dst & 15);
       uint8_t* const gb = dst - shift;  // 16-byte aligned
       const uint32_t end = shift + B;
+      {
+        const int oi = r.rev ? kWave - 1 - lane : lane;
+        w->ostart[oi] = my_off;
+        w->olane[oi] = (uint8_t)lane;
+        if (lane == 0) w->ostart[kWave] = B;
+        if (linelen > 0) {
+          const uint32_t c1 = (my_off + (uint32_t)linelen + shift + 15) >> 4;
+          if (my_off == 0) w->cmap[0] = (uint8_t)oi;
+          for (uint32_t ci = (my_off + shift + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) w->cmap[ci] = (uint8_t)oi;
+        }
+      }
+      wave_sync();
+#if PW_ABL & 16
+      if (true) {
+        wave_sync();
+        continue;
+      }
+#endif
+      // gather: each lane assembles 16 output bytes from (at most a few) line buffers with
+      // aligned dword reads + byte-align shifts, then one 16-byte store
       for (uint32_t c = (uint32_t)lane * 16; c < end; c += kWave * 16) {
-        const uint32_t b0 = c < shift ? 0u : c - shift;  // first output byte of this chunk
-        int kk = 0;  // last line with ostart <= b0
+        const int cb = (int)c - (int)shift;  // output byte at chunk position 0 (< 0 in chunk 0)
+        uint32_t b = cb < 0 ? 0u : (uint32_t)cb;
+        const uint32_t be = (c + 16 - shift < B) ? c + 16 - shift : B;
+        int oi;
+        if ((c >> 4) < (uint32_t)kMap) {
+          oi = w->cmap[c >> 4];
+        } else {  // past the map (rounds with long lines): last line starting at or before b
+          oi = 0;
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-          if (kk + step <= kWave - 1 && w->ostart[kk + step] <= b0) kk += step;
+          for (int step = 32; step >= 1; step >>= 1)
+            if (oi + step <= kWave - 1 && w->ostart[oi + step] <= b) oi += step;
+        }
         uint32_t v[4] = {0u, 0u, 0u, 0u};
+        while (b < be) {
+          const uint32_t s0 = w->ostart[oi], s1 = w->ostart[oi + 1];
+          const uint32_t pe = s1 < be ? s1 : be;
+          if (pe > b) {
+            int x = cb - (int)s0;          // line offset at chunk position 0, >= -15
+            if (x > kLine) x = kLine;      // long line: garbage here, long_lines_kernel rewrites it
+            const int a = (int)w->olane[oi] * kLine + x;
+            const LDS uint32_t* src = reinterpret_cast<const LDS uint32_t*>(w->line + (a & ~3));
+            const uint32_t sh = (uint32_t)a & 3u;
+            uint32_t d[5];
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-          // output byte; before the slot (chunk 0) it is clamped to 0 so kk never runs ahead
-          const uint32_t b = (c + q < shift) ? 0u : c + q - shift;
-          while (kk < kWave - 1 && w->ostart[kk + 1] <= b) kk++;
-          const uint32_t ln = w->olane[kk];
-          uint32_t o = b - w->ostart[kk];
-          if (o >= (uint32_t)kLine) o = kLine - 1;  // long line: long_lines_kernel rewrites it
-          const uint8_t ch = w->line[ln * kLine + o];
-          v[q >> 2] |= (uint32_t)ch << (8 * (q & 3));
+            for (int i = 0; i < 5; i++) d[i] = src[i];
+            const uint32_t qlo = (uint32_t)((int)b - cb), qhi = (uint32_t)((int)pe - cb);
+            const uint32_t m16 = ((1u << qhi) - 1u) & ~((1u << qlo) - 1u);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const uint32_t nib = (m16 >> (4 * i)) & 15u;
+              const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
+              v[i] |= __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) & bm;
+            }
+          }
+          b = pe > b ? pe : b;
+          oi++;
         }
         if (c >= shift && c + 16 <= end) {
           v4u vv;
@@ -881,16 +965,22 @@ __global__ __launch_bounds__(kWave) void long_lines_kernel(pw_report_args A) {
   LDS Lds* sp = (LDS Lds*)&s;
   const int lane = threadIdx.x;
   bool staged = false;
-  for (uint32_t ai = blockIdx.x; ai < A.n_alns; ai += gridDim.x) {
-    if (!(A.results[ai].err & kLongFlag)) continue;
-    if (!staged) {
-      stage_tables(sp, lane);
+  // the flags of 64 records per step, one per lane; flagged records are handled in order
+  for (uint32_t a0 = blockIdx.x * kWave; a0 < A.n_alns; a0 += gridDim.x * kWave) {
+    const uint32_t mine = a0 + lane;
+    uint64_t fl = __ballot(mine < A.n_alns && (A.results[mine].err & kLongFlag));
+    while (fl) {
+      const uint32_t ai = a0 + (uint32_t)__builtin_ctzll(fl);
+      fl &= fl - 1;
+      if (!staged) {
+        stage_tables(sp, lane);
+        __syncthreads();
+        staged = true;
+      }
+      process_record<true>(A, sp, ai, lane);
       __syncthreads();
-      staged = true;
+      if (lane == 0) A.results[ai].err &= ~kLongFlag;
     }
-    process_record<true>(A, sp, ai, lane);
-    __syncthreads();
-    if (lane == 0) A.results[ai].err &= ~kLongFlag;
   }
 }
 
@@ -966,7 +1056,8 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
   const uint32_t max_blocks = (uint32_t)ncu * 16u;
   const uint32_t grid = args->n_alns < max_blocks ? args->n_alns : max_blocks;
   hipLaunchKernelGGL(pw::report_kernel, dim3(grid), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
-  const uint32_t grid2 = args->n_alns < 1024u ? args->n_alns : 1024u;
+  const uint32_t nchunk = (args->n_alns + pw::kWave - 1) / pw::kWave;
+  const uint32_t grid2 = nchunk < max_blocks ? nchunk : max_blocks;
   hipLaunchKernelGGL(pw::long_lines_kernel, dim3(grid2), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }

@@ -8,6 +8,8 @@
 //              indexed by nt[c0]<<8 | nt[c1]<<4 | nt[c2]: NCBI table 1, stop '.', 'X' when any
 //              base is not a nucleotide; degenerate codons give the amino acid common to all
 //              expansions, Asx 'B' / Glx 'Z' for RAY / SAR (parity unpinned off ACGT).
+//  codon64[64] fast path of codon[] for three bases of {A,C,G,T,a,c,g,t}, indexed by the 2-bit
+//              code (c >> 1) & 3 of each base (A=0 C=1 T=2 G=3, either case).
 #pragma once
 #include <stdint.h>
 
@@ -17,6 +19,7 @@ struct Tables {
   uint8_t nt[256];
   uint8_t comp[256];
   uint8_t codon[4096];
+  uint8_t codon64[64];
 };
 
 constexpr char kAA64[65] = "KNKNTTTTRSRSIIMIQHQHPPPPRRRRLLLLEDEDAAAAGGGGVVVV.Y.YSSSS.CWCLFLF";
@@ -73,6 +76,9 @@ constexpr Tables build_tables() {
   }
   for (int i = 0; kIupacDefs[i]; i++) t.comp[(uint8_t)kIupacDefs[i]] = (uint8_t)kIupacComp[i];
   for (int i = 0; i < 4096; i++) t.codon[i] = codon_of_masks(i >> 8, (i >> 4) & 15, i & 15);
+  constexpr int kCodeToAcgt[4] = {0, 1, 3, 2};  // fast code A,C,T,G -> kAA64 index A,C,G,T
+  for (int i = 0; i < 64; i++)
+    t.codon64[i] = (uint8_t)kAA64[16 * kCodeToAcgt[i >> 4] + 4 * kCodeToAcgt[(i >> 2) & 3] + kCodeToAcgt[i & 3]];
   return t;
 }
 

@@ -210,3 +210,27 @@ def test_gapassem_tile_boundaries(built, tmp_path):
     rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.02, "--rows", 40, "--out", lay])
     assert rc == 0, err
     assert ga_same(lay, tmp_path) == 0
+
+
+# ---------------------------------------------------------------- multi-GPU shard path
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_run_on_gpu(built, tmp_path, world):
+    """Each shard through the HIP batch path (the per-rank work of a multi-GPU run, here all on
+    cuda:0), item streams merged by global line: must equal the single-process oracle run."""
+    import torch
+    from pwasm_amd import shard
+    from test_shard import _with_duplicates_and_comments
+    fa, paf = synth_paf(tmp_path, 0, seed=8)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 2)
+    parts = shard.split_paf(dup, world, str(tmp_path))
+    got = []
+    for r, (p, gmap) in enumerate(parts):
+        b = pw.HostBatch(fa, p, 0)
+        dev = pw.stage_batch(b, "cuda:0")
+        pw.run_report(b, dev, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ip = str(tmp_path / f"s{r}.pwi")
+        assert b.write_items(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), ip) == 0
+        got.append((shard.read_items(ip), gmap))
+    out, err, rc = shard.merge_items(got)
+    assert (rc, out, err) == run([ORACLE, "-r", fa, dup])
