@@ -82,12 +82,7 @@ def main():
             rc = pw.lib().pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
                                               int(v.n_queries), dev["next_stop"].data_ptr(), sp)
             assert rc == 0
-        a = pw.ReportArgs()
-        a.desc, a.ops, a.lits = dev["desc"].data_ptr(), dev["ops"].data_ptr(), dev["lits"].data_ptr()
-        a.qseq, a.qoff, a.qlen = dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr()
-        a.next_stop = 0 if v.skip_codan else dev["next_stop"].data_ptr()
-        a.text, a.results = dev["text"].data_ptr(), dev["results"].data_ptr()
-        a.text_total, a.n_alns, a.skip_codan = int(v.text_total), int(v.n_alns), int(v.skip_codan)
+        a = pw.report_args(batch, dev)
         if ev is not None:
             ev[0].record(stream)
         rc = pw.lib().pw_report_events(pw.ctypes.byref(a), sp)

@@ -87,7 +87,13 @@ typedef struct pw_report_args {
   uint64_t text_total;      /* end of the last slot */
   uint32_t n_alns;
   uint32_t skip_codan;      /* 1 = no codon impact column (pafreport.cpp:259-262, 915) */
+  void* workspace;          /* device scratch, 16-byte aligned, >= pw_report_workspace_bytes() */
+  uint64_t workspace_bytes;
 } pw_report_args;
+
+/* Device workspace pw_report_events needs for a batch with at most n_events_max events
+ * (pw_cs_totals.n_events_max summed over the batch; pw_batch_view.n_events_max). */
+uint64_t pw_report_workspace_bytes(uint64_t n_events_max);
 
 /* ---------------------------------------------------------------- device entry points */
 

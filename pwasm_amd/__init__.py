@@ -46,7 +46,8 @@ class ReportArgs(ctypes.Structure):
     _fields_ = [("desc", ctypes.c_void_p), ("ops", ctypes.c_void_p), ("lits", ctypes.c_void_p),
                 ("qseq", ctypes.c_void_p), ("qoff", ctypes.c_void_p), ("qlen", ctypes.c_void_p),
                 ("next_stop", ctypes.c_void_p), ("text", ctypes.c_void_p), ("results", ctypes.c_void_p),
-                ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32)]
+                ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
+                ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64)]
 
 
 class CsTotals(ctypes.Structure):
@@ -86,6 +87,7 @@ _SIGS = {
                                               ctypes.c_size_t]),
     "pw_batch_view_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatchView)]),
     "pw_batch_write_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
+    "pw_report_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
     "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
     "pw_batch_free": (None, [ctypes.c_void_p]),
     "pw_version": (ctypes.c_char_p, []),
@@ -175,15 +177,9 @@ class HostBatch:
             pass
 
 
-def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
-    """Launch pw_stop_table_build (unless -F/-N) + pw_report_events on device tensors in `dev`."""
-    L = lib()
+def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
+    """pw_report_args over the device tensors of stage_batch()."""
     v = batch.view
-    if not v.skip_codan:
-        rc = L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
-                                   int(v.n_queries), dev["next_stop"].data_ptr(), stream_ptr)
-        if rc != 0:
-            raise RuntimeError(f"pw_stop_table_build: {rc}")
     a = ReportArgs()
     a.desc = dev["desc"].data_ptr()
     a.ops = dev["ops"].data_ptr()
@@ -197,6 +193,21 @@ def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
     a.text_total = int(v.text_total)
     a.n_alns = int(v.n_alns)
     a.skip_codan = int(v.skip_codan)
+    a.workspace = dev["work"].data_ptr()
+    a.workspace_bytes = dev["work"].numel()
+    return a
+
+
+def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
+    """Launch pw_stop_table_build (unless -F/-N) + pw_report_events on device tensors in `dev`."""
+    L = lib()
+    v = batch.view
+    if not v.skip_codan:
+        rc = L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                   int(v.n_queries), dev["next_stop"].data_ptr(), stream_ptr)
+        if rc != 0:
+            raise RuntimeError(f"pw_stop_table_build: {rc}")
+    a = report_args(batch, dev)
     rc = L.pw_report_events(ctypes.byref(a), stream_ptr)
     if rc != 0:
         raise RuntimeError(f"pw_report_events: {rc}")
@@ -219,6 +230,8 @@ def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
         dev[name] = torch.from_numpy(arr).to(device)
     dev["next_stop"] = torch.empty(max(int(v.qseq_len), 1), dtype=torch.int32, device=device)
     dev["text"] = torch.empty(max(int(v.text_total), 1), dtype=torch.uint8, device=device)
+    dev["work"] = torch.empty(int(lib().pw_report_workspace_bytes(int(v.n_events_max))), dtype=torch.uint8,
+                              device=device)
     dev["results"] = torch.empty(max(int(v.n_alns), 1) * ctypes.sizeof(AlnResult), dtype=torch.uint8,
                                  device=device)
     return dev

@@ -534,7 +534,7 @@ struct Device {
   DevBuf<int32_t> qlen, next_stop;
   DevBuf<pw_aln_desc> desc;
   DevBuf<uint32_t> ops;
-  DevBuf<uint8_t> lits, text;
+  DevBuf<uint8_t> lits, text, work;
   DevBuf<pw_aln_result> res;
   uint32_t nq = 0;
   bool init(const QueryDb& q, bool skip_codan) {
@@ -569,7 +569,8 @@ struct Device {
     text_h.resize(b.text_total);
     if (na == 0) return true;
     if (!desc.ensure(na) || !ops.ensure(b.ops.size() + 1) || !lits.ensure(b.lits.size() + kDevPad) ||
-        !text.ensure(b.text_total + 1) || !res.ensure(na)) {
+        !text.ensure(b.text_total + 1) || !res.ensure(na) ||
+        !work.ensure(pw_report_workspace_bytes(b.n_events_max))) {
       fprintf(stderr, "pafreport: device allocation failed\n");
       return false;
     }
@@ -591,6 +592,8 @@ struct Device {
     a.text_total = b.text_total;
     a.n_alns = (uint32_t)na;
     a.skip_codan = skip_codan ? 1u : 0u;
+    a.workspace = work.p;
+    a.workspace_bytes = pw_report_workspace_bytes(b.n_events_max);
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
       return false;

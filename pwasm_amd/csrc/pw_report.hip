@@ -22,13 +22,14 @@
 //      pafreport.cpp:556-560; `:0` ops are dropped by the pre-pass so "consecutive" is exact);
 //      heads are compacted into an event list, one event per lane;
 //   4. each lane computes its event and writes the report line, field by field as the values
-//      become known, into its own 144-byte LDS line buffer (stores are unconditional: a
+//      become known, into its own 112-byte LDS line buffer (stores are unconditional: a
 //      masked-off character goes to the lane's junk byte, so there is no per-character branch);
 //   5. a wave prefix-scan of line lengths places the lines in the record's text slot (events of
 //      '-' records back-to-front = the reference's tdiffs.Reverse(), pafreport.cpp:643) and the
 //      lines are gathered 16 bytes per lane into full-width global stores.
-// A line longer than its buffer (an S run with many changed codons) is flagged and re-emitted
-// straight to global memory by long_lines_kernel, launched behind the main kernel.
+// Rare, divergent work is not done in the wave (where one lane taking a slow path stalls all 64):
+// a target context that needs an op walk, and a line longer than its buffer (an S run with many
+// changed codons), get their bytes reserved and are queued for fixup_kernel, launched behind.
 // Workgroups are persistent (grid-stride over records): the 4.6 KB of byte tables are staged
 // into LDS once per workgroup.
 #include <hip/hip_runtime.h>
@@ -58,11 +59,10 @@ constexpr int kLine = 112;      // per-lane report-line buffer (bytes)
 constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries (rounds without long lines)
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
-constexpr int32_t kLongFlag = 0x100;
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
 #ifndef PW_ABL
 #define PW_ABL 0
-#endif  // results[].err bit: a line left for long_lines_kernel
+#endif
 
 struct WaveLds {
   uint8_t line[kWave * kLine];  // per-lane line buffers
@@ -191,7 +191,7 @@ __device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
 
 // ------------------------------------------------------------------ line sinks
 // LineSink writes into the lane's LDS line buffer; a store past the buffer or a masked-off
-// character goes to the lane's junk byte (no branch).  GlobalSink (long_lines_kernel) writes
+// character goes to the lane's junk byte (no branch).  GlobalSink (fixup_kernel) writes
 // the line straight to its place in the text slot.
 struct LineSink {
   LDS uint8_t* buf;
@@ -284,6 +284,99 @@ __device__ __forceinline__ void wr_lit(S& k, const char (&s)[N]) {
   for (int i = 0; i < N - 1; i++) k.put((uint8_t)s[i]);
 }
 
+// evtbases length of the event headed by op j: the run of directly consecutive '*' ops
+// (pafreport.cpp:556-560) or the indel length
+__device__ __forceinline__ int event_len(const Rec& r, uint32_t j, uint32_t wd) {
+  if ((wd >> 30) != PW_OP_SUB) return (int)(wd & 0x3FFFFFFFu);
+  int n = 1;
+  uint32_t kk = j + 1;
+  while (kk < r.n_ops && (opword(r, kk) >> 30) == PW_OP_SUB) {
+    n++;
+    kk++;
+  }
+  return n;
+}
+
+// Length of the tctx field for a context of cl target bases (abbreviated past 10+MAX_EVLEN).
+__device__ __forceinline__ int tctx_field_len(int cl) {
+  if (cl <= 10 + kMaxEv) return cl;
+  const uint32_t v = (uint32_t)(cl - 10);
+  return 12 + 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
+         (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
+}
+
+// The tctx field (setTContext, pafreport.cpp:120-128; revCompl :631; abbreviation :918-927).
+// Fast path — match runs of >= 5 on both sides (the common case): query bytes, the event's own
+// target bases, query bytes, no op walk.  Otherwise the context is gathered by walking the op
+// stream; with `defer` that walk is not done here: the field's bytes are skipped (its length is
+// known) and the return value is its position in the line, for fixup_kernel to fill.
+template <class S>
+__device__ __forceinline__ int emit_tctx(S& k, const Rec& r, uint32_t typ, int n, uint32_t j, uint32_t wd, int qs,
+                                         int ts, uint32_t ls, bool defer) {
+  const int qp = r.offset + qs;
+  const int evtlen = typ == PW_OP_SUB ? 1 : n;  // merged S keeps evtlen 1 (pafreport.cpp:562)
+  int tcs = ts - 5;
+  if (tcs < 0) tcs = 0;
+  int tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
+  if (tce >= r.T) tce = r.T - 1;
+  int cl = tce - tcs;
+  if (cl < 0) cl = 0;
+  const int ll = ts - tcs;                                          // target bases before
+  const int nm = typ == PW_OP_DEL ? 0 : (typ == PW_OP_SUB ? 1 : n);  // the event's own
+  const int rl = tce - (ts + nm);                                   // bases after
+  const uint32_t pw = (ll > 0 && j > 0) ? opword(r, j - 1) : 0u;
+  const uint32_t aw = (rl > 0 && j + 1 < r.n_ops) ? opword(r, j + 1) : 0u;
+  const bool fast = cl <= 10 + kMaxEv && (typ != PW_OP_SUB || n == 1) && rl >= 0 &&
+                    (ll == 0 || (j > 0 && (pw >> 30) == PW_OP_MATCH && (int)(pw & 0x3FFFFFFFu) >= ll)) &&
+                    (rl == 0 || (j + 1 < r.n_ops && (aw >> 30) == PW_OP_MATCH && (int)(aw & 0x3FFFFFFFu) >= rl));
+  if (fast) {
+    // aligned query start after the event; '-' records read the forward query in the other
+    // order (revCompl of tctx: comp(comp(x)) = x up to U)
+    const int qpa = qp + (typ == PW_OP_SUB ? 1 : (typ == PW_OP_DEL ? n : 0));
+    const int f1 = r.rev ? r.L - qpa - rl : qp - ll, n1 = r.rev ? rl : ll;
+    const int f2 = r.rev ? r.L - qp : qpa, n2 = r.rev ? ll : rl;
+    uint8_t c1[5], c2[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      c1[q] = Rc(r, f1 + q);
+      c2[q] = Rc(r, f2 + q);
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) k.put_if(q < n1, r.rev ? comp2(c1[q]) : c1[q]);
+    for (int q = 0; q < nm; q++) {
+      uint8_t ch = to_lower(litb(r, ls + (typ == PW_OP_SUB ? 0u : (uint32_t)(r.rev ? nm - 1 - q : q))));
+      k.put(r.rev ? r.tab->comp[ch] : ch);
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) k.put_if(q < n2, r.rev ? comp2(c2[q]) : c2[q]);
+    return -1;
+  }
+  if (defer) {
+    const int at = k.pos;
+    k.pos += tctx_field_len(cl);
+    return at;
+  }
+  Cursor cur;
+  cur.j = j;
+  cur.ts = ts;
+  cur.qs = qs;
+  cur.ls = ls;
+  cur.w = wd;
+  if (cl <= 10 + kMaxEv) {
+    emit_tseq(k, r, cur, tcs, tce, k.pos);
+    k.pos += cl;
+  } else {  // first5[len-10]last5 of the (oriented) context
+    emit_tseq(k, r, cur, r.rev ? tce - 5 : tcs, r.rev ? tce : tcs + 5, k.pos);
+    k.pos += 5;
+    k.put('[');
+    wr_dig(k, (uint32_t)(cl - 10));
+    k.put(']');
+    emit_tseq(k, r, cur, r.rev ? tcs : tce - 5, r.rev ? tcs + 5 : tce, k.pos);
+    k.pos += 5;
+  }
+  return -1;
+}
+
 // S consequence, one codon of modseq (predictImpact, pafreport.cpp:811-826)
 __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, uint8_t& aa, uint8_t& maa) {
   const int p0 = e.rloc - e.r_trloc;
@@ -311,39 +404,89 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e)
   const int sfx = e.rloc + dl;
   const int M = (r.L - e.r_trloc) + x - dl;
   const int trlen = r.L - e.r_trloc;
-  int E = a + x;
-  if (E < 15) E = 15;
   int stop_i = -1;
   uint32_t aa4 = 0, maa4 = 0;
   int aa4n = 0, maa4n = 0;
-  int i = 0;
-  for (; i + 2 < M && i < E; i += 3) {
-    uint8_t m[3];
+  if (a + x <= 15) {
+    // the reference scans codons i = 0,3,..,12 (while i+2 < M), stopping at the first stop;
+    // here all five codons and the four reference codons are read and translated at once
+    // (independent reads, no loop-carried latency) and the scan is replayed on the results
+    uint8_t m[15];
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const int p = i + j;
-      m[j] = (p < a) ? Rc(r, e.r_trloc + p) : (p < a + x ? ev_base(r, e, p - a) : Rc(r, sfx + p - a - x));
+    for (int p = 0; p < 15; p++) {
+      const uint8_t q = Rc(r, p < a ? e.r_trloc + p : sfx + p - a - x);
+      const int ii = p - a;
+      const uint32_t li = e.ls + (uint32_t)(r.rev ? x - 1 - ii : ii);
+      const uint8_t ib = (ii >= 0 && ii < x) ? litb(r, li) : (uint8_t)0;
+      m[p] = (ii >= 0 && ii < x) ? (r.rev ? r.tab->comp[ib] : ib) : q;
     }
-    const uint8_t mm = translate(r.tab, m[0], m[1], m[2]);
-    if (mm == '.') {
-      stop_i = i;
-      break;
+    uint8_t mm[5], rr[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+      mm[c] = translate(r.tab, m[3 * c], m[3 * c + 1], m[3 * c + 2]);
+      rr[c] = c == 0 ? 0 : translate(r.tab, Rc(r, e.r_trloc + 3 * c), Rc(r, e.r_trloc + 3 * c + 1),
+                                     Rc(r, e.r_trloc + 3 * c + 2));
     }
-    if (i > 0 && maa4n < 4) {
-      if (i + 2 < trlen) {
-        aa4 |= (uint32_t)translate(r.tab, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1), Rc(r, e.r_trloc + i + 2))
-               << (8 * aa4n);
-        aa4n++;
+    int stopc = 5, nvalid = 0;
+#pragma unroll
+    for (int c = 4; c >= 0; c--) {
+      const bool valid = 3 * c + 2 < M;
+      if (valid && mm[c] == '.') stopc = c;
+      nvalid += valid ? 1 : 0;
+    }
+    const int last = stopc < nvalid ? stopc : nvalid;  // codons scanned without a stop: [0, last)
+#pragma unroll
+    for (int c = 1; c < 5; c++) {
+      if (c < last) {
+        if (3 * c + 2 < trlen) {
+          aa4 |= (uint32_t)rr[c] << (8 * aa4n);
+          aa4n++;
+        }
+        maa4 |= (uint32_t)mm[c] << (8 * maa4n);
+        maa4n++;
       }
-      maa4 |= (uint32_t)mm << (8 * maa4n);
-      maa4n++;
     }
-  }
-  if (stop_i < 0 && i + 2 < M && r.NS) {
-    const int k0 = sfx + (i - a - x);
-    if (k0 >= 0 && k0 < r.L) {
-      const int st = r.NS[k0];
-      if (st != kNoStop) stop_i = st - sfx + a + x;
+    if (stopc < nvalid) {
+      stop_i = 3 * stopc;
+    } else if (nvalid == 5 && 15 + 2 < M && r.NS) {
+      const int k0 = sfx + (15 - a - x);
+      if (k0 >= 0 && k0 < r.L) {
+        const int st = r.NS[k0];
+        if (st != kNoStop) stop_i = st - sfx + a + x;
+      }
+    }
+  } else {  // long insertion: the reference loop as is
+    const int E = a + x;
+    int i = 0;
+    for (; i + 2 < M && i < E; i += 3) {
+      uint8_t m[3];
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const int p = i + j;
+        m[j] = (p < a) ? Rc(r, e.r_trloc + p) : (p < a + x ? ev_base(r, e, p - a) : Rc(r, sfx + p - a - x));
+      }
+      const uint8_t mm = translate(r.tab, m[0], m[1], m[2]);
+      if (mm == '.') {
+        stop_i = i;
+        break;
+      }
+      if (i > 0 && maa4n < 4) {
+        if (i + 2 < trlen) {
+          aa4 |= (uint32_t)translate(r.tab, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1),
+                                     Rc(r, e.r_trloc + i + 2))
+                 << (8 * aa4n);
+          aa4n++;
+        }
+        maa4 |= (uint32_t)mm << (8 * maa4n);
+        maa4n++;
+      }
+    }
+    if (stop_i < 0 && i + 2 < M && r.NS) {
+      const int k0 = sfx + (i - a - x);
+      if (k0 >= 0 && k0 < r.L) {
+        const int st = r.NS[k0];
+        if (st != kNoStop) stop_i = st - sfx + a + x;
+      }
     }
   }
   if (stop_i >= 0) {
@@ -366,29 +509,15 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e)
 // Returns the evtsub index failing the modseq check (pafreport.cpp:811-814), or -1; `rel`
 // receives rloc - r_trloc for the error message.
 template <class S>
-__device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds* w, uint32_t idx, uint32_t j,
-                                          bool skip, int& rel) {
+__device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32_t wd, int qs, int ts, uint32_t ls,
+                                          bool skip, bool defer, int& rel, int& tpos) {
   Event e;
-  const uint32_t wd = w->opw[kOpHalo + idx];
   const uint32_t typ = wd >> 30;
-  const int qs = w->qs[idx], ts = w->ts[idx];
-  const uint32_t ls = w->ls[idx];
   const int qp = r.offset + qs;
   e.type = typ;
   e.q_pos = qp;
   e.ls = ls;
-  if (typ == PW_OP_SUB) {  // run of directly consecutive '*' ops (pafreport.cpp:556-560)
-    int n = 1;
-    uint32_t kk = j + 1;
-    while (kk < r.n_ops && (opword(r, kk) >> 30) == PW_OP_SUB) {
-      n++;
-      kk++;
-    }
-    e.n = n;
-  } else {
-    e.n = (int)(wd & 0x3FFFFFFFu);
-  }
-  const int evtlen = typ == PW_OP_SUB ? 1 : e.n;  // merged S keeps evtlen 1 (pafreport.cpp:562)
+  e.n = event_len(r, j, wd);
   int tloc;
   if (!r.rev) {
     e.rloc = qp;
@@ -450,36 +579,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
   wr_dig(k, (uint32_t)(tloc + 1));
   k.put('\t');
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
-#if PW_ABL & 1
-  wr_lit(k, "acgtaCGTACG");
-#else
-  {
-    int tcs = ts - 5;
-    if (tcs < 0) tcs = 0;
-    int tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
-    if (tce >= r.T) tce = r.T - 1;
-    int cl = tce - tcs;
-    if (cl < 0) cl = 0;
-    Cursor cur;
-    cur.j = j;
-    cur.ts = ts;
-    cur.qs = qs;
-    cur.ls = ls;
-    cur.w = wd;
-    if (cl <= 10 + kMaxEv) {
-      emit_tseq(k, r, cur, tcs, tce, k.pos);
-      k.pos += cl;
-    } else {  // first5[len-10]last5 of the (oriented) context
-      emit_tseq(k, r, cur, r.rev ? tce - 5 : tcs, r.rev ? tce : tcs + 5, k.pos);
-      k.pos += 5;
-      k.put('[');
-      wr_dig(k, (uint32_t)(cl - 10));
-      k.put(']');
-      emit_tseq(k, r, cur, r.rev ? tcs : tce - 5, r.rev ? tcs + 5 : tce, k.pos);
-      k.pos += 5;
-    }
-  }
-#endif
+  tpos = emit_tctx(k, r, typ, e.n, j, wd, qs, ts, ls, defer);
   k.put('\t');
   // ---- query context (getRefContext, pafreport.cpp:721-733) + status
 #if PW_ABL & 4
@@ -529,14 +629,10 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
       m3 = m3 || v4 == 0x43415447u;                 // "GTAC"
     }
     const int st = (same && l >= 0 && l <= eloc && l + 4 >= eloc) ? 1 : (m0 ? 2 : (m1 ? 3 : (m2 ? 4 : (m3 ? 5 : 0))));
-    switch (st) {
-      case 0: wr_lit(k, "[unknown]"); break;
-      case 1: wr_lit(k, "homopolymer"); break;
-      case 2: wr_lit(k, "motif CCTGG"); break;
-      case 3: wr_lit(k, "motif CCAGG"); break;
-      case 4: wr_lit(k, "motif GATC"); break;
-      default: wr_lit(k, "motif GTAC"); break;
-    }
+    const LDS uint8_t* sw = r.tab->status[st];  // one table row, no divergent literal writes
+    const int sl = sw[11];
+#pragma unroll
+    for (int q = 0; q < 11; q++) k.put_if(q < sl, sw[q]);
   }
 #endif
   k.put('\t');
@@ -547,6 +643,16 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
   if (false) {
 #else
   if (!skip) {
+#endif
+#if PW_ABL & 128
+    if (typ == PW_OP_SUB) {
+      wr_lit(k, "synonymous");
+    } else
+#endif
+#if PW_ABL & 256
+    if (typ != PW_OP_SUB) {
+      wr_lit(k, "premature stop at AA1");
+    } else
 #endif
     if (typ == PW_OP_SUB) {
       for (int i = 0; i < e.n; i++)
@@ -582,10 +688,23 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const LDS WaveLds*
 }
 
 // ------------------------------------------------------------------ per-record driver
-// kLong: long_lines_kernel instance — only flagged records, only lines longer than kLine,
-// written straight to the text slot.
-template <bool kLong>
-__device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds* S, uint32_t ai, int lane) {
+// Work left for fixup_kernel: a target context that needs the op walk (pos = its position in
+// the line) or a whole line longer than the LDS line buffer (pos = kFixLine).
+struct Fixup {
+  uint32_t ai, j;
+  int32_t qs, ts;
+  uint32_t ls, pos;
+  uint64_t dst;  // text offset of the line
+};
+constexpr uint32_t kFixLine = 0x80000000u;
+struct FixList {
+  Fixup* list;
+  uint32_t* count;
+  uint32_t cap;
+};
+
+__device__ __forceinline__ void process_record(const pw_report_args& A, const FixList& F, LDS Lds* S, uint32_t ai,
+                                               int lane) {
   LDS WaveLds* w = &S->w;
   const pw_aln_desc d = A.desc[ai];
   const uint32_t qi = d.ref & 0x7FFFFFFFu;
@@ -610,7 +729,7 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
 
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
-  bool prev_sub = false, any_long = false;
+  bool prev_sub = false, fix_overflow = false;
   uint32_t ev_idx = 0;
   int me_first = INT_MAX, me_last = -1, me_fa = 0, me_fb = 0, me_la = 0, me_lb = 0;  // modseq errors
   LDS uint8_t* my_line = w->line + lane * kLine;
@@ -739,7 +858,7 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
       }
     }
     if (bad_idx != INT_MAX) {
-      if (lane == 0 && !kLong) {
+      if (lane == 0) {
         pw_aln_result res;
         res.text_off = slot_lo;
         res.text_len = 0;
@@ -768,13 +887,14 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
       const uint32_t ei = e0 + lane;
       const bool act = ei < nev;
       const uint32_t idx = act ? w->evl[ei] : 0u;
-      int linelen = 0, merr = -1, rel = 0;
+      int linelen = 0, merr = -1, rel = 0, tpos = -1;
       if (act) {
         LineSink k;
         k.buf = my_line;
         k.junk = w->junk + lane;
         k.pos = 0;
-        merr = emit_event(k, r, w, idx, sb + idx, skip, rel);
+        merr = emit_event(k, r, sb + idx, w->opw[kOpHalo + idx], w->qs[idx], w->ts[idx], w->ls[idx], skip, true,
+                          rel, tpos);
         linelen = k.pos;
       }
       // modseq errors: first / last failing event of the record (in creation order)
@@ -802,7 +922,7 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
       const uint32_t my_off = r.rev ? (B - incl) : (incl - (uint32_t)linelen);
       if (B == 0) continue;
       if (out_hi - out_lo < B) {  // host slot bound violated: report, never write outside the slot
-        if (lane == 0 && !kLong) {
+        if (lane == 0) {
           pw_aln_result res = {};
           res.text_off = slot_lo;
           res.err = 3;
@@ -818,18 +938,29 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
         out_hi -= B;
         g0 = out_hi;
       }
-      const bool is_long = act && linelen > kLine;
-      if (kLong) {  // second pass: rewrite the long lines in place
-        if (is_long) {
-          GlobalSink gk;
-          gk.p = A.text + g0 + my_off;
-          gk.pos = 0;
-          int rl2;
-          emit_event(gk, r, w, idx, sb + idx, skip, rl2);
+      // deferred work -> fixup list (one wave-aggregated atomic)
+      {
+        const bool need = act && (linelen > kLine || tpos >= 0);
+        const uint64_t nm = __ballot(need);
+        if (nm) {
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(F.count, (uint32_t)__popcll(nm));
+          base = bcast(base, 0);
+          const uint32_t slot = base + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+          if (need && slot < F.cap) {
+            Fixup f;
+            f.ai = ai;
+            f.j = sb + idx;
+            f.qs = w->qs[idx];
+            f.ts = w->ts[idx];
+            f.ls = w->ls[idx];
+            f.pos = linelen > kLine ? kFixLine : (uint32_t)tpos;
+            f.dst = g0 + my_off;
+            F.list[slot] = f;
+          }
+          fix_overflow = fix_overflow || (__ballot(need && slot >= F.cap) != 0ull);
         }
-        continue;
       }
-      any_long = any_long || (__ballot(is_long) != 0ull);
       // line starts in output order (k-th line = lane k, or lane 63-k for '-' records) and the
       // chunk map: 16-byte chunk ci of the aligned destination -> line holding its first byte
       uint8_t* const dst = A.text + g0;
@@ -875,7 +1006,7 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
           const uint32_t pe = s1 < be ? s1 : be;
           if (pe > b) {
             int x = cb - (int)s0;          // line offset at chunk position 0, >= -15
-            if (x > kLine) x = kLine;      // long line: garbage here, long_lines_kernel rewrites it
+            if (x > kLine) x = kLine;      // long line: garbage here, fixup_kernel rewrites it
             const int a = (int)w->olane[oi] * kLine + x;
             const LDS uint32_t* src = reinterpret_cast<const LDS uint32_t*>(w->line + (a & ~3));
             const uint32_t sh = (uint32_t)a & 3u;
@@ -917,12 +1048,12 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, LDS Lds*
     sb += nseg;
   }
 
-  if (lane == 0 && !kLong) {
+  if (lane == 0) {
     pw_aln_result res;
     res.text_off = r.rev ? out_hi : slot_lo;
     res.text_len = (uint32_t)(r.rev ? (slot_hi - out_hi) : (out_lo - slot_lo));
     res.n_events = ev_idx;
-    res.err = any_long ? kLongFlag : PW_REC_OK;
+    res.err = fix_overflow ? 3 : PW_REC_OK;
     res.err_a = res.err_b = res.err_c = 0;
     if (me_last >= 0) {  // first failing event in OUTPUT order
       res.err |= PW_REC_MODSEQ;
@@ -946,40 +1077,63 @@ __device__ __forceinline__ void stage_tables(LDS Lds* sp, int lane) {
   for (int i = lane; i < (int)(sizeof(Tables) / 16); i += kWave) dst[i] = src[i];
 }
 
-__global__ __launch_bounds__(kWave) void report_kernel(pw_report_args A) {
+__global__ __launch_bounds__(kWave) void report_kernel(pw_report_args A, FixList F) {
   __shared__ __attribute__((aligned(16))) Lds s;
   LDS Lds* sp = (LDS Lds*)&s;
   const int lane = threadIdx.x;
   stage_tables(sp, lane);
   __syncthreads();
   for (uint32_t ai = blockIdx.x; ai < A.n_alns; ai += gridDim.x) {
-    process_record<false>(A, sp, ai, lane);
+    process_record(A, F, sp, ai, lane);
     __syncthreads();
   }
 }
 
-// Second pass over records flagged by report_kernel: lines longer than kLine are written to
-// their (already reserved) place in the text slot, then the flag is cleared.
-__global__ __launch_bounds__(kWave) void long_lines_kernel(pw_report_args A) {
-  __shared__ __attribute__((aligned(16))) Lds s;
-  LDS Lds* sp = (LDS Lds*)&s;
-  const int lane = threadIdx.x;
-  bool staged = false;
-  // the flags of 64 records per step, one per lane; flagged records are handled in order
-  for (uint32_t a0 = blockIdx.x * kWave; a0 < A.n_alns; a0 += gridDim.x * kWave) {
-    const uint32_t mine = a0 + lane;
-    uint64_t fl = __ballot(mine < A.n_alns && (A.results[mine].err & kLongFlag));
-    while (fl) {
-      const uint32_t ai = a0 + (uint32_t)__builtin_ctzll(fl);
-      fl &= fl - 1;
-      if (!staged) {
-        stage_tables(sp, lane);
-        __syncthreads();
-        staged = true;
-      }
-      process_record<true>(A, sp, ai, lane);
-      __syncthreads();
-      if (lane == 0) A.results[ai].err &= ~kLongFlag;
+// Deferred work of report_kernel, one entry per thread: the op-walk target contexts and the
+// lines longer than the LDS line buffer, written in place (their bytes were reserved).  The
+// record is read straight from global memory (empty LDS windows).
+__global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, FixList F) {
+  __shared__ __attribute__((aligned(16))) Tables tab;
+  {
+    const v4u* src = reinterpret_cast<const v4u*>(&c_tables);
+    LDS v4u* dst = reinterpret_cast<LDS v4u*>((LDS Tables*)&tab);
+    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += 256) dst[i] = src[i];
+  }
+  __syncthreads();
+  const uint32_t n = min(*F.count, F.cap);
+  const bool skip = A.skip_codan != 0;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const Fixup f = F.list[i];
+    const pw_aln_desc d = A.desc[f.ai];
+    const uint32_t qi = d.ref & 0x7FFFFFFFu;
+    Rec r;
+    r.ops = A.ops + d.op_begin;
+    r.lits = A.lits;
+    r.R = A.qseq + A.qoff[qi];
+    r.L = A.qlen[qi];
+    r.NS = A.next_stop ? A.next_stop + A.qoff[qi] : nullptr;
+    r.tab = (const LDS Tables*)&tab;
+    r.qw = r.lw = (const LDS uint8_t*)&tab;  // windows empty: every read goes to global memory
+    r.opw = (const LDS uint32_t*)&tab;
+    r.qlo = -(1 << 30);
+    r.l_lo = 0;
+    r.l_n = 0;
+    r.op_lo = 0;
+    r.op_n = 0;
+    r.offset = d.offset;
+    r.T = d.t_len;
+    r.n_ops = d.n_ops;
+    r.rev = (d.ref & PW_REF_REVERSE) != 0;
+    const uint32_t wd = r.ops[f.j];
+    GlobalSink g;
+    g.pos = 0;
+    if (f.pos == kFixLine) {
+      g.p = A.text + f.dst;
+      int rel, tpos;
+      emit_event(g, r, f.j, wd, f.qs, f.ts, f.ls, skip, false, rel, tpos);
+    } else {
+      g.p = A.text + f.dst + f.pos;
+      emit_tctx(g, r, wd >> 30, event_len(r, f.j, wd), f.j, wd, f.qs, f.ts, f.ls, false);
     }
   }
 }
@@ -1042,23 +1196,34 @@ __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, co
 
 }  // namespace pw
 
+extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max) {
+  return 64u + sizeof(pw::Fixup) * (n_events_max ? n_events_max : 1u);
+}
+
 extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
   if (!args || !args->desc || !args->ops || !args->qseq || !args->qoff || !args->qlen || !args->results ||
       (!args->text && args->text_total))
     return PW_E_ARG;
   if (!args->skip_codan && !args->next_stop) return PW_E_ARG;
+  if (!args->workspace || args->workspace_bytes < pw_report_workspace_bytes(1) ||
+      ((uintptr_t)args->workspace & 15))
+    return PW_E_ARG;
   if (args->n_alns == 0) return PW_OK;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
   }
+  pw::FixList F;
+  F.count = static_cast<uint32_t*>(args->workspace);
+  F.list = reinterpret_cast<pw::Fixup*>(static_cast<uint8_t*>(args->workspace) + 64);
+  const uint64_t cap = (args->workspace_bytes - 64) / sizeof(pw::Fixup);
+  F.cap = cap > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap;
+  if (hipMemsetAsync(F.count, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return PW_E_HIP;
   const uint32_t max_blocks = (uint32_t)ncu * 16u;
   const uint32_t grid = args->n_alns < max_blocks ? args->n_alns : max_blocks;
-  hipLaunchKernelGGL(pw::report_kernel, dim3(grid), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
-  const uint32_t nchunk = (args->n_alns + pw::kWave - 1) / pw::kWave;
-  const uint32_t grid2 = nchunk < max_blocks ? nchunk : max_blocks;
-  hipLaunchKernelGGL(pw::long_lines_kernel, dim3(grid2), dim3(pw::kWave), 0, (hipStream_t)stream, *args);
+  hipLaunchKernelGGL(pw::report_kernel, dim3(grid), dim3(pw::kWave), 0, (hipStream_t)stream, *args, F);
+  hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu * 2u), dim3(256), 0, (hipStream_t)stream, *args, F);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 

@@ -8,6 +8,7 @@
 //              indexed by nt[c0]<<8 | nt[c1]<<4 | nt[c2]: NCBI table 1, stop '.', 'X' when any
 //              base is not a nucleotide; degenerate codons give the amino acid common to all
 //              expansions, Asx 'B' / Glx 'Z' for RAY / SAR (parity unpinned off ACGT).
+//  status      the hpolyCheck/mmotifCheck status words, indexed by status id (0 = unknown)
 //  codon64[64] fast path of codon[] for three bases of {A,C,G,T,a,c,g,t}, indexed by the 2-bit
 //              code (c >> 1) & 3 of each base (A=0 C=1 T=2 G=3, either case).
 #pragma once
@@ -20,6 +21,7 @@ struct Tables {
   uint8_t comp[256];
   uint8_t codon[4096];
   uint8_t codon64[64];
+  uint8_t status[8][12];  // printDiffInfo status words (pafreport.cpp:904-917), length in [11]
 };
 
 constexpr char kAA64[65] = "KNKNTTTTRSRSIIMIQHQHPPPPRRRRLLLLEDEDAAAAGGGGVVVV.Y.YSSSS.CWCLFLF";
@@ -79,6 +81,16 @@ constexpr Tables build_tables() {
   constexpr int kCodeToAcgt[4] = {0, 1, 3, 2};  // fast code A,C,T,G -> kAA64 index A,C,G,T
   for (int i = 0; i < 64; i++)
     t.codon64[i] = (uint8_t)kAA64[16 * kCodeToAcgt[i >> 4] + 4 * kCodeToAcgt[(i >> 2) & 3] + kCodeToAcgt[i & 3]];
+  constexpr const char* kStatus[6] = {"[unknown]", "homopolymer", "motif CCTGG", "motif CCAGG", "motif GATC",
+                                      "motif GTAC"};
+  for (int i = 0; i < 6; i++) {
+    int n = 0;
+    while (kStatus[i][n]) {
+      t.status[i][n] = (uint8_t)kStatus[i][n];
+      n++;
+    }
+    t.status[i][11] = (uint8_t)n;
+  }
   return t;
 }
 

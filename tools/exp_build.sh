@@ -5,7 +5,7 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 mkdir -p build_exp
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Ipwasm_amd/csrc"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Ipwasm_amd/csrc ${EXP_FLAGS:-}"
 for n in "$@"; do
   /opt/rocm/bin/hipcc $F -DPW_ABL=$n -c pwasm_amd/csrc/pw_report.hip -o build_exp/pw_report_$n.o &
 done
