@@ -93,10 +93,10 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
-    res = dev["results"].cpu().numpy().view(np.uint8).reshape(-1, 32)
-    n_events = int(res[:, 12:16].copy().view(np.uint32).sum())
-    errs = int((res[:, 16:20].copy().view(np.int32) != 0).sum())
-    text_bytes = int(res[:, 8:12].copy().view(np.uint32).astype(np.int64).sum())
+    res = pw.results_array(dev["results"].cpu().numpy())[: v.n_alns]
+    n_events = int(res["n_events"].sum())
+    errs = int((res["err"] != 0).sum())
+    text_bytes = int(res["text_len"].astype(np.int64).sum())
     assert errs == 0, f"{errs} records reported errors"
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

@@ -52,19 +52,35 @@ typedef struct pw_aln_desc {
   uint32_t ref;        /* bits 0..30 query index; bit 31 = reverse strand ('-') */
   int32_t offset;      /* start on the aligned-strand query (pafreport.cpp:486-490) */
   int32_t t_len;       /* tseq length implied by the cs string */
-  uint64_t text_begin; /* byte offset of this record's report slot in text[] */
+  uint64_t ev_begin;   /* first event slot of this record (prefix of pw_cs_totals.n_events_max) */
 } pw_aln_desc;
 #define PW_REF_REVERSE 0x80000000u
 
-/* Per-record result written by pw_report_events, 32 bytes. */
+/* Text pages.  The event lines of 64 consecutive event slots (one chunk) form one page, written
+ * at text[page.off, page.off + page.len).  A page normally lives at chunk * PW_PAGE_BYTES; a
+ * page that does not fit is placed in the arena after the page area.  A record's lines are the
+ * bytes from text_off (in page page_first) to text_end (in page page_last), crossing the pages
+ * in between in chunk order (pw_batch_write_report stitches them). */
+#define PW_PAGE_EVENTS 64
+#define PW_PAGE_BYTES 8192
+typedef struct pw_page {
+  uint64_t off;  /* first byte of the page's lines in text[] */
+  uint32_t len;  /* bytes of lines */
+  uint32_t pad;
+} pw_page;
+
+/* Per-record result written by pw_report_events, 48 bytes. */
 typedef struct pw_aln_result {
-  uint64_t text_off; /* first byte of the event lines in text[] */
-  uint32_t text_len; /* bytes of event lines (header excluded) */
-  uint32_t n_events; /* TDiffInfo records after S-merging */
-  int32_t err;       /* PW_REC_* */
-  int32_t err_a;     /* MISMATCH: q_pos          MODSEQ: modseq index */
-  int32_t err_b;     /* MISMATCH: query char     MODSEQ: evtsub index */
-  int32_t err_c;     /* MISMATCH: aligned-strand query char; MODSEQ: output line index */
+  uint64_t text_off;   /* first byte of the record's first event line in text[] */
+  uint64_t text_end;   /* one past the last byte of its last event line */
+  uint32_t page_first; /* pages holding those two lines */
+  uint32_t page_last;
+  uint32_t text_len;   /* bytes of event lines (header excluded) */
+  uint32_t n_events;   /* TDiffInfo records after S-merging */
+  int32_t err;         /* PW_REC_* */
+  int32_t err_a;       /* MISMATCH: q_pos          MODSEQ: modseq index */
+  int32_t err_b;       /* MISMATCH: query char     MODSEQ: evtsub index */
+  int32_t err_c;       /* MISMATCH: aligned-strand query char; MODSEQ: output line index */
 } pw_aln_result;
 
 #define PW_REC_OK 0
@@ -82,24 +98,32 @@ typedef struct pw_report_args {
   const uint64_t* qoff;     /* [n_queries] start of each query in qseq */
   const int32_t* qlen;      /* [n_queries] */
   const int32_t* next_stop; /* [sum qlen] from pw_stop_table_build; may be NULL if skip_codan */
-  uint8_t* text;            /* report slots, text_total bytes */
+  uint8_t* text;            /* text pages + arena, text_total bytes (pw_report_text_bytes) */
   pw_aln_result* results;   /* [n_alns] */
-  uint64_t text_total;      /* end of the last slot */
+  uint64_t text_total;      /* capacity of text */
   uint32_t n_alns;
   uint32_t skip_codan;      /* 1 = no codon impact column (pafreport.cpp:259-262, 915) */
-  void* workspace;          /* device scratch, 16-byte aligned, >= pw_report_workspace_bytes() */
+  void* workspace;          /* device scratch, 64-byte aligned, >= pw_report_workspace_bytes() */
   uint64_t workspace_bytes;
+  uint64_t n_ev_slots;      /* event slots of the batch = sum of pw_cs_totals.n_events_max */
+  pw_page* pages;           /* [pw_report_page_count(n_ev_slots)] */
 } pw_report_args;
 
-/* Device workspace pw_report_events needs for a batch with at most n_events_max events
- * (pw_cs_totals.n_events_max summed over the batch; pw_batch_view.n_events_max). */
-uint64_t pw_report_workspace_bytes(uint64_t n_events_max);
+/* Pages of a batch with n_ev_slots event slots, and the text capacity that always suffices:
+ * the page area plus an arena of text_bound bytes (sum of pw_cs_totals.text_bound). */
+uint64_t pw_report_page_count(uint64_t n_ev_slots);
+uint64_t pw_report_text_bytes(uint64_t n_ev_slots, uint64_t text_bound);
+
+/* Device workspace pw_report_events needs for a batch of n_alns records with n_events_max event
+ * slots (pw_cs_totals.n_events_max summed over the batch; pw_batch_view.n_events_max). */
+uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_alns);
 
 /* ---------------------------------------------------------------- device entry points */
 
 /* Replaces PAFAlignment::PAFAlignment (decode, pafreport.cpp:477-643) +
  * PAFAlignment::printDiffInfo's event loop (classify, codon, format; pafreport.cpp:893-954)
- * for a whole batch of records: one 64-lane wavefront per record. */
+ * for a whole batch of records: a wavefront per record decodes the op stream into event
+ * descriptors, then wavefronts of 64 consecutive events render the report lines. */
 int pw_report_events(const pw_report_args* args, void* stream);
 
 /* Per-query stop-codon lookahead used by the codon pass (replaces the forward scan of
@@ -181,23 +205,24 @@ typedef struct pw_batch_view {
   const uint8_t* qseq;
   const uint64_t* qoff;
   const int32_t* qlen;
-  uint64_t n_alns, n_ops, n_lits, qseq_len, n_queries, text_total, n_events_max;
+  uint64_t n_alns, n_ops, n_lits, qseq_len, n_queries, text_total, n_events_max;  /* text_total = text bound */
   uint64_t alg_bytes_in; /* algorithmic input bytes of one pass */
   uint32_t skip_codan;
 } pw_batch_view;
 /* flags: bit0 = -G, bit1 = -F, bit2 = -C, bit3 = -N (same defaults as the CLI) */
 pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uint32_t flags, char* errbuf, size_t errlen);
 int pw_batch_view_get(const pw_batch* b, pw_batch_view* out);
-/* Render the report (headers + event text) for results of a finished batch into `path`. */
+/* Render the report (headers + event text) for results of a finished batch into `path`
+ * (host copies of text, results and pages). */
 int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
-                          const char* path);
+                          const pw_page* pages_host, const char* path);
 /* Shard output for a multi-GPU run: the same bytes as pw_batch_write_report, cut
  * into items tagged with their 0-based input line ("PWI1", then per item {u64 line, i32 status
  * (-1 = continue, else the exit code the reference ends with), u32 n_stdout, u32 n_stderr,
  * stdout bytes, stderr bytes}).  Merging the items of all shards by global line, up to the
  * first item with status >= 0, reproduces the single-process output (pwasm_amd/shard.py). */
 int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
-                         const char* path);
+                         const pw_page* pages_host, const char* path);
 void pw_batch_free(pw_batch* b);
 
 const char* pw_version(void);

@@ -33,13 +33,32 @@ FLAG_G, FLAG_F, FLAG_C, FLAG_N = 1, 2, 4, 8
 class AlnDesc(ctypes.Structure):
     _fields_ = [("op_begin", ctypes.c_uint32), ("n_ops", ctypes.c_uint32), ("lit_begin", ctypes.c_uint32),
                 ("ref", ctypes.c_uint32), ("offset", ctypes.c_int32), ("t_len", ctypes.c_int32),
-                ("text_begin", ctypes.c_uint64)]
+                ("ev_begin", ctypes.c_uint64)]
 
 
 class AlnResult(ctypes.Structure):
-    _fields_ = [("text_off", ctypes.c_uint64), ("text_len", ctypes.c_uint32), ("n_events", ctypes.c_uint32),
+    _fields_ = [("text_off", ctypes.c_uint64), ("text_end", ctypes.c_uint64), ("page_first", ctypes.c_uint32),
+                ("page_last", ctypes.c_uint32), ("text_len", ctypes.c_uint32), ("n_events", ctypes.c_uint32),
                 ("err", ctypes.c_int32), ("err_a", ctypes.c_int32), ("err_b", ctypes.c_int32),
                 ("err_c", ctypes.c_int32)]
+
+
+class Page(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+PAGE_EVENTS, PAGE_BYTES = 64, 8192
+
+
+def results_array(raw):
+    """A results buffer (bytes / uint8 numpy / torch cpu tensor) as a numpy structured array."""
+    import numpy as np
+    dt = np.dtype([("text_off", "<u8"), ("text_end", "<u8"), ("page_first", "<u4"), ("page_last", "<u4"),
+                   ("text_len", "<u4"), ("n_events", "<u4"), ("err", "<i4"), ("err_a", "<i4"), ("err_b", "<i4"),
+                   ("err_c", "<i4")])
+    assert dt.itemsize == ctypes.sizeof(AlnResult)
+    a = np.asarray(raw).view(np.uint8).ravel()
+    return a[: a.size - a.size % dt.itemsize].view(dt)
 
 
 class ReportArgs(ctypes.Structure):
@@ -47,7 +66,8 @@ class ReportArgs(ctypes.Structure):
                 ("qseq", ctypes.c_void_p), ("qoff", ctypes.c_void_p), ("qlen", ctypes.c_void_p),
                 ("next_stop", ctypes.c_void_p), ("text", ctypes.c_void_p), ("results", ctypes.c_void_p),
                 ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
-                ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64)]
+                ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
+                ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p)]
 
 
 class CsTotals(ctypes.Structure):
@@ -86,9 +106,13 @@ _SIGS = {
     "pw_batch_from_files": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                               ctypes.c_size_t]),
     "pw_batch_view_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatchView)]),
-    "pw_batch_write_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
-    "pw_report_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
-    "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p]),
+    "pw_batch_write_report": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_char_p]),
+    "pw_report_page_count": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "pw_report_text_bytes": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "pw_report_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_char_p]),
     "pw_batch_free": (None, [ctypes.c_void_p]),
     "pw_version": (ctypes.c_char_p, []),
     "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
@@ -157,13 +181,24 @@ class HostBatch:
         buf = (ct * int(n)).from_address(int(ptr))
         return np.ctypeslib.as_array(buf).copy()
 
-    def write_report(self, text_host, results_host, path: str) -> int:
+    def write_report(self, text_host, results_host, pages_host, path: str) -> int:
         """Headers + event text for a finished batch (numpy arrays on the host)."""
-        return lib().pw_batch_write_report(self._h, text_host.ctypes.data, results_host.ctypes.data, path.encode())
+        return lib().pw_batch_write_report(self._h, text_host.ctypes.data, results_host.ctypes.data,
+                                           pages_host.ctypes.data, path.encode())
 
-    def write_items(self, text_host, results_host, path: str) -> int:
+    def write_items(self, text_host, results_host, pages_host, path: str) -> int:
         """The same output cut into line-tagged items (PWI1) for the multi-GPU shard merge."""
-        return lib().pw_batch_write_items(self._h, text_host.ctypes.data, results_host.ctypes.data, path.encode())
+        return lib().pw_batch_write_items(self._h, text_host.ctypes.data, results_host.ctypes.data,
+                                          pages_host.ctypes.data, path.encode())
+
+    def write_report_from(self, dev: dict, path: str) -> int:
+        """write_report with the device buffers of stage_batch() copied to the host."""
+        return self.write_report(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), dev["pages"].cpu().numpy(),
+                                 path)
+
+    def write_items_from(self, dev: dict, path: str) -> int:
+        return self.write_items(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), dev["pages"].cpu().numpy(),
+                                path)
 
     def close(self):
         if self._h:
@@ -190,11 +225,13 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     a.next_stop = 0 if v.skip_codan else dev["next_stop"].data_ptr()
     a.text = dev["text"].data_ptr()
     a.results = dev["results"].data_ptr()
-    a.text_total = int(v.text_total)
+    a.text_total = dev["text"].numel()
     a.n_alns = int(v.n_alns)
     a.skip_codan = int(v.skip_codan)
     a.workspace = dev["work"].data_ptr()
     a.workspace_bytes = dev["work"].numel()
+    a.n_ev_slots = int(v.n_events_max)
+    a.pages = dev["pages"].data_ptr()
     return a
 
 
@@ -229,8 +266,12 @@ def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
             arr = np.concatenate([arr, np.zeros(DEV_PAD, dtype=arr.dtype)])
         dev[name] = torch.from_numpy(arr).to(device)
     dev["next_stop"] = torch.empty(max(int(v.qseq_len), 1), dtype=torch.int32, device=device)
-    dev["text"] = torch.empty(max(int(v.text_total), 1), dtype=torch.uint8, device=device)
-    dev["work"] = torch.empty(int(lib().pw_report_workspace_bytes(int(v.n_events_max))), dtype=torch.uint8,
+    L = lib()
+    dev["text"] = torch.empty(max(int(L.pw_report_text_bytes(int(v.n_events_max), int(v.text_total))), 16),
+                              dtype=torch.uint8, device=device)
+    dev["pages"] = torch.zeros(max(int(L.pw_report_page_count(int(v.n_events_max))), 1) * ctypes.sizeof(Page),
+                               dtype=torch.uint8, device=device)
+    dev["work"] = torch.empty(int(lib().pw_report_workspace_bytes(int(v.n_events_max), int(v.n_alns))), dtype=torch.uint8,
                               device=device)
     dev["results"] = torch.empty(max(int(v.n_alns), 1) * ctypes.sizeof(AlnResult), dtype=torch.uint8,
                                  device=device)

@@ -392,7 +392,7 @@ struct Packer {
     d.ref = (uint32_t)qi | (reverse ? PW_REF_REVERSE : 0u);
     d.offset = offset;
     d.t_len = 0;
-    d.text_begin = b.text_total;
+    d.ev_begin = b.n_events_max;
     if (cigar == nullptr || cigar[0] == 0) {
       rh.pre_msg = (int32_t)b.add_msg(strf(CIGAR_ERROR, lstr, "(null)"));
     } else if (cs == nullptr) {
@@ -536,6 +536,7 @@ struct Device {
   DevBuf<uint32_t> ops;
   DevBuf<uint8_t> lits, text, work;
   DevBuf<pw_aln_result> res;
+  DevBuf<pw_page> pages;
   uint32_t nq = 0;
   bool init(const QueryDb& q, bool skip_codan) {
     int n = 0;
@@ -563,14 +564,17 @@ struct Device {
     return true;
   }
   // run the batch; fills text/results on the host
-  bool run(const Batch& b, bool skip_codan, std::vector<uint8_t>& text_h, std::vector<pw_aln_result>& res_h) {
+  bool run(const Batch& b, bool skip_codan, std::vector<uint8_t>& text_h, std::vector<pw_aln_result>& res_h,
+           std::vector<pw_page>& pages_h) {
     const size_t na = b.desc.size();
     res_h.resize(na);
-    text_h.resize(b.text_total);
+    const uint64_t np = pw_report_page_count(b.n_events_max);
+    const uint64_t tcap = pw_report_text_bytes(b.n_events_max, b.text_total);
+    pages_h.resize(np);
     if (na == 0) return true;
     if (!desc.ensure(na) || !ops.ensure(b.ops.size() + 1) || !lits.ensure(b.lits.size() + kDevPad) ||
-        !text.ensure(b.text_total + 1) || !res.ensure(na) ||
-        !work.ensure(pw_report_workspace_bytes(b.n_events_max))) {
+        !text.ensure(tcap + 1) || !res.ensure(na) || !pages.ensure(np + 1) ||
+        !work.ensure(pw_report_workspace_bytes(b.n_events_max, na))) {
       fprintf(stderr, "pafreport: device allocation failed\n");
       return false;
     }
@@ -589,19 +593,27 @@ struct Device {
     a.next_stop = skip_codan ? nullptr : next_stop.p;
     a.text = text.p;
     a.results = res.p;
-    a.text_total = b.text_total;
+    a.text_total = tcap;
     a.n_alns = (uint32_t)na;
     a.skip_codan = skip_codan ? 1u : 0u;
     a.workspace = work.p;
-    a.workspace_bytes = pw_report_workspace_bytes(b.n_events_max);
+    a.workspace_bytes = pw_report_workspace_bytes(b.n_events_max, na);
+    a.n_ev_slots = b.n_events_max;
+    a.pages = pages.p;
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
       return false;
     }
     HIPCHK(hipMemcpyAsync(res_h.data(), res.p, na * sizeof(pw_aln_result), hipMemcpyDeviceToHost, stream));
-    if (b.text_total)
-      HIPCHK(hipMemcpyAsync(text_h.data(), text.p, b.text_total, hipMemcpyDeviceToHost, stream));
+    if (np) HIPCHK(hipMemcpyAsync(pages_h.data(), pages.p, np * sizeof(pw_page), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    // copy back the used part of the text (pages + arena)
+    uint64_t used = 0;
+    for (const pw_page& pg : pages_h)
+      if (pg.len && pg.off + pg.len > used) used = pg.off + pg.len;
+    if (used > tcap) used = tcap;
+    text_h.resize(used);
+    if (used) HIPCHK(hipMemcpy(text_h.data(), text.p, used, hipMemcpyDeviceToHost));
     return true;
   }
   ~Device() {
@@ -611,8 +623,31 @@ struct Device {
 
 // Print what the reference prints for one log item; returns -1 to continue, else the exit code
 // the reference ends with at this item.
-int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_aln_result* res, FILE* out,
-              FILE* err) {
+// Write the first `nlines` event lines of a record (all of them when nlines == n_events): the
+// bytes from text_off to text_end, crossing pages in chunk order (pwasm_amd.h, text pages).
+void write_lines(const uint8_t* text, const pw_page* pages, const pw_aln_result& r, uint32_t nlines, FILE* out) {
+  if (r.n_events == 0 || nlines == 0) return;
+  uint32_t seen = 0;
+  for (uint32_t c = r.page_first;; c++) {
+    const uint64_t lo = c == r.page_first ? r.text_off : pages[c].off;
+    const uint64_t hi = c == r.page_last ? r.text_end : pages[c].off + pages[c].len;
+    const uint8_t* p = text + lo;
+    size_t n = (size_t)(hi - lo);
+    if (nlines != r.n_events) {  // stop after the nlines-th newline
+      size_t k = 0;
+      while (k < n && seen < nlines) {
+        if (p[k] == '\n') seen++;
+        k++;
+      }
+      n = k;
+    }
+    fwrite(p, 1, n, out);
+    if (c == r.page_last || (nlines != r.n_events && seen >= nlines)) break;
+  }
+}
+
+int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_aln_result* res, const pw_page* pages,
+              FILE* out, FILE* err) {
   if (it.kind == 0) {
     fputs(b.msgs[it.idx].c_str(), err);
     return -1;
@@ -658,26 +693,17 @@ int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_a
     nlines = (uint32_t)r.err_c;
     post = strf("Error: modseq[%d] not matching di.evtsub[%d] !\n", r.err_a, r.err_b);
   }
-  const uint8_t* tx = text + r.text_off;
-  if (nlines == r.n_events) {
-    fwrite(tx, 1, r.text_len, out);
-    return -1;
-  }
-  uint32_t pos = 0, seen = 0;
-  while (seen < nlines && pos < r.text_len) {
-    if (tx[pos] == '\n') seen++;
-    pos++;
-  }
-  fwrite(tx, 1, pos, out);
+  write_lines(text, pages, r, nlines, out);
+  if (nlines == r.n_events) return -1;
   fflush(out);
   fputs(post.c_str(), err);
   return 1;
 }
 
 // Print what the reference prints for this batch; returns -1 to continue, else an exit code.
-int emit(const Batch& b, const uint8_t* text, const pw_aln_result* res, FILE* out) {
+int emit(const Batch& b, const uint8_t* text, const pw_aln_result* res, const pw_page* pages, FILE* out) {
   for (const LogItem& it : b.log) {
-    const int rc = emit_item(b, it, text, res, out, stderr);
+    const int rc = emit_item(b, it, text, res, pages, out, stderr);
     if (rc >= 0) return rc;
   }
   return -1;
@@ -904,6 +930,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   Batch b;
   std::vector<uint8_t> text_h;
   std::vector<pw_aln_result> res_h;
+  std::vector<pw_page> pages_h;
   const size_t kBatchBytes = 256u << 20, kBatchRecs = 1u << 20;
   bool more = true;
   while (more) {
@@ -918,8 +945,8 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
         break;
       }
     }
-    if (!dev.run(b, skip_codan, text_h, res_h)) return 2;
-    const int rc = emit(b, text_h.data(), res_h.data(), out.f);
+    if (!dev.run(b, skip_codan, text_h, res_h, pages_h)) return 2;
+    const int rc = emit(b, text_h.data(), res_h.data(), pages_h.data(), out.f);
     if (rc >= 0) {
       fflush(out.f);
       return rc;
@@ -995,11 +1022,11 @@ extern "C" int pw_batch_view_get(const pw_batch* bt, pw_batch_view* v) {
 }
 
 extern "C" int pw_batch_write_report(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
-                                     const char* path) {
+                                     const pw_page* pages_host, const char* path) {
   if (!bt || !path) return PW_E_ARG;
   FILE* f = fopen(path, "wb");
   if (!f) return PW_E_IO;
-  int rc = emit(bt->b, text_host, res_host, f);
+  int rc = emit(bt->b, text_host, res_host, pages_host, f);
   fclose(f);
   return rc < 0 ? 0 : rc;
 }
@@ -1007,7 +1034,7 @@ extern "C" int pw_batch_write_report(const pw_batch* bt, const uint8_t* text_hos
 // Item stream of a shard (PWI1): per log item {u64 line, i32 status, u32 n_out,
 // u32 n_err, stdout bytes, stderr bytes}; ends after the first item with status >= 0.
 extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
-                                    const char* path) {
+                                    const pw_page* pages_host, const char* path) {
   if (!bt || !path) return PW_E_ARG;
   FILE* f = fopen(path, "wb");
   if (!f) return PW_E_IO;
@@ -1024,7 +1051,7 @@ extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host
       if (e) fclose(e);
       break;
     }
-    const int32_t st = emit_item(bt->b, it, text_host, res_host, o, e);
+    const int32_t st = emit_item(bt->b, it, text_host, res_host, pages_host, o, e);
     fclose(o);
     fclose(e);
     const uint32_t no = (uint32_t)on, ne = (uint32_t)en;

@@ -1,5 +1,5 @@
 // pw_report.hip — the MI355X hot path of pafreport: cs decode -> event classifier -> codon
-// consequence -> report-line rendering, fused into one kernel (gfx950, wave64).
+// consequence -> report-line rendering (gfx950, wave64).
 //
 // Reference behaviour restated here (gpertea/pwasm, /root/reference):
 //   decode            PAFAlignment::PAFAlignment           pafreport.cpp:526-643
@@ -9,29 +9,29 @@
 //   codon consequence predictImpact                        pafreport.cpp:801-883
 //   event line        printDiffInfo (event loop)           pafreport.cpp:893-954
 //
-// Layout: one 64-lane wavefront (= one 64-thread workgroup) owns one PAF record at a time and
-// walks its packed op stream in SEGMENTS of up to 128 ops (2 per lane):
-//   1. coalesced load of the segment's op words; wave prefix-scan of (query, target, literal)
-//      advances -> every op's start coordinates;
-//   2. the segment is cut where its query span or literal span would overflow the LDS windows,
-//      then staged in LDS with 16-byte loads: op words (+16-op halo each side), per-op starts,
-//      the literal bytes and the forward-query window its events can touch (span + 64 bytes
-//      each side).  Byte accesses hit LDS; one outside a window (long indels at a segment edge)
-//      falls back to the global copy, so windows change speed, never results;
-//   3. ballot of SUB ops -> S-run heads (pafreport merges directly consecutive '*' ops,
-//      pafreport.cpp:556-560; `:0` ops are dropped by the pre-pass so "consecutive" is exact);
-//      heads are compacted into an event list, one event per lane;
-//   4. each lane computes its event and writes the report line, field by field as the values
-//      become known, into its own 112-byte LDS line buffer (stores are unconditional: a
-//      masked-off character goes to the lane's junk byte, so there is no per-character branch);
-//   5. a wave prefix-scan of line lengths places the lines in the record's text slot (events of
-//      '-' records back-to-front = the reference's tdiffs.Reverse(), pafreport.cpp:643) and the
-//      lines are gathered 16 bytes per lane into full-width global stores.
-// Rare, divergent work is not done in the wave (where one lane taking a slow path stalls all 64):
-// a target context that needs an op walk, and a line longer than its buffer (an S run with many
-// changed codons), get their bytes reserved and are queued for fixup_kernel, launched behind.
-// Workgroups are persistent (grid-stride over records): the 4.6 KB of byte tables are staged
-// into LDS once per workgroup.
+// One pass (pw_report_events) is four launches on one stream:
+//
+//  index_kernel     one wavefront per PAF record: wave prefix scans over the packed op stream
+//                   give every op its query / target / literal coordinates (the sequential walk
+//                   of pafreport.cpp:536-626), '*' ops are base-checked, directly consecutive '*'
+//                   ops merged into one S event (:556-560), and every event is written as a
+//                   32-byte render record (+ a 16-byte cold record) into its record's event
+//                   slots, already in OUTPUT order ('-' records fill their slots back to front =
+//                   tdiffs.Reverse(), :643).  Target contexts that need an op walk (another event
+//                   within 5 bases) are rendered here, where the op words are in LDS.
+//  render_kernel    lane-dense: one wavefront takes 64 consecutive event slots (across record
+//                   boundaries) from a work ticket, each lane renders its event's report line
+//                   into an LDS line buffer, a decoupled look-back over the chunks gives the
+//                   chunk's place in the contiguous text, and the wave writes the lines with
+//                   16-byte stores.  The forward query bytes an event reads are staged per lane
+//                   (a 64-byte LDS window around the event); the next chunk's records are
+//                   loaded while the current one renders.
+//  fixup_kernel     lines longer than the line buffer (S runs with many changed codons),
+//                   written in place.
+//  finalize_kernel  per-record results (text offset/length, event count, errors).
+//
+// The text is one contiguous stream of event lines in record order; record headers are
+// formatted by the host (the only floating-point value, coverage:%.2f).
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -45,43 +45,60 @@ namespace pw {
 // "LDS hit ? lds[o] : global[i]" into one flat load (global latency + vmcnt waits).
 #define LDS __attribute__((address_space(3)))
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // 16-byte copies
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 __constant__ Tables c_tables = build_tables();
 
 constexpr int kWave = 64;
-constexpr int kSegOps = 128;    // ops per segment (2 per lane)
-constexpr int kOpHalo = 16;     // op words staged before / after a segment
-constexpr int kQW = 4096;       // forward-query window per wave (bytes)
-constexpr int kQPad = 64;       // context reach beyond a segment's query span
-constexpr int kLW = 1024;       // literal window per wave (bytes)
-constexpr int kLPad = 64;
-constexpr int kLine = 112;      // per-lane report-line buffer (bytes)
-constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries (rounds without long lines)
+constexpr int kWaves = 4;       // wavefronts per workgroup (independent; they share the tables)
+constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
+constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
+constexpr int kQWin = 64;       // render_kernel: forward-query window per lane (bytes)
+constexpr int kQStride = 72;    // ... its LDS stride (18 dwords: conflict-free 8-byte stores)
+constexpr int kLine = 96;       // render_kernel: per-lane report-line buffer (bytes)
+constexpr int kLStride = 100;   // ... its LDS stride (25 dwords: per-lane byte stores conflict-free)
+constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
+constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, failed records)
+constexpr uint32_t kNBig = (1u << 20) - 1;  // evtbases length field saturates here
+constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
 #ifndef PW_ABL
 #define PW_ABL 0
 #endif
 
-struct WaveLds {
-  uint8_t line[kWave * kLine];  // per-lane line buffers
-  uint8_t qw[kQW];
-  uint8_t lw[kLW];
-  uint32_t opw[kSegOps + 2 * kOpHalo];
-  int32_t qs[kSegOps];
-  int32_t ts[kSegOps];
-  uint32_t ls[kSegOps];
-  uint32_t ostart[kWave + 1];   // line starts in output order
-  uint8_t junk[kWave];
-  uint8_t olane[kWave];         // lane of the k-th line in output order
-  uint8_t cmap[kMap];           // 16-byte output chunk -> output index of its first line
-  uint16_t evl[kSegOps];
+// Render record of one event (index_kernel -> render_kernel), 32 bytes.
+//   fn: type (31-30) | reverse (29) | fast tctx (28) | first line of its record (27) |
+//       last line (26) | ll (25-23) | rl (22-20) | evtbases length (19-0, saturated)
+//   l0, l1: the event's first 8 literal bytes (SUB: target,query pairs; INS: inserted bases)
+struct Hot {
+  uint32_t qb;    // forward query start in qseq
+  int32_t L;      // query length
+  int32_t qp;     // offset + qpos at the event (aligned strand)
+  int32_t tloc;   // printed tloc - 1 (pafreport.cpp:639)
+  uint32_t ls;    // literal start
+  uint32_t fn;
+  uint32_t l0, l1;
 };
+// Cold record (fixups, record results), 16 bytes.
+struct Cold {
+  uint32_t ai, j;  // record, head op
+  int32_t qs, ts;  // query / target position at the head op
+};
+__device__ __forceinline__ uint32_t hot_fn(uint32_t typ, bool rev, bool fast, bool first, bool last, int ll, int rl,
+                                           uint32_t n) {
+  return typ << 30 | (rev ? 1u << 29 : 0u) | (fast ? 1u << 28 : 0u) | (first ? 1u << 27 : 0u) |
+         (last ? 1u << 26 : 0u) | (uint32_t)(ll & 7) << 23 | (uint32_t)(rl & 7) << 20 | (n < kNBig ? n : kNBig);
+}
 
-struct Lds {
-  Tables tab;
-  WaveLds w;
+// Byte tables read per event (LDS copy per workgroup).  The 4096-entry IUPAC codon table is
+// only needed off {A,C,G,T} and is read from c_tables.
+struct SmallTables {
+  uint8_t nt[256];
+  uint8_t comp[256];
+  uint8_t codon64[64];
+  uint8_t status[8][12];
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -94,8 +111,14 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
   return v;
 }
 __device__ __forceinline__ uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, kWave); }
-// LDS written by some lanes and read by others of the same (single-wave) workgroup
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// LDS written by some lanes of a wavefront and read by others of the SAME wavefront (the
+// waves of a workgroup are independent): LDS operations of one wave execute in order, so only
+// the compiler has to be kept from moving memory operations across this point.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ------------------------------------------------------------------ record context
 struct Rec {
@@ -103,29 +126,35 @@ struct Rec {
   const uint8_t* lits;      // global literal array
   const uint8_t* R;         // forward query (global)
   const int32_t* NS;        // next-stop table of this query (or null)
-  const LDS Tables* tab;    // LDS tables
+  const LDS SmallTables* tab;
   const LDS uint8_t* qw;    // LDS forward-query window
-  const LDS uint8_t* lw;    // LDS literal window
-  const LDS uint32_t* opw;  // LDS op words
+  int qlo;                  // forward position of qw[0]
+  int qn;                   // window bytes (0 = no window)
+  const LDS uint32_t* opw;  // LDS op-word window (index_kernel)
+  int op_lo;                // record op index of opw[0]
+  uint32_t op_n;            // window ops (0 = none)
+  uint32_t lit0, lit1;      // literal bytes [ls0, ls0 + ln) in registers (render_kernel)
+  uint32_t ls0, ln;
+  const LDS uint8_t* lw;    // LDS literal window [l_lo, l_lo + l_n) (index_kernel)
+  uint32_t l_lo, l_n;
   int L;                    // query length
   int offset;               // start on the aligned strand
   int T;                    // tseq length
   uint32_t n_ops;
-  int qlo;                  // forward position of qw[0]
-  uint32_t l_lo, l_n;       // literal window [l_lo, l_lo + l_n)
-  int op_lo;                // record op index of opw[0]
-  uint32_t op_n;
   bool rev;
 };
 
 __device__ __forceinline__ uint8_t Rc(const Rec& r, int x) {
   if ((unsigned)x >= (unsigned)r.L) return 0;
   const unsigned o = (unsigned)(x - r.qlo);
-  return o < (unsigned)kQW ? r.qw[o] : r.R[x];
+  return o < (unsigned)r.qn ? r.qw[o] : r.R[x];
 }
 __device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
-  const uint32_t o = i - r.l_lo;
-  return o < r.l_n ? r.lw[o] : r.lits[i];
+  const uint32_t o = i - r.ls0;
+  if (o < r.ln) return (uint8_t)((o < 4 ? r.lit0 : r.lit1) >> (8 * (o & 3)));
+  const uint32_t ow = i - r.l_lo;
+  if (ow < r.l_n) return r.lw[ow];
+  return r.lits[i];
 }
 __device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
   const unsigned o = (unsigned)((int)j - r.op_lo);
@@ -134,9 +163,9 @@ __device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
 
 // aligned-strand query char at p (refseq_rc for '-' records, pafreport.cpp:352-362); p == L
 // reads the NUL terminator as the reference does.
-__device__ __forceinline__ uint8_t aligned_char(const Rec& r, int p) {
-  if ((unsigned)p >= (unsigned)r.L) return 0;
-  return r.rev ? r.tab->comp[Rc(r, r.L - 1 - p)] : Rc(r, p);
+__device__ __forceinline__ uint8_t aligned_char_g(const uint8_t* R, int L, bool rev, const LDS SmallTables* t, int p) {
+  if ((unsigned)p >= (unsigned)L) return 0;
+  return rev ? t->comp[R[L - 1 - p]] : R[p];
 }
 
 // translateCodon: three bases of {A,C,G,T} in either case take one lookup in codon64 (no
@@ -145,10 +174,10 @@ __device__ __forceinline__ bool is_acgt(uint32_t c) {
   // letters 0x40-0x7F whose low 5 bits are 1 (A), 3 (C), 7 (G) or 20 (T)
   return (c & 0xC0u) == 0x40u && ((0x0010008Au >> (c & 0x1Fu)) & 1u);
 }
-__device__ __forceinline__ uint8_t translate(const LDS Tables* t, uint8_t a, uint8_t b, uint8_t c) {
+__device__ __forceinline__ uint8_t translate(const LDS SmallTables* t, uint8_t a, uint8_t b, uint8_t c) {
   if (is_acgt(a) && is_acgt(b) && is_acgt(c))
     return t->codon64[((a >> 1) & 3u) << 4 | ((b >> 1) & 3u) << 2 | ((c >> 1) & 3u)];
-  return t->codon[(t->nt[a] << 8) | (t->nt[b] << 4) | t->nt[c]];
+  return c_tables.codon[(t->nt[a] << 8) | (t->nt[b] << 4) | t->nt[c]];
 }
 
 __device__ __forceinline__ uint32_t op_tadv(uint32_t w) {
@@ -178,6 +207,18 @@ struct Event {
   int r_trloc;
 };
 
+// What a line needs besides the record: the event's coordinates and how to produce its tctx.
+struct EvIn {
+  uint32_t typ;
+  int n, qp, tloc;
+  uint32_t ls;
+  int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
+  int ll, rl;
+  const uint8_t* tx;  // length byte + field (tmode 1)
+  uint32_t j, wd;
+  int qs, ts;
+};
+
 // evtbases[i] in final orientation, upper case (pafreport.cpp:563,594-596,612-614,637,895)
 __device__ __forceinline__ uint8_t ev_base(const Rec& r, const Event& e, int i) {
   if (e.type == PW_OP_SUB) return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i))] : litb(r, e.ls + 2 * i);
@@ -191,22 +232,24 @@ __device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
 
 // ------------------------------------------------------------------ line sinks
 // LineSink writes into the lane's LDS line buffer; a store past the buffer or a masked-off
-// character goes to the lane's junk byte (no branch).  GlobalSink (fixup_kernel) writes
-// the line straight to its place in the text slot.
-struct LineSink {
+// character goes to the lane's junk byte (no branch).  GlobalSink writes straight to global
+// memory (fixup_kernel lines, index_kernel target contexts).
+template <int CAP>
+struct LdsSink {
   LDS uint8_t* buf;
   LDS uint8_t* junk;
   int pos;
   __device__ __forceinline__ void put(uint8_t c) {
-    *(pos < kLine ? buf + pos : junk) = c;
+    *(pos < CAP ? buf + pos : junk) = c;
     pos++;
   }
   __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
-    *((pred && pos < kLine) ? buf + pos : junk) = c;
+    *((pred && pos < CAP) ? buf + pos : junk) = c;
     pos += pred ? 1 : 0;
   }
-  __device__ __forceinline__ void put_at(int i, uint8_t c) { *(i < kLine ? buf + i : junk) = c; }
+  __device__ __forceinline__ void put_at(int i, uint8_t c) { *(i < CAP ? buf + i : junk) = c; }
 };
+typedef LdsSink<kLine> LineSink;
 struct GlobalSink {
   uint8_t* p;
   int pos;
@@ -267,10 +310,6 @@ __device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, 
 // "%d" of a non-negative int
 template <class S>
 __device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
-#if PW_ABL & 8
-  k.put('1'); k.put('2'); k.put('3'); k.put((uint8_t)('0' + (v & 7)));
-  return;
-#endif
   if (v >= 100000u) {
     for (uint32_t P = 1000000000u; P >= 100000u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   }
@@ -297,84 +336,85 @@ __device__ __forceinline__ int event_len(const Rec& r, uint32_t j, uint32_t wd) 
   return n;
 }
 
-// Length of the tctx field for a context of cl target bases (abbreviated past 10+MAX_EVLEN).
-__device__ __forceinline__ int tctx_field_len(int cl) {
-  if (cl <= 10 + kMaxEv) return cl;
-  const uint32_t v = (uint32_t)(cl - 10);
-  return 12 + 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
-         (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
+// Target-context geometry of an event (setTContext, pafreport.cpp:120-128): context [tcs, tce)
+// of cl bases, ll target bases before the event, nm of its own, rl after.
+struct TGeom {
+  int tcs, tce, cl, ll, nm, rl;
+};
+__device__ __forceinline__ TGeom tgeom(int T, uint32_t typ, int n, int ts) {
+  TGeom g;
+  const int evtlen = typ == PW_OP_SUB ? 1 : n;  // merged S keeps evtlen 1 (pafreport.cpp:562)
+  g.tcs = ts - 5;
+  if (g.tcs < 0) g.tcs = 0;
+  g.tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
+  if (g.tce >= T) g.tce = T - 1;
+  g.cl = g.tce - g.tcs;
+  if (g.cl < 0) g.cl = 0;
+  g.ll = ts - g.tcs;
+  g.nm = typ == PW_OP_DEL ? 0 : (typ == PW_OP_SUB ? 1 : n);
+  g.rl = g.tce - (ts + g.nm);
+  return g;
+}
+// Fast target context: match runs on both sides cover it (the common case), so it is query
+// bytes, the event's own target bases, query bytes — no op walk.  pw / aw: the op words before
+// the event and after its head op.
+__device__ __forceinline__ bool tctx_fast(const TGeom& g, uint32_t typ, int n, uint32_t pw, bool has_pw, uint32_t aw,
+                                          bool has_aw) {
+  return g.cl <= 10 + kMaxEv && (typ != PW_OP_SUB || n == 1) && g.rl >= 0 &&
+         (g.ll == 0 || (has_pw && (pw >> 30) == PW_OP_MATCH && (int)(pw & 0x3FFFFFFFu) >= g.ll)) &&
+         (g.rl == 0 || (has_aw && (aw >> 30) == PW_OP_MATCH && (int)(aw & 0x3FFFFFFFu) >= g.rl));
 }
 
-// The tctx field (setTContext, pafreport.cpp:120-128; revCompl :631; abbreviation :918-927).
-// Fast path — match runs of >= 5 on both sides (the common case): query bytes, the event's own
-// target bases, query bytes, no op walk.  Otherwise the context is gathered by walking the op
-// stream; with `defer` that walk is not done here: the field's bytes are skipped (its length is
-// known) and the return value is its position in the line, for fixup_kernel to fill.
+// The tctx field, fast form: ll query bytes, the event's own target bases, rl query bytes.
 template <class S>
-__device__ __forceinline__ int emit_tctx(S& k, const Rec& r, uint32_t typ, int n, uint32_t j, uint32_t wd, int qs,
-                                         int ts, uint32_t ls, bool defer) {
-  const int qp = r.offset + qs;
-  const int evtlen = typ == PW_OP_SUB ? 1 : n;  // merged S keeps evtlen 1 (pafreport.cpp:562)
-  int tcs = ts - 5;
-  if (tcs < 0) tcs = 0;
-  int tce = ts + (typ == PW_OP_DEL ? 0 : evtlen) + 5;
-  if (tce >= r.T) tce = r.T - 1;
-  int cl = tce - tcs;
-  if (cl < 0) cl = 0;
-  const int ll = ts - tcs;                                          // target bases before
-  const int nm = typ == PW_OP_DEL ? 0 : (typ == PW_OP_SUB ? 1 : n);  // the event's own
-  const int rl = tce - (ts + nm);                                   // bases after
-  const uint32_t pw = (ll > 0 && j > 0) ? opword(r, j - 1) : 0u;
-  const uint32_t aw = (rl > 0 && j + 1 < r.n_ops) ? opword(r, j + 1) : 0u;
-  const bool fast = cl <= 10 + kMaxEv && (typ != PW_OP_SUB || n == 1) && rl >= 0 &&
-                    (ll == 0 || (j > 0 && (pw >> 30) == PW_OP_MATCH && (int)(pw & 0x3FFFFFFFu) >= ll)) &&
-                    (rl == 0 || (j + 1 < r.n_ops && (aw >> 30) == PW_OP_MATCH && (int)(aw & 0x3FFFFFFFu) >= rl));
-  if (fast) {
-    // aligned query start after the event; '-' records read the forward query in the other
-    // order (revCompl of tctx: comp(comp(x)) = x up to U)
-    const int qpa = qp + (typ == PW_OP_SUB ? 1 : (typ == PW_OP_DEL ? n : 0));
-    const int f1 = r.rev ? r.L - qpa - rl : qp - ll, n1 = r.rev ? rl : ll;
-    const int f2 = r.rev ? r.L - qp : qpa, n2 = r.rev ? ll : rl;
-    uint8_t c1[5], c2[5];
+__device__ __forceinline__ void emit_tctx_fast(S& k, const Rec& r, uint32_t typ, int n, int qp, uint32_t ls, int ll,
+                                               int rl) {
+  const int nm = typ == PW_OP_DEL ? 0 : (typ == PW_OP_SUB ? 1 : n);
+  // aligned query start after the event; '-' records read the forward query in the other
+  // order (revCompl of tctx: comp(comp(x)) = x up to U)
+  const int qpa = qp + (typ == PW_OP_SUB ? 1 : (typ == PW_OP_DEL ? n : 0));
+  const int f1 = r.rev ? r.L - qpa - rl : qp - ll, n1 = r.rev ? rl : ll;
+  const int f2 = r.rev ? r.L - qp : qpa, n2 = r.rev ? ll : rl;
+  uint8_t c1[5], c2[5];
 #pragma unroll
-    for (int q = 0; q < 5; q++) {
-      c1[q] = Rc(r, f1 + q);
-      c2[q] = Rc(r, f2 + q);
-    }
-#pragma unroll
-    for (int q = 0; q < 5; q++) k.put_if(q < n1, r.rev ? comp2(c1[q]) : c1[q]);
-    for (int q = 0; q < nm; q++) {
-      uint8_t ch = to_lower(litb(r, ls + (typ == PW_OP_SUB ? 0u : (uint32_t)(r.rev ? nm - 1 - q : q))));
-      k.put(r.rev ? r.tab->comp[ch] : ch);
-    }
-#pragma unroll
-    for (int q = 0; q < 5; q++) k.put_if(q < n2, r.rev ? comp2(c2[q]) : c2[q]);
-    return -1;
+  for (int q = 0; q < 5; q++) {
+    c1[q] = Rc(r, f1 + q);
+    c2[q] = Rc(r, f2 + q);
   }
-  if (defer) {
-    const int at = k.pos;
-    k.pos += tctx_field_len(cl);
-    return at;
+#pragma unroll
+  for (int q = 0; q < 5; q++) k.put_if(q < n1, r.rev ? comp2(c1[q]) : c1[q]);
+  for (int q = 0; q < nm; q++) {
+    uint8_t ch = to_lower(litb(r, ls + (typ == PW_OP_SUB ? 0u : (uint32_t)(r.rev ? nm - 1 - q : q))));
+    k.put(r.rev ? r.tab->comp[ch] : ch);
   }
+#pragma unroll
+  for (int q = 0; q < 5; q++) k.put_if(q < n2, r.rev ? comp2(c2[q]) : c2[q]);
+}
+
+// The tctx field by walking the op stream (setTContext, pafreport.cpp:120-128; revCompl :631;
+// abbreviation first5[len-10]last5, :918-927).
+template <class S>
+__device__ __forceinline__ void emit_tctx_walk(S& k, const Rec& r, uint32_t typ, int n, uint32_t j, uint32_t wd,
+                                               int qs, int ts, uint32_t ls) {
+  const TGeom g = tgeom(r.T, typ, n, ts);
   Cursor cur;
   cur.j = j;
   cur.ts = ts;
   cur.qs = qs;
   cur.ls = ls;
   cur.w = wd;
-  if (cl <= 10 + kMaxEv) {
-    emit_tseq(k, r, cur, tcs, tce, k.pos);
-    k.pos += cl;
-  } else {  // first5[len-10]last5 of the (oriented) context
-    emit_tseq(k, r, cur, r.rev ? tce - 5 : tcs, r.rev ? tce : tcs + 5, k.pos);
+  if (g.cl <= 10 + kMaxEv) {
+    emit_tseq(k, r, cur, g.tcs, g.tce, k.pos);
+    k.pos += g.cl;
+  } else {
+    emit_tseq(k, r, cur, r.rev ? g.tce - 5 : g.tcs, r.rev ? g.tce : g.tcs + 5, k.pos);
     k.pos += 5;
     k.put('[');
-    wr_dig(k, (uint32_t)(cl - 10));
+    wr_dig(k, (uint32_t)(g.cl - 10));
     k.put(']');
-    emit_tseq(k, r, cur, r.rev ? tcs : tce - 5, r.rev ? tcs + 5 : tce, k.pos);
+    emit_tseq(k, r, cur, r.rev ? g.tcs : g.tce - 5, r.rev ? g.tcs + 5 : g.tce, k.pos);
     k.pos += 5;
   }
-  return -1;
 }
 
 // S consequence, one codon of modseq (predictImpact, pafreport.cpp:811-826)
@@ -504,28 +544,24 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e)
   }
 }
 
-// Compute the event whose head op is `j` (record op index), segment slot `idx`, and write its
-// report line (printDiffInfo, pafreport.cpp:886-953) to the sink as the fields become known.
-// Returns the evtsub index failing the modseq check (pafreport.cpp:811-814), or -1; `rel`
-// receives rloc - r_trloc for the error message.
+// forward-query position the event's reads centre on (its final rloc, pafreport.cpp:597,615,633)
+__device__ __forceinline__ int event_rloc(int L, bool rev, uint32_t typ, int qp, int n) {
+  if (!rev) return qp;
+  return (typ == PW_OP_INS) ? L - qp : L - qp - n;
+}
+
+// Write one event's report line (printDiffInfo, pafreport.cpp:886-953) to the sink as the
+// fields become known.  Returns the evtsub index failing the modseq check
+// (pafreport.cpp:811-814), or -1; `rel` receives rloc - r_trloc for the error message.
 template <class S>
-__device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32_t wd, int qs, int ts, uint32_t ls,
-                                          bool skip, bool defer, int& rel, int& tpos) {
+__device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bool skip, int& rel) {
   Event e;
-  const uint32_t typ = wd >> 30;
-  const int qp = r.offset + qs;
+  const uint32_t typ = in.typ;
   e.type = typ;
-  e.q_pos = qp;
-  e.ls = ls;
-  e.n = event_len(r, j, wd);
-  int tloc;
-  if (!r.rev) {
-    e.rloc = qp;
-    tloc = ts;
-  } else {  // pafreport.cpp:597, 615, 633, 639
-    e.rloc = (typ == PW_OP_INS) ? r.L - qp : r.L - qp - e.n;
-    tloc = r.T - ts;
-  }
+  e.q_pos = in.qp;
+  e.ls = in.ls;
+  e.n = in.n;
+  e.rloc = event_rloc(r.L, r.rev, typ, in.qp, in.n);
   // amino acid at the event (pafreport.cpp:897-899)
   const int aap0 = e.rloc / 3;
   const uint8_t aa = translate(r.tab, Rc(r, 3 * aap0), Rc(r, 3 * aap0 + 1), Rc(r, 3 * aap0 + 2));
@@ -544,11 +580,6 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32
   k.put('\t');
   // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity
   const bool big = e.n > kMaxEv;
-#if PW_ABL & 32
-  const uint8_t b0 = 'A';
-  const bool same = e.n == 1;
-  k.put('A'); k.put(':'); k.put('C');
-#else
   if (typ == PW_OP_SUB) {
     if (big) {
       k.put('[');
@@ -574,19 +605,20 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32
     }
   }
   if (typ == PW_OP_DEL) k.put(':');
-#endif
   k.put('\t');
-  wr_dig(k, (uint32_t)(tloc + 1));
+  wr_dig(k, (uint32_t)(in.tloc + 1));
   k.put('\t');
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
-  tpos = emit_tctx(k, r, typ, e.n, j, wd, qs, ts, ls, defer);
+  if (in.tmode == 0) {
+    emit_tctx_fast(k, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
+  } else if (in.tmode == 1) {
+    const int tl = in.tx[0];
+    for (int q = 0; q < tl; q++) k.put(in.tx[1 + q]);
+  } else {
+    emit_tctx_walk(k, r, typ, e.n, in.j, in.wd, in.qs, in.ts, in.ls);
+  }
   k.put('\t');
   // ---- query context (getRefContext, pafreport.cpp:721-733) + status
-#if PW_ABL & 4
-  wr_lit(k, "ACGTACGTA\t[unknown]");
-  (void)same;
-  (void)b0;
-#else
   int c0 = e.rloc - 4, eloc = 4;
   if (c0 < 0) {
     eloc += c0;
@@ -634,26 +666,10 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32
 #pragma unroll
     for (int q = 0; q < 11; q++) k.put_if(q < sl, sw[q]);
   }
-#endif
   k.put('\t');
   // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
   int modseq_err = -1;
-#if PW_ABL & 2
-  if (!skip) wr_lit(k, "synonymous");
-  if (false) {
-#else
   if (!skip) {
-#endif
-#if PW_ABL & 128
-    if (typ == PW_OP_SUB) {
-      wr_lit(k, "synonymous");
-    } else
-#endif
-#if PW_ABL & 256
-    if (typ != PW_OP_SUB) {
-      wr_lit(k, "premature stop at AA1");
-    } else
-#endif
     if (typ == PW_OP_SUB) {
       for (int i = 0; i < e.n; i++)
         if (modseq_err < 0 && to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, e, i))) modseq_err = i;
@@ -687,314 +703,648 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, uint32_t j, uint32
   return modseq_err;
 }
 
-// ------------------------------------------------------------------ per-record driver
-// Work left for fixup_kernel: a target context that needs the op walk (pos = its position in
-// the line) or a whole line longer than the LDS line buffer (pos = kFixLine).
+// ------------------------------------------------------------------ workspace
+// Device scratch of one pass (pw_report_workspace_bytes):
+//   ctr      u32 [1] long-line count, [2] overflow flags; u64 at byte 16: arena bytes used
+//   rec_mod  per record: modseq error key (first failing line in output order)
+//   hot/cold per event slot (Hot, Cold); tx: pre-rendered target contexts
+//   fix      long-line list
 struct Fixup {
-  uint32_t ai, j;
-  int32_t qs, ts;
-  uint32_t ls, pos;
+  uint32_t s, pad;
   uint64_t dst;  // text offset of the line
 };
-constexpr uint32_t kFixLine = 0x80000000u;
-struct FixList {
-  Fixup* list;
-  uint32_t* count;
-  uint32_t cap;
+
+struct Work {
+  uint32_t* ctr;
+  unsigned long long* arena_used;
+  uint64_t* rec_mod;
+  Hot* hot;
+  Cold* cold;
+  uint8_t* tx;
+  Fixup* fix;
+  uint32_t fix_cap;
+  uint64_t n_slots, n_chunks;
+  uint64_t arena0;  // first arena byte in text (= n_chunks * PW_PAGE_BYTES)
 };
 
-__device__ __forceinline__ void process_record(const pw_report_args& A, const FixList& F, LDS Lds* S, uint32_t ai,
-                                               int lane) {
-  LDS WaveLds* w = &S->w;
+__host__ __device__ inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+// layout of the workspace; returns its size (base may be null to only size it)
+__host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots, uint64_t n_alns, Work* w) {
+  const uint64_t n_chunks = (n_slots + kWave - 1) / kWave;
+  const uint64_t ns = n_chunks * kWave;  // slot arrays padded to whole chunks
+  uint64_t o = 256;
+  const uint64_t o_rm = o;
+  o = align_up(o + 8 * n_alns, 256);
+  const uint64_t o_hot = o;
+  o = align_up(o + sizeof(Hot) * ns, 256);
+  const uint64_t o_cold = o;
+  o = align_up(o + sizeof(Cold) * ns, 256);
+  const uint64_t o_tx = o;
+  o = align_up(o + (uint64_t)kTx * ns, 256);
+  const uint64_t o_fix = o;
+  o = align_up(o + sizeof(Fixup) * (n_slots ? n_slots : 1), 256);
+  if (w && base) {
+    w->ctr = reinterpret_cast<uint32_t*>(base);
+    w->arena_used = reinterpret_cast<unsigned long long*>(base + 16);
+    w->rec_mod = reinterpret_cast<uint64_t*>(base + o_rm);
+    w->hot = reinterpret_cast<Hot*>(base + o_hot);
+    w->cold = reinterpret_cast<Cold*>(base + o_cold);
+    w->tx = base + o_tx;
+    w->fix = reinterpret_cast<Fixup*>(base + o_fix);
+    w->fix_cap = n_slots > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(n_slots ? n_slots : 1);
+    w->n_slots = n_slots;
+    w->n_chunks = n_chunks;
+    w->arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
+  }
+  return o;
+}
+
+__device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid, int nthreads) {
+  const uint8_t* s = reinterpret_cast<const uint8_t*>(&c_tables);
+  LDS uint8_t* d = reinterpret_cast<LDS uint8_t*>(dst);
+  for (int i = tid; i < 256; i += nthreads) {
+    d[offsetof(SmallTables, nt) + i] = s[offsetof(Tables, nt) + i];
+    d[offsetof(SmallTables, comp) + i] = s[offsetof(Tables, comp) + i];
+  }
+  for (int i = tid; i < 64; i += nthreads) d[offsetof(SmallTables, codon64) + i] = s[offsetof(Tables, codon64) + i];
+  for (int i = tid; i < 96; i += nthreads) d[offsetof(SmallTables, status) + i] = s[offsetof(Tables, status) + i];
+}
+
+// ------------------------------------------------------------------ index_kernel
+constexpr int kTxStride = 48;              // index_kernel: per-lane target-context buffer
+constexpr int kOpWin = kSegOps + 2 * kOpHalo;
+struct IndexWave {
+  uint32_t opw[kOpWin];            // op words of the segment + halo
+  int32_t ots[kOpWin];             // their target / query / literal starts
+  int32_t oqs[kOpWin];
+  uint32_t ols[kOpWin];
+  int32_t xoff[kWave];             // slow contexts: first item of each lane's context
+  uint8_t tx[kWave * kTxStride];   // per-lane target-context field (length byte + bytes; [40] = walk)
+  uint8_t junk[kWave];
+};
+
+__device__ __forceinline__ int ndigits(uint32_t v) {
+  return 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
+         (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
+}
+
+__device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
+                                             LDS IndexWave* w, uint32_t ai, int lane) {
   const pw_aln_desc d = A.desc[ai];
   const uint32_t qi = d.ref & 0x7FFFFFFFu;
-  Rec r;
-  r.ops = A.ops + d.op_begin;
-  r.lits = A.lits;
-  r.R = A.qseq + A.qoff[qi];
-  r.L = A.qlen[qi];
-  r.NS = A.next_stop ? A.next_stop + A.qoff[qi] : nullptr;
-  r.tab = &S->tab;
-  r.qw = w->qw;
-  r.lw = w->lw;
-  r.opw = w->opw;
-  r.offset = d.offset;
-  r.T = d.t_len;
-  r.n_ops = d.n_ops;
-  r.rev = (d.ref & PW_REF_REVERSE) != 0;
-  const bool skip = A.skip_codan != 0;
-  const uint64_t slot_lo = d.text_begin;
-  const uint64_t slot_hi = (ai + 1 < A.n_alns) ? A.desc[ai + 1].text_begin : A.text_total;
-  uint64_t out_lo = slot_lo, out_hi = slot_hi;
+  const uint32_t* ops = A.ops + d.op_begin;
+  const uint64_t qb = A.qoff[qi];
+  const uint8_t* R = A.qseq + qb;
+  const int L = A.qlen[qi];
+  const bool rev = (d.ref & PW_REF_REVERSE) != 0;
+  const int T = d.t_len;
+  const uint32_t n_ops = d.n_ops;
+  const uint64_t evb = d.ev_begin;
+  const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
+  const uint32_t nmax = (uint32_t)(ev_next - evb);
+  const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
+  LDS uint8_t* my_tx = w->tx + lane * kTxStride;
 
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
-  bool prev_sub = false, fix_overflow = false;
-  uint32_t ev_idx = 0;
-  int me_first = INT_MAX, me_last = -1, me_fa = 0, me_fb = 0, me_la = 0, me_lb = 0;  // modseq errors
-  LDS uint8_t* my_line = w->line + lane * kLine;
+  bool prev_sub = false;
+  uint32_t ev = 0;
+  int err = PW_REC_OK, err_a = 0, err_b = 0, err_c = 0;
 
-  for (uint32_t sb = 0; sb < r.n_ops;) {
-    // ---- 1. op words + scan (2 ops per lane, op sb + 64k + lane)
-    uint32_t wd[2], qa[2], ta[2], la[2];
+  for (uint32_t sb = 0; sb < n_ops; sb += kSegOps) {
+    const uint32_t nseg = (n_ops - sb) < (uint32_t)kSegOps ? (n_ops - sb) : (uint32_t)kSegOps;
+    // ---- op words (2 per lane) + wave scans of the query / target / literal advances
+    uint32_t wd[2];
     int qs[2], ts[2];
     uint32_t ls[2];
     uint32_t qtot = 0, ttot = 0, ltot = 0;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-      const uint32_t j = sb + 64 * k + lane;
-      wd[k] = j < r.n_ops ? r.ops[j] : 0u;
-      qa[k] = op_qadv(wd[k]);
-      ta[k] = op_tadv(wd[k]);
-      la[k] = op_ladv(wd[k]);
-      const uint32_t qi_ = wave_incl_scan(qa[k], lane), ti_ = wave_incl_scan(ta[k], lane),
-                     li_ = wave_incl_scan(la[k], lane);
-      qs[k] = qc + (int)(qtot + qi_ - qa[k]);
-      ts[k] = tc + (int)(ttot + ti_ - ta[k]);
-      ls[k] = lc + ltot + li_ - la[k];
+      const uint32_t idx = 64 * k + lane;
+      wd[k] = idx < nseg ? ops[sb + idx] : 0u;
+      const uint32_t qa = idx < nseg ? op_qadv(wd[k]) : 0u, ta = idx < nseg ? op_tadv(wd[k]) : 0u,
+                     la = idx < nseg ? op_ladv(wd[k]) : 0u;
+      const uint32_t qi_ = wave_incl_scan(qa, lane), ti_ = wave_incl_scan(ta, lane), li_ = wave_incl_scan(la, lane);
+      qs[k] = qc + (int)(qtot + qi_ - qa);
+      ts[k] = tc + (int)(ttot + ti_ - ta);
+      ls[k] = lc + ltot + li_ - la;
       qtot += bcast(qi_, 63);
       ttot += bcast(ti_, 63);
       ltot += bcast(li_, 63);
+      w->opw[kOpHalo + idx] = wd[k];
+      w->ots[kOpHalo + idx] = idx < nseg ? ts[k] : INT_MAX;
+      w->oqs[kOpHalo + idx] = qs[k];
+      w->ols[kOpHalo + idx] = ls[k];
     }
-    // ---- 2. segment length: query / literal spans must fit the windows
-    uint32_t nseg = 0;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const uint32_t j = sb + 64 * k + lane;
-      const bool fits = j < r.n_ops && (uint32_t)(qs[k] + (int)qa[k] - qc) <= (uint32_t)(kQW - 2 * kQPad - 16) &&
-                        (ls[k] + la[k] - lc) <= (uint32_t)(kLW - 2 * kLPad - 16);
-      nseg += (uint32_t)__popcll(__ballot(fits));
-    }
-    if (nseg == 0) nseg = 1;
-    // ---- 3. stage op words (+halo), starts
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const uint32_t idx = 64 * k + lane;
-      if (idx < nseg) {
-        w->opw[kOpHalo + idx] = wd[k];
-        w->qs[idx] = qs[k];
-        w->ts[idx] = ts[k];
-        w->ls[idx] = ls[k];
+    {  // halo: op words before / after the segment and their coordinates
+      const bool h = lane < 2 * kOpHalo;
+      const int j = lane < kOpHalo ? (int)sb - kOpHalo + lane : (int)(sb + nseg) + (lane - kOpHalo);
+      const bool valid = h && j >= 0 && (uint32_t)j < n_ops;
+      const uint32_t v = valid ? ops[j] : 0u;
+      const uint32_t qa = op_qadv(v), ta = op_tadv(v), la = op_ladv(v);
+      const uint32_t qi_ = wave_incl_scan(qa, lane), ti_ = wave_incl_scan(ta, lane), li_ = wave_incl_scan(la, lane);
+      const uint32_t q16 = bcast(qi_, kOpHalo - 1), t16 = bcast(ti_, kOpHalo - 1), l16 = bcast(li_, kOpHalo - 1);
+      const uint32_t qx = qi_ - qa, tx_ = ti_ - ta, lx = li_ - la;  // exclusive prefixes
+      if (h) {
+        const int pos = lane < kOpHalo ? lane : kOpHalo + (int)nseg + (lane - kOpHalo);
+        w->opw[pos] = v;
+        if (lane < kOpHalo) {  // before: segment start minus the advances from here to it
+          w->ots[pos] = valid ? tc - (int)(t16 - tx_) : INT_MIN;
+          w->oqs[pos] = qc - (int)(q16 - qx);
+          w->ols[pos] = lc - (l16 - lx);
+        } else {  // after: segment end plus the advances before
+          w->ots[pos] = valid ? tc + (int)ttot + (int)(tx_ - t16) : INT_MAX;
+          w->oqs[pos] = qc + (int)qtot + (int)(qx - q16);
+          w->ols[pos] = lc + ltot + (lx - l16);
+        }
       }
     }
-    if (lane < 2 * kOpHalo) {
-      const int j = lane < kOpHalo ? (int)sb - kOpHalo + lane : (int)(sb + nseg) + (lane - kOpHalo);
-      const uint32_t v = (j >= 0 && (uint32_t)j < r.n_ops) ? r.ops[j] : 0u;
-      w->opw[lane < kOpHalo ? lane : kOpHalo + nseg + (lane - kOpHalo)] = v;
-    }
-    r.op_lo = (int)sb - kOpHalo;
-    r.op_n = nseg + 2 * kOpHalo;
-    uint32_t sq = 0, st = 0, sl = 0;  // segment totals
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const bool in = (uint32_t)(64 * k + lane) < nseg;
-      sq += in ? qa[k] : 0u;
-      st += in ? ta[k] : 0u;
-      sl += in ? la[k] : 0u;
-    }
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) {
-      sq += __shfl_xor(sq, dd, kWave);
-      st += __shfl_xor(st, dd, kWave);
-      sl += __shfl_xor(sl, dd, kWave);
-    }
-    // ---- 4. forward-query window: aligned span [offset+qc-pad, offset+qc+sq+pad)
-    {
-      const int a0q = r.offset + qc - kQPad, a1q = r.offset + qc + (int)sq + kQPad;
-      int f0 = r.rev ? r.L - a1q : a0q;
-      if (f0 < 0) f0 = 0;
-      if (f0 > r.L) f0 = r.L;
-      const uintptr_t abs0 = (uintptr_t)(r.R + f0) & ~(uintptr_t)15;
-      r.qlo = (int)((intptr_t)abs0 - (intptr_t)r.R);
-      const intptr_t avail = (intptr_t)(r.R + r.L) - (intptr_t)abs0;  // bytes up to the query end
-      int nbytes = (int)((avail + 15) & ~(intptr_t)15);
-      if (nbytes > kQW) nbytes = kQW;
-      for (int o = lane * 16; o < nbytes; o += kWave * 16)
-        *reinterpret_cast<LDS v4u*>(w->qw + o) = *reinterpret_cast<const v4u*>(abs0 + o);
-    }
-    // ---- 5. literal window [lc - pad, lc + sl + pad)
-    {
-      const uint32_t l0 = lc > (uint32_t)kLPad ? lc - kLPad : 0u;
-      const uintptr_t abs0 = (uintptr_t)(r.lits + l0) & ~(uintptr_t)15;
-      r.l_lo = (uint32_t)((const uint8_t*)abs0 - r.lits);
-      uint32_t nbytes = (lc + sl + kLPad - r.l_lo + 15) & ~15u;
-      if (nbytes > (uint32_t)kLW) nbytes = kLW;
-      r.l_n = nbytes;
-      for (uint32_t o = lane * 16; o < nbytes; o += kWave * 16)
-        *reinterpret_cast<LDS v4u*>(w->lw + o) = *reinterpret_cast<const v4u*>(abs0 + o);
-    }
-    wave_sync();
-
-    // ---- 6. base check of every '*' op (pafreport.cpp:550-554) and S-run heads
-    uint64_t hm[2];
-    uint32_t sm_prev = prev_sub ? 1u : 0u;
+    // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads
+    uint64_t subm[2], hm[2];
     int bad_idx = INT_MAX;
-    int bad_qp = 0, bad_q = 0, bad_r = 0;
+    uint32_t sm_prev = prev_sub ? 1u : 0u;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const uint32_t idx = 64 * k + lane;
       const bool in = idx < nseg;
       const uint32_t typ = wd[k] >> 30;
       const bool is_sub = in && typ == PW_OP_SUB;
-      const uint64_t subm = __ballot(is_sub);
-      const bool prevsub = lane == 0 ? sm_prev != 0 : ((subm >> (lane - 1)) & 1ull) != 0;
-      sm_prev = (uint32_t)((subm >> 63) & 1ull);
+      subm[k] = __ballot(is_sub);
+      const bool prevsub = lane == 0 ? sm_prev != 0 : ((subm[k] >> (lane - 1)) & 1ull) != 0;
+      sm_prev = (uint32_t)((subm[k] >> 63) & 1ull);
       hm[k] = __ballot(in && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub)));
       bool bad = false;
       uint8_t qch = 0, rch = 0;
-      const int qp = r.offset + qs[k];
+      const int qp = d.offset + qs[k];
       if (is_sub) {
-        qch = litb(r, ls[k] + 1);
-        rch = aligned_char(r, qp);
+        qch = A.lits[ls[k] + 1];
+        rch = aligned_char_g(R, L, rev, tab, qp);
         bad = qch != rch;
       }
       const uint64_t bm = __ballot(bad);
       if (bm && bad_idx == INT_MAX) {
         const int fl = __builtin_ctzll(bm);
         bad_idx = 64 * k + fl;
-        bad_qp = __shfl(qp, fl, kWave);
-        bad_q = __shfl((int)qch, fl, kWave);
-        bad_r = __shfl((int)rch, fl, kWave);
+        err_a = __shfl(qp, fl, kWave);
+        err_b = __shfl((int)qch, fl, kWave);
+        err_c = __shfl((int)rch, fl, kWave);
       }
-    }
-    if (bad_idx != INT_MAX) {
-      if (lane == 0) {
-        pw_aln_result res;
-        res.text_off = slot_lo;
-        res.text_len = 0;
-        res.n_events = 0;
-        res.err = PW_REC_MISMATCH;
-        res.err_a = bad_qp;
-        res.err_b = bad_q;
-        res.err_c = bad_r;
-        A.results[ai] = res;
-      }
-      return;
-    }
-    // compact the heads into the event list
-    const uint32_t n0 = (uint32_t)__popcll(hm[0]);
-    const uint32_t nev = n0 + (uint32_t)__popcll(hm[1]);
-    {
-      const uint64_t lt = (1ull << lane) - 1ull;
-      if ((hm[0] >> lane) & 1ull) w->evl[__popcll(hm[0] & lt)] = (uint16_t)lane;
-      if ((hm[1] >> lane) & 1ull) w->evl[n0 + __popcll(hm[1] & lt)] = (uint16_t)(64 + lane);
     }
     wave_sync();
-    prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;  // carry into the next segment
-
-    // ---- 7. events, 64 per round: each lane writes its line into its LDS line buffer
-    for (uint32_t e0 = 0; e0 < nev; e0 += kWave) {
-      const uint32_t ei = e0 + lane;
-      const bool act = ei < nev;
-      const uint32_t idx = act ? w->evl[ei] : 0u;
-      int linelen = 0, merr = -1, rel = 0, tpos = -1;
-      if (act) {
-        LineSink k;
-        k.buf = my_line;
-        k.junk = w->junk + lane;
-        k.pos = 0;
-        merr = emit_event(k, r, sb + idx, w->opw[kOpHalo + idx], w->qs[idx], w->ts[idx], w->ls[idx], skip, true,
-                          rel, tpos);
-        linelen = k.pos;
-      }
-      // modseq errors: first / last failing event of the record (in creation order)
-      {
-        const uint64_t fm = __ballot(merr >= 0);
-        if (fm) {
-          const int lo = __builtin_ctzll(fm), hi = 63 - __builtin_clzll(fm);
-          const int fi_lo = __shfl(merr, lo, kWave), fi_hi = __shfl(merr, hi, kWave);
-          const int rl_lo = __shfl(rel, lo, kWave), rl_hi = __shfl(rel, hi, kWave);
-          const int gi_lo = (int)(ev_idx + e0) + lo, gi_hi = (int)(ev_idx + e0) + hi;
-          if (gi_lo < me_first) {
-            me_first = gi_lo;
-            me_fa = rl_lo + fi_lo;
-            me_fb = fi_lo;
+    if (bad_idx != INT_MAX) {
+      err = PW_REC_MISMATCH;
+      break;
+    }
+    // ---- events of this segment: creation index, S-run length, target context
+    const uint32_t n0 = (uint32_t)__popcll(hm[0]);
+    const uint32_t nev = n0 + (uint32_t)__popcll(hm[1]);
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t idx = 64 * k + lane;
+      const uint32_t typ = wd[k] >> 30;
+      bool slow = false;
+      uint64_t s = 0;
+      TGeom g;
+      uint32_t n = 0;
+      if ((hm[k] >> lane) & 1ull) {
+        if (typ != PW_OP_SUB) {
+          n = wd[k] & 0x3FFFFFFFu;
+        } else {  // run of '*' ops from idx: first non-'*' op at or after it
+          const uint64_t ns0 = ~subm[0], ns1 = ~subm[1];
+          uint32_t end;
+          const uint64_t r0 = k == 0 ? (ns0 >> lane) : 0ull;
+          if (k == 0 && r0) end = (uint32_t)lane + (uint32_t)__builtin_ctzll(r0);
+          else {
+            const uint64_t r1 = k == 0 ? ns1 : (ns1 >> lane);
+            end = r1 ? (k == 0 ? 64u + (uint32_t)__builtin_ctzll(r1)
+                               : 64u + (uint32_t)lane + (uint32_t)__builtin_ctzll(r1))
+                     : 128u;
           }
-          if (gi_hi > me_last) {
-            me_last = gi_hi;
-            me_la = rl_hi + fi_hi;
-            me_lb = fi_hi;
+          n = end - idx;
+          if (end >= 128u) {  // the run continues past the segment
+            uint32_t jj = sb + 128u;
+            while (jj < n_ops && (ops[jj] >> 30) == PW_OP_SUB) {
+              n++;
+              jj++;
+            }
           }
         }
-      }
-      const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
-      const uint32_t B = bcast(incl, kWave - 1);
-      const uint32_t my_off = r.rev ? (B - incl) : (incl - (uint32_t)linelen);
-      if (B == 0) continue;
-      if (out_hi - out_lo < B) {  // host slot bound violated: report, never write outside the slot
-        if (lane == 0) {
-          pw_aln_result res = {};
-          res.text_off = slot_lo;
-          res.err = 3;
-          A.results[ai] = res;
+        const uint32_t j = sb + idx;
+        g = tgeom(T, typ, (int)n, ts[k]);
+        const uint32_t pw = w->opw[kOpHalo + idx - 1], aw = w->opw[kOpHalo + idx + 1];
+        const bool fast = tctx_fast(g, typ, (int)n, pw, j > 0, aw, j + 1 < n_ops);
+        const uint32_t kidx = ev + (k == 0 ? (uint32_t)__popcll(hm[0] & lt) : n0 + (uint32_t)__popcll(hm[1] & lt));
+        if (kidx < nmax) {
+          s = rev ? evb + nmax - 1 - kidx : evb + kidx;
+          // first / last line of the record in output order: the first created event is flagged
+          // here, the last created one once the record is done (below)
+          const bool first = !rev && kidx == 0, last = rev && kidx == 0;
+          // the event's first 8 literal bytes
+          const uint32_t la = ls[k] >> 2, sh = ls[k] & 3u;
+          const uint32_t w0 = lits32[la], w1 = lits32[la + 1], w2 = lits32[la + 2];
+          Hot hh;
+          hh.qb = (uint32_t)qb;
+          hh.L = L;
+          hh.qp = d.offset + qs[k];
+          hh.tloc = rev ? T - ts[k] : ts[k];
+          hh.ls = ls[k];
+          hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, n);
+          hh.l0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+          hh.l1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+          W.hot[s] = hh;
+          Cold cd;
+          cd.ai = ai;
+          cd.j = j;
+          cd.qs = qs[k];
+          cd.ts = ts[k];
+          W.cold[s] = cd;
+          slow = !fast && !(PW_ABL & 32);
         }
-        return;
       }
-      uint64_t g0;
-      if (!r.rev) {
-        g0 = out_lo;
-        out_lo += B;
-      } else {
-        out_hi -= B;
-        g0 = out_hi;
-      }
-      // deferred work -> fixup list (one wave-aggregated atomic)
-      {
-        const bool need = act && (linelen > kLine || tpos >= 0);
-        const uint64_t nm = __ballot(need);
-        if (nm) {
-          uint32_t base = 0;
-          if (lane == 0) base = atomicAdd(F.count, (uint32_t)__popcll(nm));
-          base = bcast(base, 0);
-          const uint32_t slot = base + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
-          if (need && slot < F.cap) {
-            Fixup f;
-            f.ai = ai;
-            f.j = sb + idx;
-            f.qs = w->qs[idx];
-            f.ts = w->ts[idx];
-            f.ls = w->ls[idx];
-            f.pos = linelen > kLine ? kFixLine : (uint32_t)tpos;
-            f.dst = g0 + my_off;
-            F.list[slot] = f;
+      // ---- target contexts that are not a plain query copy (another event within 5 bases,
+      // an S run, a long insertion), all of this half-segment at once: every byte of every such
+      // context is one item, a lane resolves one item per round by a binary search over the op
+      // target starts in LDS (tseq is never materialised, pafreport.cpp:543,575,588)
+      if (__ballot(slow) == 0ull) continue;
+      const bool abbr = g.cl > 10 + kMaxEv;
+      const int ndig = abbr ? ndigits((uint32_t)(g.cl - 10)) : 0;
+      const uint32_t npos = slow ? (uint32_t)(abbr ? 10 : g.cl) : 0u;
+      const uint32_t incl = wave_incl_scan(npos, lane);
+      const uint32_t nitems = bcast(incl, kWave - 1);
+      w->xoff[lane] = (int32_t)(incl - npos);
+      if (slow) my_tx[40] = 0;
+      const int xtcs = g.tcs, xtce = g.tce;
+      wave_sync();
+      for (uint32_t i0 = 0; i0 < nitems; i0 += kWave) {
+        // (the shuffles run with every lane active: a shuffle from an inactive lane reads 0)
+        const bool active = i0 + (uint32_t)lane < nitems;
+        const int item = active ? (int)(i0 + (uint32_t)lane) : (int)nitems - 1;
+        int o = 0;  // owner lane: the last lane whose first item is <= item
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+          if (w->xoff[o + step] <= item) o += step;
+        const int tcs = __shfl(xtcs, o, kWave), tce = __shfl(xtce, o, kWave);
+        const int ond = __shfl(ndig, o, kWave);
+        if (active) {
+          const int q = item - w->xoff[o];
+          const int ocl = tce - tcs;
+          const bool oabbr = ocl > 10 + kMaxEv;
+          int tp, outp;
+          if (!oabbr || q < 5) {
+            tp = rev ? tce - 1 - q : tcs + q;
+            outp = q;
+          } else {
+            const int q2 = q - 5;
+            tp = rev ? tcs + 4 - q2 : tce - 5 + q2;
+            outp = 5 + 1 + ond + 1 + q2;
           }
-          fix_overflow = fix_overflow || (__ballot(need && slot >= F.cap) != 0ull);
-        }
-      }
-      // line starts in output order (k-th line = lane k, or lane 63-k for '-' records) and the
-      // chunk map: 16-byte chunk ci of the aligned destination -> line holding its first byte
-      uint8_t* const dst = A.text + g0;
-      const uint32_t shift = (uint32_t)((uintptr_t)dst & 15);
-      uint8_t* const gb = dst - shift;  // 16-byte aligned
-      const uint32_t end = shift + B;
-      {
-        const int oi = r.rev ? kWave - 1 - lane : lane;
-        w->ostart[oi] = my_off;
-        w->olane[oi] = (uint8_t)lane;
-        if (lane == 0) w->ostart[kWave] = B;
-        if (linelen > 0) {
-          const uint32_t c1 = (my_off + (uint32_t)linelen + shift + 15) >> 4;
-          if (my_off == 0) w->cmap[0] = (uint8_t)oi;
-          for (uint32_t ci = (my_off + shift + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) w->cmap[ci] = (uint8_t)oi;
+          // op covering target position tp: the last op whose target start is <= tp
+          int lo = 0, hi = kOpHalo + (int)nseg + kOpHalo - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (w->ots[mid] <= tp) lo = mid;
+            else hi = mid - 1;
+          }
+          const uint32_t ow = w->opw[lo];
+          const int ot = w->ots[lo];
+          const int off = tp - ot;
+          const uint32_t oty = ow >> 30;
+          const bool covered = ot != INT_MIN && ot <= tp && off < (int)op_tadv(ow);
+          uint8_t ch = 0;
+          if (covered) {
+            if (oty == PW_OP_MATCH) {
+              const int x = d.offset + w->oqs[lo] + off;  // aligned-strand query position
+              ch = (x < 0 || x >= L) ? 0 : (rev ? comp2(R[L - 1 - x]) : R[x]);
+            } else {
+              ch = to_lower(A.lits[w->ols[lo] + (oty == PW_OP_SUB ? 0u : (uint32_t)off)]);
+              if (rev) ch = tab->comp[ch];
+            }
+          }
+          LDS uint8_t* otx = w->tx + o * kTxStride;
+          otx[1 + outp] = ch;
+          if (!covered) otx[40] = 1;
         }
       }
       wave_sync();
-#if PW_ABL & 16
-      if (true) {
-        wave_sync();
-        continue;
+      if (slow) {
+        int len = (int)npos;
+        if (abbr) {  // first5[len-10]last5
+          my_tx[1 + 5] = '[';
+          uint32_t v = (uint32_t)(g.cl - 10);
+          for (int q = ndig - 1; q >= 0; q--) {
+            my_tx[1 + 6 + q] = (uint8_t)('0' + v % 10u);
+            v /= 10u;
+          }
+          my_tx[1 + 6 + ndig] = ']';
+          len = 12 + ndig;
+        }
+        if (my_tx[40]) {  // the context reaches past the staged ops: walk the op stream
+          Rec rr;
+          rr.ops = ops;
+          rr.lits = A.lits;
+          rr.R = R;
+          rr.NS = nullptr;
+          rr.tab = tab;
+          rr.qw = nullptr;
+          rr.qlo = 0;
+          rr.qn = 0;
+          rr.opw = w->opw;
+          rr.op_lo = (int)sb - kOpHalo;
+          rr.op_n = nseg + 2 * kOpHalo;
+          rr.lit0 = rr.lit1 = 0;
+          rr.ls0 = 0;
+          rr.ln = 0;
+          rr.lw = nullptr;
+          rr.l_lo = 0;
+          rr.l_n = 0;
+          rr.L = L;
+          rr.offset = d.offset;
+          rr.T = T;
+          rr.n_ops = n_ops;
+          rr.rev = rev;
+          LdsSink<kTx - 1> ks;
+          ks.buf = my_tx + 1;
+          ks.junk = w->junk + lane;
+          ks.pos = 0;
+          emit_tctx_walk(ks, rr, typ, (int)n, sb + idx, wd[k], qs[k], ts[k], ls[k]);
+          len = ks.pos;
+        }
+        my_tx[0] = (uint8_t)len;
+        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(my_tx);
+        v4u t0, t1;
+        t0.x = t32[0];
+        t0.y = t32[1];
+        t0.z = t32[2];
+        t0.w = t32[3];
+        t1.x = t32[4];
+        t1.y = t32[5];
+        t1.z = t32[6];
+        t1.w = t32[7];
+        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
+        dtx[0] = t0;
+        dtx[1] = t1;
       }
+      wave_sync();
+    }
+    ev += nev;
+    prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;
+    qc += (int)qtot;
+    tc += (int)ttot;
+    lc += ltot;
+    wave_sync();
+  }
+  if (ev > nmax) {  // host event bound violated (cannot happen: every head is a counted op)
+    err = 3;
+    ev = nmax;
+  }
+  // empty slots: merged '*' runs, or everything after a failure
+  const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;
+  for (uint64_t s = h0 + lane; s < h1; s += kWave) W.hot[s].fn = kNoEv;
+  if (lane == 0 && ev > 0 && err == PW_REC_OK) {
+    const uint64_t s_last = rev ? evb + nmax - ev : evb + ev - 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's store of that record first
+    atomicOr(&W.hot[s_last].fn, rev ? 1u << 27 : 1u << 26);
+  }
+  if (lane == 0) {
+    pw_aln_result res;
+    res.text_off = res.text_end = 0;
+    res.page_first = res.page_last = 0;
+    res.text_len = 0;
+    res.n_events = ev;
+    res.err = err;
+    res.err_a = err_a;
+    res.err_b = err_b;
+    res.err_c = err_c;
+    A.results[ai] = res;
+    W.rec_mod[ai] = ~0ull;
+  }
+}
+
+__global__ __launch_bounds__(kWave* kWaves) void index_kernel(pw_report_args A, Work W) {
+  __shared__ SmallTables tab;
+  __shared__ IndexWave iw[kWaves];
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, kWave * kWaves);
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  LDS IndexWave* w = (LDS IndexWave*)&iw[wv];
+  for (uint32_t ai = blockIdx.x * kWaves + wv; ai < A.n_alns; ai += gridDim.x * kWaves) index_record(A, W, tp, w, ai, lane);
+  // the padding slots of the last chunk are empty
+  const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
+  if (blockIdx.x == 0)
+    for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) W.hot[s].fn = kNoEv;
+}
+
+// ------------------------------------------------------------------ render_kernel
+struct RenderWave {
+  uint8_t line[kWave * kLStride];   // per-lane line buffers
+  uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
+  uint32_t ostart[kWave + 1];       // line starts in the page
+  uint8_t junk[kWave];
+  uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
+};
+
+__device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
+  Hot h;
+  if (c < W.n_chunks) {
+    const v4u* p = reinterpret_cast<const v4u*>(W.hot + c * kWave + lane);
+    const v4u a = p[0], b = p[1];
+    h.qb = a.x;
+    h.L = (int32_t)a.y;
+    h.qp = (int32_t)a.z;
+    h.tloc = (int32_t)a.w;
+    h.ls = b.x;
+    h.fn = b.y;
+    h.l0 = b.z;
+    h.l1 = b.w;
+  } else {
+    h.fn = kNoEv;
+  }
+  return h;
+}
+
+// Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
+// inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
+// chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).
+__global__ __launch_bounds__(kWave* kWaves, 3) void render_kernel(pw_report_args A, Work W) {
+  __shared__ SmallTables tab;
+  __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, kWave * kWaves);
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
+  LDS uint8_t* my_line = w->line + lane * kLStride;
+  LDS uint8_t* my_qw = w->qw + lane * kQStride;
+  const bool skip = A.skip_codan != 0;
+  const uint64_t nw = (uint64_t)gridDim.x * kWaves;
+
+  uint64_t c = (uint64_t)blockIdx.x * kWaves + wv;
+  Hot h = load_hot(W, c, lane);
+  for (; c < W.n_chunks; c += nw) {
+    const uint64_t s = c * kWave + (uint64_t)lane;
+    const bool act = h.fn != kNoEv;
+    int linelen = 0;
+    if (act) {
+      const uint32_t typ = h.fn >> 30;
+      const bool rev = (h.fn >> 29) & 1u;
+      int n = (int)(h.fn & kNBig);
+      Rec r;
+      r.lits = A.lits;
+      r.R = A.qseq + h.qb;
+      r.L = h.L;
+      r.NS = A.next_stop ? A.next_stop + h.qb : nullptr;
+      r.tab = tp;
+      r.opw = nullptr;
+      r.op_lo = 0;
+      r.op_n = 0;
+      r.lw = nullptr;
+      r.l_lo = 0;
+      r.l_n = 0;
+      r.lit0 = h.l0;
+      r.lit1 = h.l1;
+      r.ls0 = h.ls;
+      r.ln = 8;
+      r.rev = rev;
+      r.offset = 0;
+      r.T = 0;
+      r.qn = 0;
+      if ((uint32_t)n == kNBig) {  // saturated length: from the op stream
+        const Cold cd = W.cold[s];
+        const pw_aln_desc d = A.desc[cd.ai];
+        r.ops = A.ops + d.op_begin;
+        r.n_ops = d.n_ops;
+        n = event_len(r, cd.j, r.ops[cd.j]);
+      }
+      r.ops = nullptr;
+      r.n_ops = 0;
+      // per-lane window: 64 forward-query bytes from 24 before the event (16-byte aligned)
+      const int rl = event_rloc(r.L, rev, typ, h.qp, n);
+      int x0 = rl - 24;
+      if (x0 < 0) x0 = 0;
+      const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;  // >= qseq (16-byte aligned)
+#pragma unroll
+      for (int q = 0; q < kQWin / 16; q++) {
+        const v4u v = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){v.x, v.y};
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){v.z, v.w};
+      }
+      r.qw = my_qw;
+      r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+      r.qn = (PW_ABL & 4) ? 0 : kQWin;
+      EvIn in;
+      in.typ = typ;
+      in.n = n;
+      in.qp = h.qp;
+      in.tloc = h.tloc;
+      in.ls = h.ls;
+      in.tmode = ((h.fn >> 28) & 1u) || (PW_ABL & 64) ? 0 : 1;
+      in.ll = (int)((h.fn >> 23) & 7u);
+      in.rl = (int)((h.fn >> 20) & 7u);
+      in.tx = W.tx + (uint64_t)kTx * s;
+      in.j = in.wd = 0;
+      in.qs = in.ts = 0;
+      LineSink k;
+      k.buf = my_line;
+      k.junk = w->junk + lane;
+      k.pos = 0;
+      int rel = 0;
+#if PW_ABL & 1
+      const int merr = -1;
+      k.pos = 76;
+#else
+      const int merr = emit_event(k, r, in, skip || (PW_ABL & 2), rel);
 #endif
+      linelen = k.pos;
+      if (merr >= 0) {  // modseq error: first failing event of the record in output order
+        const uint32_t ai = W.cold[s].ai;
+        const pw_aln_desc d = A.desc[ai];
+        const uint64_t evb = d.ev_begin;
+        const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
+        const uint64_t nmax = ev_next - evb, nev = A.results[ai].n_events;
+        const uint64_t first = rev ? evb + nmax - nev : evb;
+        const uint64_t key = (s - first) << 40 | (uint64_t)((uint32_t)(rel + merr) & 0xFFFFFu) << 20 |
+                             (uint64_t)((uint32_t)merr & 0xFFFFFu);
+        atomicMin((unsigned long long*)&W.rec_mod[ai], (unsigned long long)key);
+      }
+    }
+    const uint32_t fn_cur = h.fn;
+    h = load_hot(W, c + nw, lane);  // the next chunk's records load behind this one's output
+    const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
+    const uint32_t B = bcast(incl, kWave - 1);
+    const uint32_t my_off = incl - (uint32_t)linelen;
+    // the page: in place, or an arena allocation when the lines do not fit
+    uint64_t P = c * (uint64_t)PW_PAGE_BYTES;
+    bool ok = true;
+    if (B > (uint32_t)PW_PAGE_BYTES) {
+      unsigned long long a = 0;
+      if (lane == 0) a = atomicAdd(W.arena_used, (unsigned long long)((B + 15u) & ~15u));
+      a = __shfl(a, 0, kWave);
+      P = W.arena0 + a;
+      if (P + B > A.text_total) {  // capacity violated: report, never write outside
+        ok = false;
+        if (lane == 0) atomicOr(&W.ctr[2], 1u);
+      }
+    }
+    if (lane == 0) {
+      pw_page pg;
+      pg.off = P;
+      pg.len = ok ? B : 0u;
+      pg.pad = 0;
+      A.pages[c] = pg;
+    }
+    const uint64_t g0 = P + my_off;
+    if (act && (fn_cur & (3u << 26))) {  // first / last line of a record
+      const uint32_t ai = W.cold[s].ai;
+      if ((fn_cur >> 27) & 1u) {
+        A.results[ai].text_off = g0;
+        A.results[ai].page_first = (uint32_t)c;
+      }
+      if ((fn_cur >> 26) & 1u) {
+        A.results[ai].text_end = g0 + (uint64_t)linelen;
+        A.results[ai].page_last = (uint32_t)c;
+      }
+    }
+    if (ok && B > 0 && !(PW_ABL & 16)) {
+      // long lines -> fixup list (one wave-aggregated atomic)
+      const bool need = linelen > kLine;
+      const uint64_t nm = __ballot(need);
+      if (nm) {
+        uint32_t fb = 0;
+        if (lane == 0) fb = atomicAdd(&W.ctr[1], (uint32_t)__popcll(nm));
+        fb = bcast(fb, 0);
+        const uint32_t slot = fb + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+        if (need && slot < W.fix_cap) {
+          Fixup f;
+          f.s = (uint32_t)s;
+          f.pad = 0;
+          f.dst = g0;
+          W.fix[slot] = f;
+        }
+        if (__ballot(need && slot >= W.fix_cap) && lane == 0) atomicOr(&W.ctr[2], 2u);
+      }
+      // chunk map: 16-byte block ci of the page -> line holding its first byte (P is 16-byte
+      // aligned: pages are PW_PAGE_BYTES apart, arena allocations 16-byte multiples)
+      uint8_t* const gb = A.text + P;
+      w->ostart[lane] = my_off;
+      if (lane == 0) w->ostart[kWave] = B;
+      if (linelen > 0) {
+        const uint32_t c1 = (my_off + (uint32_t)linelen + 15) >> 4;
+        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) w->cmap[ci] = (uint8_t)lane;
+        if (my_off == 0) w->cmap[0] = (uint8_t)lane;
+      }
+      wave_sync();
       // gather: each lane assembles 16 output bytes from (at most a few) line buffers with
       // aligned dword reads + byte-align shifts, then one 16-byte store
-      for (uint32_t c = (uint32_t)lane * 16; c < end; c += kWave * 16) {
-        const int cb = (int)c - (int)shift;  // output byte at chunk position 0 (< 0 in chunk 0)
-        uint32_t b = cb < 0 ? 0u : (uint32_t)cb;
-        const uint32_t be = (c + 16 - shift < B) ? c + 16 - shift : B;
+      for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {
+        uint32_t b = cc;
+        const uint32_t be = (cc + 16 < B) ? cc + 16 : B;
         int oi;
-        if ((c >> 4) < (uint32_t)kMap) {
-          oi = w->cmap[c >> 4];
-        } else {  // past the map (rounds with long lines): last line starting at or before b
+        if ((cc >> 4) < (uint32_t)kMap) {
+          oi = w->cmap[cc >> 4];
+        } else {  // past the map (pages with long lines): last line starting at or before b
           oi = 0;
 #pragma unroll
           for (int step = 32; step >= 1; step >>= 1)
@@ -1005,106 +1355,54 @@ __device__ __forceinline__ void process_record(const pw_report_args& A, const Fi
           const uint32_t s0 = w->ostart[oi], s1 = w->ostart[oi + 1];
           const uint32_t pe = s1 < be ? s1 : be;
           if (pe > b) {
-            int x = cb - (int)s0;          // line offset at chunk position 0, >= -15
+            int x = (int)cc - (int)s0;     // line offset at block position 0, >= -15
             if (x > kLine) x = kLine;      // long line: garbage here, fixup_kernel rewrites it
-            const int a = (int)w->olane[oi] * kLine + x;
+            const int a = oi * kLStride + x;
             const LDS uint32_t* src = reinterpret_cast<const LDS uint32_t*>(w->line + (a & ~3));
             const uint32_t sh = (uint32_t)a & 3u;
-            uint32_t d[5];
+            uint32_t dd[5];
 #pragma unroll
-            for (int i = 0; i < 5; i++) d[i] = src[i];
-            const uint32_t qlo = (uint32_t)((int)b - cb), qhi = (uint32_t)((int)pe - cb);
+            for (int i = 0; i < 5; i++) dd[i] = src[i];
+            const uint32_t qlo = b - cc, qhi = pe - cc;
             const uint32_t m16 = ((1u << qhi) - 1u) & ~((1u << qlo) - 1u);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
               const uint32_t nib = (m16 >> (4 * i)) & 15u;
               const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
-              v[i] |= __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) & bm;
+              v[i] |= __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh) & bm;
             }
           }
           b = pe > b ? pe : b;
           oi++;
         }
-        if (c >= shift && c + 16 <= end) {
-          v4u vv;
-          vv.x = v[0];
-          vv.y = v[1];
-          vv.z = v[2];
-          vv.w = v[3];
-          *reinterpret_cast<v4u*>(gb + c) = vv;
-        } else {
-          const uint32_t lo = c < shift ? shift : c, hi = (c + 16 < end) ? c + 16 : end;
-          for (uint32_t bb = lo; bb < hi; bb++) gb[bb] = (uint8_t)(v[(bb - c) >> 2] >> (8 * ((bb - c) & 3)));
-        }
-      }
-      wave_sync();
-    }
-
-    // ---- 8. carries
-    qc += (int)sq;
-    tc += (int)st;
-    lc += sl;
-    ev_idx += nev;
-    sb += nseg;
-  }
-
-  if (lane == 0) {
-    pw_aln_result res;
-    res.text_off = r.rev ? out_hi : slot_lo;
-    res.text_len = (uint32_t)(r.rev ? (slot_hi - out_hi) : (out_lo - slot_lo));
-    res.n_events = ev_idx;
-    res.err = fix_overflow ? 3 : PW_REC_OK;
-    res.err_a = res.err_b = res.err_c = 0;
-    if (me_last >= 0) {  // first failing event in OUTPUT order
-      res.err |= PW_REC_MODSEQ;
-      if (!r.rev) {
-        res.err_a = me_fa;
-        res.err_b = me_fb;
-        res.err_c = me_first;
-      } else {
-        res.err_a = me_la;
-        res.err_b = me_lb;
-        res.err_c = (int)ev_idx - 1 - me_last;
+        v4u vv;
+        vv.x = v[0];
+        vv.y = v[1];
+        vv.z = v[2];
+        vv.w = v[3];
+        *reinterpret_cast<v4u*>(gb + cc) = vv;  // (bytes past B are page slack)
       }
     }
-    A.results[ai] = res;
+    wave_sync();
   }
 }
 
-__device__ __forceinline__ void stage_tables(LDS Lds* sp, int lane) {
-  const v4u* src = reinterpret_cast<const v4u*>(&c_tables);
-  LDS v4u* dst = reinterpret_cast<LDS v4u*>(&sp->tab);
-  for (int i = lane; i < (int)(sizeof(Tables) / 16); i += kWave) dst[i] = src[i];
-}
-
-__global__ __launch_bounds__(kWave) void report_kernel(pw_report_args A, FixList F) {
-  __shared__ __attribute__((aligned(16))) Lds s;
-  LDS Lds* sp = (LDS Lds*)&s;
-  const int lane = threadIdx.x;
-  stage_tables(sp, lane);
+// ------------------------------------------------------------------ fixup_kernel
+// Lines longer than the LDS line buffer, one per thread, rewritten in place (their bytes were
+// reserved).  The record is read straight from global memory (no windows).
+__global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
+  __shared__ SmallTables tab;
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, 256);
   __syncthreads();
-  for (uint32_t ai = blockIdx.x; ai < A.n_alns; ai += gridDim.x) {
-    process_record(A, F, sp, ai, lane);
-    __syncthreads();
-  }
-}
-
-// Deferred work of report_kernel, one entry per thread: the op-walk target contexts and the
-// lines longer than the LDS line buffer, written in place (their bytes were reserved).  The
-// record is read straight from global memory (empty LDS windows).
-__global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, FixList F) {
-  __shared__ __attribute__((aligned(16))) Tables tab;
-  {
-    const v4u* src = reinterpret_cast<const v4u*>(&c_tables);
-    LDS v4u* dst = reinterpret_cast<LDS v4u*>((LDS Tables*)&tab);
-    for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += 256) dst[i] = src[i];
-  }
-  __syncthreads();
-  const uint32_t n = min(*F.count, F.cap);
+  const uint32_t n = min(W.ctr[1], W.fix_cap);
   const bool skip = A.skip_codan != 0;
+  if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const Fixup f = F.list[i];
-    const pw_aln_desc d = A.desc[f.ai];
+    const Fixup f = W.fix[i];
+    const Hot h = W.hot[f.s];
+    const Cold cd = W.cold[f.s];
+    const pw_aln_desc d = A.desc[cd.ai];
     const uint32_t qi = d.ref & 0x7FFFFFFFu;
     Rec r;
     r.ops = A.ops + d.op_begin;
@@ -1112,30 +1410,75 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, FixList F)
     r.R = A.qseq + A.qoff[qi];
     r.L = A.qlen[qi];
     r.NS = A.next_stop ? A.next_stop + A.qoff[qi] : nullptr;
-    r.tab = (const LDS Tables*)&tab;
-    r.qw = r.lw = (const LDS uint8_t*)&tab;  // windows empty: every read goes to global memory
-    r.opw = (const LDS uint32_t*)&tab;
-    r.qlo = -(1 << 30);
-    r.l_lo = 0;
-    r.l_n = 0;
+    r.tab = tp;
+    r.qw = nullptr;
+    r.qlo = 0;
+    r.qn = 0;
+    r.opw = nullptr;
     r.op_lo = 0;
     r.op_n = 0;
+    r.lit0 = r.lit1 = 0;
+    r.ls0 = 0;
+    r.ln = 0;
+    r.lw = nullptr;
+    r.l_lo = 0;
+    r.l_n = 0;
     r.offset = d.offset;
     r.T = d.t_len;
     r.n_ops = d.n_ops;
     r.rev = (d.ref & PW_REF_REVERSE) != 0;
-    const uint32_t wd = r.ops[f.j];
+    const uint32_t wd = r.ops[cd.j];
+    EvIn in;
+    in.typ = wd >> 30;
+    in.n = event_len(r, cd.j, wd);
+    in.qp = h.qp;
+    in.tloc = h.tloc;
+    in.ls = h.ls;
+    in.tmode = ((h.fn >> 28) & 1u) ? 0 : 2;
+    in.ll = (int)((h.fn >> 23) & 7u);
+    in.rl = (int)((h.fn >> 20) & 7u);
+    in.tx = nullptr;
+    in.j = cd.j;
+    in.wd = wd;
+    in.qs = cd.qs;
+    in.ts = cd.ts;
     GlobalSink g;
+    g.p = A.text + f.dst;
     g.pos = 0;
-    if (f.pos == kFixLine) {
-      g.p = A.text + f.dst;
-      int rel, tpos;
-      emit_event(g, r, f.j, wd, f.qs, f.ts, f.ls, skip, false, rel, tpos);
-    } else {
-      g.p = A.text + f.dst + f.pos;
-      emit_tctx(g, r, wd >> 30, event_len(r, f.j, wd), f.j, wd, f.qs, f.ts, f.ls, false);
+    int rel;
+    emit_event(g, r, in, skip, rel);
+  }
+}
+
+// ------------------------------------------------------------------ finalize_kernel
+__global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W) {
+  const uint32_t ai = blockIdx.x * 256 + threadIdx.x;
+  if (ai >= A.n_alns) return;
+  pw_aln_result r = A.results[ai];
+  if (W.ctr[2]) {
+    r.err = 3;
+  } else if (r.err == PW_REC_OK) {
+    if (r.n_events) {  // bytes of the lines, across the pages they span
+      uint64_t len;
+      if (r.page_first == r.page_last) {
+        len = r.text_end - r.text_off;
+      } else {
+        const pw_page p0 = A.pages[r.page_first];
+        len = p0.off + p0.len - r.text_off;
+        for (uint32_t c = r.page_first + 1; c < r.page_last; c++) len += A.pages[c].len;
+        len += r.text_end - A.pages[r.page_last].off;
+      }
+      r.text_len = (uint32_t)len;
+    }
+    const uint64_t key = W.rec_mod[ai];
+    if (key != ~0ull) {
+      r.err = PW_REC_MODSEQ;
+      r.err_c = (int32_t)(key >> 40);
+      r.err_a = (int32_t)((key >> 20) & 0xFFFFFu);
+      r.err_b = (int32_t)(key & 0xFFFFFu);
     }
   }
+  A.results[ai] = r;
 }
 
 // ------------------------------------------------------------------ next-stop table
@@ -1143,15 +1486,13 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, FixList F)
 // three consecutive positions (one per frame); per frame a suffix-min scan over the tile.
 __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, const uint64_t* qoff,
                                                          const int32_t* qlen, uint32_t nq, int32_t* ns) {
-  __shared__ Tables tab;
+  __shared__ SmallTables tab;
   __shared__ int32_t sm[3][256];
   __shared__ int32_t carry[3];
   const int t = threadIdx.x;
-  {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&c_tables);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&tab);
-    for (int i = t; i < (int)(sizeof(Tables) / 4); i += 256) dst[i] = src[i];
-  }
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, t, 256);
+  __syncthreads();
   for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
     const uint8_t* R = qseq + qoff[qi];
     int32_t* out = ns + qoff[qi];
@@ -1166,8 +1507,7 @@ __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, co
         const int p = base + 3 * t + f;
         int32_t v = kNoStop;
         if (p + 2 < L) {
-          uint8_t c = tab.codon[(tab.nt[R[p]] << 8) | (tab.nt[R[p + 1]] << 4) | tab.nt[R[p + 2]]];
-          if (c == '.') v = p;
+          if (translate(tp, R[p], R[p + 1], R[p + 2]) == '.') v = p;
         }
         sm[f][t] = v;
       }
@@ -1196,8 +1536,12 @@ __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, co
 
 }  // namespace pw
 
-extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max) {
-  return 64u + sizeof(pw::Fixup) * (n_events_max ? n_events_max : 1u);
+extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_alns) {
+  return pw::work_layout(nullptr, n_events_max, n_alns, nullptr);
+}
+extern "C" uint64_t pw_report_page_count(uint64_t n_ev_slots) { return (n_ev_slots + PW_PAGE_EVENTS - 1) / PW_PAGE_EVENTS; }
+extern "C" uint64_t pw_report_text_bytes(uint64_t n_ev_slots, uint64_t text_bound) {
+  return pw_report_page_count(n_ev_slots) * PW_PAGE_BYTES + pw::align_up(text_bound, 16) + 16;
 }
 
 extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
@@ -1205,25 +1549,33 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
       (!args->text && args->text_total))
     return PW_E_ARG;
   if (!args->skip_codan && !args->next_stop) return PW_E_ARG;
-  if (!args->workspace || args->workspace_bytes < pw_report_workspace_bytes(1) ||
-      ((uintptr_t)args->workspace & 15))
-    return PW_E_ARG;
   if (args->n_alns == 0) return PW_OK;
+  const uint64_t need = pw_report_workspace_bytes(args->n_ev_slots, args->n_alns);
+  if (!args->workspace || args->workspace_bytes < need || ((uintptr_t)args->workspace & 255)) return PW_E_ARG;
+  // per-lane windows are 16-byte loads, literal words 4-byte loads, pages 16-byte stores
+  if (((uintptr_t)args->qseq & 15) || ((uintptr_t)args->lits & 3) || ((uintptr_t)args->text & 15)) return PW_E_ARG;
+  if (args->n_ev_slots && (!args->pages || args->text_total < pw_report_page_count(args->n_ev_slots) * PW_PAGE_BYTES))
+    return PW_E_ARG;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
   }
-  pw::FixList F;
-  F.count = static_cast<uint32_t*>(args->workspace);
-  F.list = reinterpret_cast<pw::Fixup*>(static_cast<uint8_t*>(args->workspace) + 64);
-  const uint64_t cap = (args->workspace_bytes - 64) / sizeof(pw::Fixup);
-  F.cap = cap > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cap;
-  if (hipMemsetAsync(F.count, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return PW_E_HIP;
-  const uint32_t max_blocks = (uint32_t)ncu * 16u;
-  const uint32_t grid = args->n_alns < max_blocks ? args->n_alns : max_blocks;
-  hipLaunchKernelGGL(pw::report_kernel, dim3(grid), dim3(pw::kWave), 0, (hipStream_t)stream, *args, F);
-  hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu * 2u), dim3(256), 0, (hipStream_t)stream, *args, F);
+  pw::Work W;
+  pw::work_layout(static_cast<uint8_t*>(args->workspace), args->n_ev_slots, args->n_alns, &W);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;  // counters
+  const uint32_t nwave = pw::kWaves;
+  uint64_t ig = (args->n_alns + nwave - 1) / nwave;
+  if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;
+  hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+  if (W.n_chunks) {
+    uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
+    if (rg > (uint64_t)ncu * 3u) rg = (uint64_t)ncu * 3u;
+    hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);
+  }
+  hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 

@@ -149,15 +149,13 @@ def test_batch_api_on_torch_stream(built, tmp_path):
     dev = pw.stage_batch(b, "cuda:0")
     pw.run_report(b, dev, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    text = dev["text"].cpu().numpy()
     res = dev["results"].cpu().numpy()
     outp = str(tmp_path / "batch.txt")
-    rc = b.write_report(text, res, outp)
+    rc = b.write_report_from(dev, outp)
     assert rc == 0
     _, want, _ = run([ORACLE, "-r", fa, paf])
     assert open(outp, "rb").read() == want
-    r = res.view(np.uint8).reshape(-1, 32)
-    n_events = r[:, 12:16].copy().view(np.uint32).sum()
+    n_events = pw.results_array(res)["n_events"][: b.view.n_alns].sum()
     assert n_events == want.count(b"\n") - want.count(b">")
 
 
@@ -230,7 +228,7 @@ def test_sharded_run_on_gpu(built, tmp_path, world):
         pw.run_report(b, dev, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         ip = str(tmp_path / f"s{r}.pwi")
-        assert b.write_items(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), ip) == 0
+        assert b.write_items_from(dev, ip) == 0
         got.append((shard.read_items(ip), gmap))
     out, err, rc = shard.merge_items(got)
     assert (rc, out, err) == run([ORACLE, "-r", fa, dup])
