@@ -98,6 +98,8 @@ def main():
     errs = int((res["err"] != 0).sum())
     text_bytes = int(res["text_len"].astype(np.int64).sum())
     assert errs == 0, f"{errs} records reported errors"
+    ctr = dev["work"][:16].cpu().numpy().view(np.uint32)
+    log(f"[rank {rank}] {n_events} events, {text_bytes} text bytes; long lines {int(ctr[1])}")
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
@@ -151,7 +153,7 @@ def main():
                        "parallelism": f"shard-by-target x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "pw::report_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "pw_report_events (index+tctx+render+fixup+finalize)", "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

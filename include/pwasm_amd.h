@@ -161,8 +161,34 @@ uint64_t pw_msa_slots(const int32_t* row_len_host, uint32_t n_rows, int64_t* slo
 
 /* Replaces GSeqAlign::buildMSA -> GASeq::toMSA -> GAlnColumn::addNuc/addGap and
  * GAlnColumn::bestChar (GapAssem.cpp:551-591, 1048-1069, 1088-1106; GapAssem.h:295-337).
- * minmax: INT_MAX / -1 sentinels when nothing is set. */
+ * minmax: INT_MAX / -1 sentinels when nothing is set.  = pw_msa_count + pw_msa_call. */
 int pw_msa_columns(const pw_msa_args* args, void* stream);
+
+/* The two halves of pw_msa_columns, for rows sharded over GPUs: pw_msa_count
+ * fills counts[n_cols][6] and minmax[0..2] from this shard's rows (buildMSA's toMSA/addNuc/
+ * addGap scatter); after the shards' counts are summed (all-reduce) and minmax[0] / [1]
+ * reduced with min / max, pw_msa_call writes bestChar for every column and minmax[3]. */
+int pw_msa_count(const pw_msa_args* args, void* stream);
+int pw_msa_call(const pw_msa_args* args, void* stream);
+
+/* GSeqAlign::refineMSA after buildMSA (GapAssem.cpp:1143-1181): the consensus string over
+ * [mincol, maxcol] ('-' -> '*'; with remove_gaps = MSAColumns::removeConsGaps the gap columns
+ * are dropped) and, with remove_gaps, every row's removeColumn / removeBase edits and
+ * removeClipGaps (GapAssem.cpp:755-779, 122-131, 522-549).  Needs the scratch of the
+ * pw_msa_count call that produced args->counts; rows must have ofs >= 0 when remove_gaps. */
+typedef struct pw_msa_refine_args {
+  int32_t* gap_prefix;        /* [n_cols] scratch: consensus-gap columns in [mincol, c] */
+  int32_t* tile_gaps;         /* [pw_msa_refine_tiles(n_cols)] scratch */
+  uint8_t* cons_out;          /* [n_cols] the consensus (GSeqAlign::consensus) */
+  int32_t* cons_len;          /* [1] its length */
+  const int32_t* row_offset;  /* [n_rows] GASeq::offset (remove_gaps) */
+  int16_t* ofs_out;           /* [bases] GASeq::ofs after refineMSA, same indexing as ofs */
+  int32_t* offset_out;        /* [n_rows] GASeq::offset after refineMSA */
+  int64_t* numgaps_out;       /* [n_rows] in: GASeq::numgaps; out: after refineMSA */
+  uint32_t remove_gaps;
+} pw_msa_refine_args;
+uint64_t pw_msa_refine_tiles(int32_t n_cols);
+int pw_msa_refine(const pw_msa_args* args, const pw_msa_refine_args* refine, void* stream);
 
 /* ---------------------------------------------------------------- host pre-pass + CLI */
 

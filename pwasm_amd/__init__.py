@@ -92,6 +92,12 @@ class MsaArgs(ctypes.Structure):
                 ("n_slots", ctypes.c_uint64), ("n_rows", ctypes.c_uint32), ("n_cols", ctypes.c_int32)]
 
 
+class MsaRefineArgs(ctypes.Structure):
+    _fields_ = [("gap_prefix", ctypes.c_void_p), ("tile_gaps", ctypes.c_void_p), ("cons_out", ctypes.c_void_p),
+                ("cons_len", ctypes.c_void_p), ("row_offset", ctypes.c_void_p), ("ofs_out", ctypes.c_void_p),
+                ("offset_out", ctypes.c_void_p), ("numgaps_out", ctypes.c_void_p), ("remove_gaps", ctypes.c_uint32)]
+
+
 # every function declared in include/pwasm_amd.h (tests check the export table against it)
 _SIGS = {
     "pw_report_events": (ctypes.c_int, [ctypes.POINTER(ReportArgs), ctypes.c_void_p]),
@@ -99,6 +105,10 @@ _SIGS = {
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "pw_msa_slots": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     "pw_msa_columns": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
+    "pw_msa_count": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
+    "pw_msa_call": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
+    "pw_msa_refine_tiles": (ctypes.c_uint64, [ctypes.c_int32]),
+    "pw_msa_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
     "pw_pack_cs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),
                                   ctypes.POINTER(ctypes.c_int32)]),

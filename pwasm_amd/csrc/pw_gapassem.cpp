@@ -4,7 +4,8 @@
 //   "Warning: sequence %s (length %d) was trimmed too badly ..."  GapAssem.cpp:1096-1101
 //   "MSAColumns op[]: bad index %d (size=%d)"  exit 1            GapAssem.h:366-370
 //   "WARNING: 0 coverage column ..." + row ids, exit 5           GapAssem.cpp:1121-1131
-// removeConsGaps=true (GapAssem.cpp:1152-1158) is not on the GPU yet and is refused.
+// removeConsGaps=true (GapAssem.cpp:1152-1158, 1174-1175) runs on the GPU too (pw_msa_refine);
+// it needs gap values >= 0.
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdio.h>
@@ -83,10 +84,12 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
     }
   }
   fclose(f);
-  if (remove_gaps) {
-    fprintf(stderr, "removeConsGaps is not implemented on the HIP path yet\n");
-    return 2;
-  }
+  if (remove_gaps)
+    for (int16_t g : ofs)
+      if (g < 0) {
+        fprintf(stderr, "removeConsGaps with negative gap values is not supported on the HIP path\n");
+        return 2;
+      }
   // GSeqAlign bookkeeping (GapAssem.cpp:605-641, 694-716)
   int64_t minoffset = INT64_MAX, maxend = INT64_MIN;
   for (const Row& w : rows) {
@@ -120,11 +123,16 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
   Dev<uint8_t> d_seq, d_cons;
   Dev<int16_t> d_ofs;
   Dev<uint64_t> d_roff;
-  Dev<int32_t> d_len, d_col0, d_cl, d_cr, d_scr, d_cnt, d_mm;
-  Dev<int64_t> d_slot;
+  Dev<int32_t> d_len, d_col0, d_cl, d_cr, d_scr, d_cnt, d_mm, d_gp, d_tg, d_clen, d_roffs, d_offo;
+  Dev<int64_t> d_slot, d_ngo;
+  Dev<uint8_t> d_cout;
+  Dev<int16_t> d_ofso;
+  const uint64_t ntg = pw_msa_refine_tiles(ncols);
   bool ok = d_seq.alloc(seq.size()) && d_ofs.alloc(ofs.size()) && d_roff.alloc(nrows) && d_len.alloc(nrows) &&
             d_col0.alloc(nrows) && d_cl.alloc(nrows) && d_cr.alloc(nrows) && d_slot.alloc(nrows + 1) &&
-            d_scr.alloc(2 * nslots) && d_cnt.alloc((size_t)ncols * 6) && d_cons.alloc((size_t)ncols) && d_mm.alloc(4);
+            d_scr.alloc(2 * nslots) && d_cnt.alloc((size_t)ncols * 6) && d_cons.alloc((size_t)ncols) && d_mm.alloc(4) &&
+            d_gp.alloc((size_t)ncols) && d_tg.alloc(ntg) && d_clen.alloc(1) && d_cout.alloc((size_t)ncols) &&
+            (!remove_gaps || (d_roffs.alloc(nrows) && d_offo.alloc(nrows) && d_ngo.alloc(nrows) && d_ofso.alloc(ofs.size())));
   if (!ok) {
     fprintf(stderr, "gapassem: device allocation failed\n");
     return 2;
@@ -167,7 +175,6 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
     fprintf(stderr, "gapassem: device error\n");
     return 2;
   }
-  (void)hipStreamDestroy(st);
   // buildMSA messages in row order, stopping at the first out-of-range access
   const uint32_t bad_row = mm[2] == INT_MAX ? nrows : (uint32_t)mm[2];
   for (uint32_t r = 0; r < nrows && r <= bad_row; r++) {
@@ -205,19 +212,69 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
     for (uint32_t r = 0; r < nrows; r++) fprintf(stderr, "row%u\n", r);
     return 5;
   }
+  // refineMSA's consensus loop and (removeConsGaps) row edits on the GPU
   std::string consensus;
-  if (mincol != INT_MAX)
-    for (int c = mincol; c <= maxcol; c++) consensus.push_back(cons[c] == '-' ? '*' : (char)cons[c]);
+  std::vector<int32_t> off_out(nrows);
+  std::vector<int64_t> ng_out(nrows);
+  int32_t n_removed = 0;
+  if (mincol != INT_MAX) {
+    std::vector<int32_t> roffs(nrows);
+    for (uint32_t r = 0; r < nrows; r++) {
+      roffs[r] = rows[r].offset;
+      ng_out[r] = rows[r].numgaps;
+    }
+    pw_msa_refine_args ra;
+    memset(&ra, 0, sizeof ra);
+    ra.gap_prefix = d_gp.p;
+    ra.tile_gaps = d_tg.p;
+    ra.cons_out = d_cout.p;
+    ra.cons_len = d_clen.p;
+    ra.remove_gaps = remove_gaps ? 1u : 0u;
+    if (remove_gaps) {
+      (void)hipMemcpyAsync(d_roffs.p, roffs.data(), nrows * 4, hipMemcpyHostToDevice, st);
+      (void)hipMemcpyAsync(d_ngo.p, ng_out.data(), nrows * 8, hipMemcpyHostToDevice, st);
+      ra.row_offset = d_roffs.p;
+      ra.ofs_out = d_ofso.p;
+      ra.offset_out = d_offo.p;
+      ra.numgaps_out = d_ngo.p;
+    }
+    int32_t clen = 0;
+    if (pw_msa_refine(&a, &ra, st) != PW_OK ||
+        hipMemcpyAsync(&clen, d_clen.p, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      fprintf(stderr, "gapassem: refine failed\n");
+      return 2;
+    }
+    consensus.resize((size_t)clen);
+    (void)hipMemcpyAsync(&consensus[0], d_cout.p, (size_t)clen, hipMemcpyDeviceToHost, st);
+    if (remove_gaps) {
+      (void)hipMemcpyAsync(off_out.data(), d_offo.p, nrows * 4, hipMemcpyDeviceToHost, st);
+      (void)hipMemcpyAsync(ng_out.data(), d_ngo.p, nrows * 8, hipMemcpyDeviceToHost, st);
+      (void)hipMemcpyAsync(ofs.data(), d_ofso.p, ofs.size() * 2, hipMemcpyDeviceToHost, st);
+      n_removed = (int32_t)(maxcol - mincol + 1) - clen;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      fprintf(stderr, "gapassem: device error\n");
+      return 2;
+    }
+  }
+  (void)hipStreamDestroy(st);
+  if (!remove_gaps || mincol == INT_MAX)
+    for (uint32_t r = 0; r < nrows; r++) {
+      off_out[r] = rows[r].offset;
+      ng_out[r] = rows[r].numgaps;
+    }
   FILE* o = fopen(out_path, "wb");
   if (!o) return 2;
-  int32_t h[6] = {ncols, (int32_t)minoffset, mincol == INT_MAX ? -1 : mincol, maxcol, (int32_t)consensus.size(), 0};
+  int32_t h[6] = {ncols, (int32_t)minoffset, mincol == INT_MAX ? -1 : mincol, maxcol, (int32_t)consensus.size(),
+                  n_removed};
   fwrite("PWC1", 1, 4, o);
   fwrite(h, sizeof h, 1, o);
   fwrite(consensus.data(), 1, consensus.size(), o);
   fwrite(counts.data(), 4, counts.size(), o);
   fwrite(&nrows, 4, 1, o);
   for (uint32_t r = 0; r < nrows; r++) {
-    int32_t rh[2] = {rows[r].offset, (int32_t)rows[r].numgaps};
+    int32_t rh[2] = {off_out[r], (int32_t)ng_out[r]};
     fwrite(rh, sizeof rh, 1, o);
     fwrite(ofs.data() + rows[r].base, 2, (size_t)rows[r].seqlen, o);
   }

@@ -15,9 +15,29 @@
 //                      the tile (binary search on the checkpoints), re-derive columns with a
 //                      wave scan and add into LDS; then the tile writes counts + bestChar
 //                      coalesced and folds mincol / maxcol.
-//   K4 zero_scan:      first zero-coverage column in [mincol, maxcol] (ErrZeroCov, :1121-1131).
+//                      (pw_msa_count stops here: with rows sharded over GPUs the partial
+//                      counts are summed by an all-reduce before the call)
+//   K4 call_columns:   bestChar of every column (pw_msa_call)
+//   K5 zero_scan:      first zero-coverage column in [mincol, maxcol] (ErrZeroCov, :1121-1131).
 // Column-closed form of bestChar: max count wins, ties resolved A<C<G<T; a tie between only N
 // and '-' gives '-' (glibc qsort of 6 elements is a stable merge sort).
+//
+// refineMSA's consensus loop (GapAssem.cpp:1143-1162) and, with MSAColumns::removeConsGaps,
+// its row edits (removeColumn :755-779 -> GASeq::removeBase :122-131, then removeClipGaps
+// :522-549) in closed form (pw_msa_refine).  With G(c) = consensus-gap columns in
+// [mincol, c] (gap columns are removed in increasing order, each at column - cols_removed, so
+// the k-th removal hits exactly the layout column it was in before any removal), a row with
+// first column O and base columns col(i) ends with
+//   offset' = offset - G(O)                           (removeColumn's "offset--" branch)
+//   ofs'[0] = ofs[0] - (G(col(0)) - G(O))
+//   ofs'[i] = ofs[i] - (G(col(i)) - G(col(i-1)))      (removeBase of the first base at or
+//                                                      after the removed column)
+// for ofs >= 0 (the walk of :766-771 sees raw ofs values; negative input gaps are refused).
+//   K6 gap_tiles / K7 gap_scan: G per column (tile counts + in-tile scan) and the consensus
+//                      string ('-' -> '*', or gap columns dropped)
+//   K8 row_edit:       ofs' of every base (chunked like K3)
+//   K9 row_finish:     offset', numgaps', then removeClipGaps on ofs' (i <= clipL and
+//                      i >= seqlen - clipR)
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -172,13 +192,18 @@ __global__ __launch_bounds__(256) void tile_counts(const pw_msa_args A, const in
     if (my_max >= 0) atomicMax(&A.minmax[1], my_max);
   }
   __syncthreads();
-  for (int c = c0 + tid; c < c1; c += 256) {
+  // the tile's counters, coalesced: column-major in LDS -> [col][6] rows in memory
+  int32_t* dst = A.counts + (int64_t)c0 * 6;
+  for (int i = tid; i < (c1 - c0) * 6; i += 256) dst[i] = cnt[i % 6][i / 6];
+}
+
+// bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage
+__global__ __launch_bounds__(256) void call_columns(const pw_msa_args A) {
+  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < A.n_cols; c += (int64_t)gridDim.x * 256) {
     int v[6];
+    const int32_t* src = A.counts + c * 6;
 #pragma unroll
-    for (int q = 0; q < 6; q++) v[q] = cnt[q][c - c0];
-    int32_t* dst = A.counts + (int64_t)c * 6;
-#pragma unroll
-    for (int q = 0; q < 6; q++) dst[q] = v[q];
+    for (int q = 0; q < 6; q++) v[q] = src[q];
     const int layers = v[0] + v[1] + v[2] + v[3] + v[4] + v[5];
     uint8_t best = 0;
     if (layers > 0) {
@@ -202,6 +227,155 @@ __global__ __launch_bounds__(256) void zero_scan(const pw_msa_args A) {
     if (c >= 0 && c < A.n_cols && A.consensus[c] == 0) atomicMin(&A.minmax[3], c);
 }
 
+// ---------------------------------------------------------------- refineMSA (pw_msa_refine)
+__device__ __forceinline__ bool cons_gap(const pw_msa_args& A, int lo, int hi, int c) {
+  return c >= lo && c <= hi && A.consensus[c] == '-';
+}
+
+// K6: consensus-gap columns per 2048-column tile
+__global__ __launch_bounds__(256) void gap_tiles(const pw_msa_args A, pw_msa_refine_args R) {
+  __shared__ int part[4];
+  const int lo = A.minmax[0], hi = A.minmax[1];
+  const int c0 = blockIdx.x * kTileW;
+  int n = 0;
+  for (int c = c0 + threadIdx.x; c < c0 + kTileW && c < A.n_cols; c += 256) n += cons_gap(A, lo, hi, c) ? 1 : 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) R.tile_gaps[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// K7: G(c) (inclusive) for every column of the tile and the consensus string
+__global__ __launch_bounds__(256) void gap_scan(const pw_msa_args A, pw_msa_refine_args R) {
+  __shared__ int part[4];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lo = A.minmax[0], hi = A.minmax[1];
+  const int t = blockIdx.x;
+  // gap columns of the tiles before this one
+  int b = 0;
+  for (int i = tid; i < t; i += 256) b += R.tile_gaps[i];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) b += __shfl_xor(b, d, 64);
+  if (lane == 0) part[wv] = b;
+  __syncthreads();
+  if (tid == 0) base_s = part[0] + part[1] + part[2] + part[3];
+  __syncthreads();
+  // each thread owns 8 consecutive columns
+  const int c0 = t * kTileW + tid * 8;
+  uint32_t gm = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) gm |= cons_gap(A, lo, hi, c0 + q) && c0 + q < A.n_cols ? (1u << q) : 0u;
+  const int mine = __popc(gm);
+  int incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  __syncthreads();
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  int g = base_s + incl - mine;
+  for (int w = 0; w < wv; w++) g += part[w];
+  const bool rm = R.remove_gaps != 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const int c = c0 + q;
+    if (c >= A.n_cols) break;
+    const bool isg = (gm >> q) & 1u;
+    g += isg ? 1 : 0;
+    R.gap_prefix[c] = g;
+    if (c >= lo && c <= hi) {
+      const uint8_t ch = A.consensus[c];
+      if (!rm) R.cons_out[c - lo] = isg ? (uint8_t)'*' : ch;
+      else if (!isg) R.cons_out[c - lo - g] = ch;
+      if (c == hi) *R.cons_len = (hi - lo + 1) - (rm ? g : 0);
+    }
+  }
+}
+
+__device__ __forceinline__ int gx(const pw_msa_refine_args& R, int n_cols, int c) {
+  return c < 0 ? 0 : R.gap_prefix[c < n_cols ? c : n_cols - 1];
+}
+
+// K8: ofs' of every base, one wave per 256-base chunk (columns re-derived as in K3)
+__global__ __launch_bounds__(256) void row_edit(const pw_msa_args A, pw_msa_refine_args R, const int32_t* ckpt) {
+  const int64_t* chunk_base = A.slot_base;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (uint64_t c = wid; c < A.n_slots; c += (uint64_t)gridDim.x * 4) {
+    uint32_t lo = 0, hi = A.n_rows;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((uint64_t)chunk_base[mid] <= c) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t r = lo;
+    const int64_t k = (int64_t)c - chunk_base[r];
+    const int len = A.row_len[r];
+    const int64_t ib = k * kChunk;
+    if (ib >= len) continue;  // the row's end slot
+    const uint64_t roff = A.row_off[r];
+    int col = ckpt[c];
+    long long dsum = 0;
+#pragma unroll
+    for (int j = 0; j < kChunk / 64; j++) {
+      const int64_t i = ib + j * 64 + lane;
+      const bool ok = i < len;
+      const int g = ok ? A.ofs[roff + i] : 0;  // >= 0 (checked by the host)
+      const int adv = ok ? 1 + g : 0;
+      int incl = adv;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+      }
+      const int bcol = col + incl - 1;
+      if (ok) {
+        const int prev = i == 0 ? bcol - g : bcol - g - 1;  // O for the first base
+        const int dec = gx(R, A.n_cols, bcol) - gx(R, A.n_cols, prev);
+        R.ofs_out[roff + i] = (int16_t)(g - dec);
+        dsum += dec;
+      }
+      col += __shfl(incl, 63, 64);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) dsum += __shfl_xor(dsum, d, 64);
+    if (lane == 0 && dsum) atomicAdd((unsigned long long*)&R.numgaps_out[r], (unsigned long long)(-dsum));
+  }
+}
+
+// K9: per row (one wave): offset', then removeClipGaps on ofs'
+__global__ __launch_bounds__(64) void row_finish(const pw_msa_args A, pw_msa_refine_args R) {
+  const int lane = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
+    const int len = A.row_len[r];
+    const uint64_t roff = A.row_off[r];
+    const int cl = A.clip_l[r], cr = A.clip_r[r];
+    long long dl = 0, dr = 0;
+    for (int i = lane; i < len && i <= cl; i += 64) {
+      dl += R.ofs_out[roff + i];
+      R.ofs_out[roff + i] = 0;
+    }
+    const int r0 = (len - cr > cl + 1) ? len - cr : cl + 1;
+    for (int i = r0 + lane; i < len; i += 64) {
+      dr += R.ofs_out[roff + i];
+      R.ofs_out[roff + i] = 0;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      dl += __shfl_xor(dl, d, 64);
+      dr += __shfl_xor(dr, d, 64);
+    }
+    if (lane == 0) {
+      R.offset_out[r] = R.row_offset[r] - gx(R, A.n_cols, A.col0[r]) + (int32_t)dl;
+      R.numgaps_out[r] -= dl + dr;
+    }
+  }
+}
+
 }  // namespace pw
 
 extern "C" uint64_t pw_msa_slots(const int32_t* row_len_host, uint32_t n_rows, int64_t* slot_base_host) {
@@ -214,11 +388,14 @@ extern "C" uint64_t pw_msa_slots(const int32_t* row_len_host, uint32_t n_rows, i
   return (uint64_t)acc;
 }
 
-extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) {
-  if (!a || !a->seq || !a->ofs || !a->row_off || !a->row_len || !a->col0 || !a->clip_l || !a->clip_r ||
-      !a->slot_base || !a->scratch || !a->counts || !a->consensus || !a->minmax)
-    return PW_E_ARG;
-  if (a->n_rows == 0 || a->n_cols <= 0 || a->n_slots < a->n_rows) return PW_E_ARG;
+static bool msa_args_ok(const pw_msa_args* a) {
+  return a && a->seq && a->ofs && a->row_off && a->row_len && a->col0 && a->clip_l && a->clip_r && a->slot_base &&
+         a->scratch && a->counts && a->consensus && a->minmax && a->n_rows > 0 && a->n_cols > 0 &&
+         a->n_slots >= a->n_rows;
+}
+
+extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
+  if (!msa_args_ok(a)) return PW_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
@@ -230,6 +407,38 @@ extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) {
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, chunk_sum, ckpt);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kTileW - 1) / pw::kTileW);
   hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(256), 0, s, *a, ckpt);
+  return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+}
+
+extern "C" int pw_msa_call(const pw_msa_args* a, void* stream) {
+  if (!msa_args_ok(a)) return PW_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t nb = ((uint64_t)a->n_cols + 255) / 256;
+  hipLaunchKernelGGL(pw::call_columns, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, *a);
   hipLaunchKernelGGL(pw::zero_scan, dim3(256), dim3(256), 0, s, *a);
+  return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+}
+
+extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) {
+  const int rc = pw_msa_count(a, stream);
+  return rc != PW_OK ? rc : pw_msa_call(a, stream);
+}
+
+extern "C" uint64_t pw_msa_refine_tiles(int32_t n_cols) { return n_cols > 0 ? ((uint64_t)n_cols + pw::kTileW - 1) / pw::kTileW : 0; }
+
+extern "C" int pw_msa_refine(const pw_msa_args* a, const pw_msa_refine_args* r, void* stream) {
+  if (!msa_args_ok(a) || !r || !r->gap_prefix || !r->tile_gaps || !r->cons_out || !r->cons_len) return PW_E_ARG;
+  if (r->remove_gaps && (!r->row_offset || !r->ofs_out || !r->offset_out || !r->numgaps_out)) return PW_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(r->cons_len, 0, sizeof(int32_t), s) != hipSuccess) return PW_E_HIP;
+  const unsigned ntiles = (unsigned)pw_msa_refine_tiles(a->n_cols);
+  hipLaunchKernelGGL(pw::gap_tiles, dim3(ntiles), dim3(256), 0, s, *a, *r);
+  hipLaunchKernelGGL(pw::gap_scan, dim3(ntiles), dim3(256), 0, s, *a, *r);
+  if (r->remove_gaps) {
+    const int32_t* ckpt = a->scratch + a->n_slots;  // from pw_msa_count
+    const uint64_t nb = (a->n_slots + 3) / 4;
+    hipLaunchKernelGGL(pw::row_edit, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, *a, *r, ckpt);
+    hipLaunchKernelGGL(pw::row_finish, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, *r);
+  }
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }

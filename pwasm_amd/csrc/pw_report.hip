@@ -53,8 +53,8 @@ constexpr int kWave = 64;
 constexpr int kWaves = 4;       // wavefronts per workgroup (independent; they share the tables)
 constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
 constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
-constexpr int kQWin = 64;       // render_kernel: forward-query window per lane (bytes)
-constexpr int kQStride = 72;    // ... its LDS stride (18 dwords: conflict-free 8-byte stores)
+constexpr int kQWin = 48;       // render_kernel: forward-query window per lane (bytes)
+constexpr int kQStride = 48;    // ... its LDS stride
 constexpr int kLine = 96;       // render_kernel: per-lane report-line buffer (bytes)
 constexpr int kLStride = 100;   // ... its LDS stride (25 dwords: per-lane byte stores conflict-free)
 constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
@@ -64,6 +64,9 @@ constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, f
 constexpr uint32_t kNBig = (1u << 20) - 1;  // evtbases length field saturates here
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
+#ifndef PW_RENDER_OCC
+#define PW_RENDER_OCC 3
+#endif
 #ifndef PW_ABL
 #define PW_ABL 0
 #endif
@@ -92,10 +95,9 @@ __device__ __forceinline__ uint32_t hot_fn(uint32_t typ, bool rev, bool fast, bo
          (last ? 1u << 26 : 0u) | (uint32_t)(ll & 7) << 23 | (uint32_t)(rl & 7) << 20 | (n < kNBig ? n : kNBig);
 }
 
-// Byte tables read per event (LDS copy per workgroup).  The 4096-entry IUPAC codon table is
-// only needed off {A,C,G,T} and is read from c_tables.
+// Byte tables read per event (LDS copy per workgroup).  The IUPAC code / 4096-entry codon
+// tables are only needed off {A,C,G,T} and are read from c_tables.
 struct SmallTables {
-  uint8_t nt[256];
   uint8_t comp[256];
   uint8_t codon64[64];
   uint8_t status[8][12];
@@ -144,10 +146,12 @@ struct Rec {
   bool rev;
 };
 
+// Query byte x of the forward query, 0 outside [0, L) (the NUL / missing bytes).  The LDS
+// window holds zeros where it extends past the query, so a window hit needs no bounds check.
 __device__ __forceinline__ uint8_t Rc(const Rec& r, int x) {
-  if ((unsigned)x >= (unsigned)r.L) return 0;
   const unsigned o = (unsigned)(x - r.qlo);
-  return o < (unsigned)r.qn ? r.qw[o] : r.R[x];
+  if (o < (unsigned)r.qn) return r.qw[o];
+  return (unsigned)x < (unsigned)r.L ? r.R[x] : (uint8_t)0;
 }
 __device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
   const uint32_t o = i - r.ls0;
@@ -174,10 +178,14 @@ __device__ __forceinline__ bool is_acgt(uint32_t c) {
   // letters 0x40-0x7F whose low 5 bits are 1 (A), 3 (C), 7 (G) or 20 (T)
   return (c & 0xC0u) == 0x40u && ((0x0010008Au >> (c & 0x1Fu)) & 1u);
 }
+// (off {A,C,G,T}: rare, kept out of line so its table reads do not hold registers in the callers)
+__device__ __noinline__ uint8_t translate_iupac(uint32_t a, uint32_t b, uint32_t c) {
+  return c_tables.codon[(c_tables.nt[a] << 8) | (c_tables.nt[b] << 4) | c_tables.nt[c]];
+}
 __device__ __forceinline__ uint8_t translate(const LDS SmallTables* t, uint8_t a, uint8_t b, uint8_t c) {
   if (is_acgt(a) && is_acgt(b) && is_acgt(c))
     return t->codon64[((a >> 1) & 3u) << 4 | ((b >> 1) & 3u) << 2 | ((c >> 1) & 3u)];
-  return c_tables.codon[(t->nt[a] << 8) | (t->nt[b] << 4) | t->nt[c]];
+  return translate_iupac(a, b, c);
 }
 
 __device__ __forceinline__ uint32_t op_tadv(uint32_t w) {
@@ -215,9 +223,11 @@ struct EvIn {
   int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
   int ll, rl;
   const uint8_t* tx;  // length byte + field (tmode 1)
+  int ns_pre;         // next_stop entry the indel scan needs, loaded ahead (kNsNone: not loaded)
   uint32_t j, wd;
   int qs, ts;
 };
+constexpr int kNsNone = INT_MIN;
 
 // evtbases[i] in final orientation, upper case (pafreport.cpp:563,594-596,612-614,637,895)
 __device__ __forceinline__ uint8_t ev_base(const Rec& r, const Event& e, int i) {
@@ -437,7 +447,7 @@ __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, 
 // explicitly; past that, modseq codons are query codons and the first stop is one lookup in the
 // next-stop table.
 template <class S>
-__device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e) {
+__device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e, int ns_pre) {
   const int a = e.rloc - e.r_trloc;
   const int x = (e.type == PW_OP_INS) ? e.n : 0;
   const int dl = (e.type == PW_OP_DEL) ? e.n : 0;
@@ -491,7 +501,7 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e)
     } else if (nvalid == 5 && 15 + 2 < M && r.NS) {
       const int k0 = sfx + (15 - a - x);
       if (k0 >= 0 && k0 < r.L) {
-        const int st = r.NS[k0];
+        const int st = ns_pre != kNsNone ? ns_pre : r.NS[k0];
         if (st != kNoStop) stop_i = st - sfx + a + x;
       }
     }
@@ -696,7 +706,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       }
       if (!any) wr_lit(k, "synonymous");
     } else {
-      indel_impact(k, r, e);
+      indel_impact(k, r, e, in.ns_pre);
     }
   }
   k.put('\n');
@@ -708,6 +718,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
 //   ctr      u32 [1] long-line count, [2] overflow flags; u64 at byte 16: arena bytes used
 //   rec_mod  per record: modseq error key (first failing line in output order)
 //   hot/cold per event slot (Hot, Cold); tx: pre-rendered target contexts
+//   sflag    per slot: 1 = tctx_kernel renders its target context (zeroed per pass)
 //   fix      long-line list
 struct Fixup {
   uint32_t s, pad;
@@ -721,6 +732,7 @@ struct Work {
   Hot* hot;
   Cold* cold;
   uint8_t* tx;
+  uint8_t* sflag;
   Fixup* fix;
   uint32_t fix_cap;
   uint64_t n_slots, n_chunks;
@@ -742,6 +754,8 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
   o = align_up(o + sizeof(Cold) * ns, 256);
   const uint64_t o_tx = o;
   o = align_up(o + (uint64_t)kTx * ns, 256);
+  const uint64_t o_sflag = o;
+  o = align_up(o + ns, 256);
   const uint64_t o_fix = o;
   o = align_up(o + sizeof(Fixup) * (n_slots ? n_slots : 1), 256);
   if (w && base) {
@@ -751,6 +765,7 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->hot = reinterpret_cast<Hot*>(base + o_hot);
     w->cold = reinterpret_cast<Cold*>(base + o_cold);
     w->tx = base + o_tx;
+    w->sflag = base + o_sflag;
     w->fix = reinterpret_cast<Fixup*>(base + o_fix);
     w->fix_cap = n_slots > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(n_slots ? n_slots : 1);
     w->n_slots = n_slots;
@@ -764,7 +779,6 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
   const uint8_t* s = reinterpret_cast<const uint8_t*>(&c_tables);
   LDS uint8_t* d = reinterpret_cast<LDS uint8_t*>(dst);
   for (int i = tid; i < 256; i += nthreads) {
-    d[offsetof(SmallTables, nt) + i] = s[offsetof(Tables, nt) + i];
     d[offsetof(SmallTables, comp) + i] = s[offsetof(Tables, comp) + i];
   }
   for (int i = tid; i < 64; i += nthreads) d[offsetof(SmallTables, codon64) + i] = s[offsetof(Tables, codon64) + i];
@@ -772,16 +786,12 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
 }
 
 // ------------------------------------------------------------------ index_kernel
-constexpr int kTxStride = 48;              // index_kernel: per-lane target-context buffer
 constexpr int kOpWin = kSegOps + 2 * kOpHalo;
 struct IndexWave {
   uint32_t opw[kOpWin];            // op words of the segment + halo
   int32_t ots[kOpWin];             // their target / query / literal starts
   int32_t oqs[kOpWin];
   uint32_t ols[kOpWin];
-  int32_t xoff[kWave];             // slow contexts: first item of each lane's context
-  uint8_t tx[kWave * kTxStride];   // per-lane target-context field (length byte + bytes; [40] = walk)
-  uint8_t junk[kWave];
 };
 
 __device__ __forceinline__ int ndigits(uint32_t v) {
@@ -804,7 +814,6 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
   const uint32_t nmax = (uint32_t)(ev_next - evb);
   const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
-  LDS uint8_t* my_tx = w->tx + lane * kTxStride;
 
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
@@ -964,129 +973,8 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
         }
       }
       // ---- target contexts that are not a plain query copy (another event within 5 bases,
-      // an S run, a long insertion), all of this half-segment at once: every byte of every such
-      // context is one item, a lane resolves one item per round by a binary search over the op
-      // target starts in LDS (tseq is never materialised, pafreport.cpp:543,575,588)
-      if (__ballot(slow) == 0ull) continue;
-      const bool abbr = g.cl > 10 + kMaxEv;
-      const int ndig = abbr ? ndigits((uint32_t)(g.cl - 10)) : 0;
-      const uint32_t npos = slow ? (uint32_t)(abbr ? 10 : g.cl) : 0u;
-      const uint32_t incl = wave_incl_scan(npos, lane);
-      const uint32_t nitems = bcast(incl, kWave - 1);
-      w->xoff[lane] = (int32_t)(incl - npos);
-      if (slow) my_tx[40] = 0;
-      const int xtcs = g.tcs, xtce = g.tce;
-      wave_sync();
-      for (uint32_t i0 = 0; i0 < nitems; i0 += kWave) {
-        // (the shuffles run with every lane active: a shuffle from an inactive lane reads 0)
-        const bool active = i0 + (uint32_t)lane < nitems;
-        const int item = active ? (int)(i0 + (uint32_t)lane) : (int)nitems - 1;
-        int o = 0;  // owner lane: the last lane whose first item is <= item
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-          if (w->xoff[o + step] <= item) o += step;
-        const int tcs = __shfl(xtcs, o, kWave), tce = __shfl(xtce, o, kWave);
-        const int ond = __shfl(ndig, o, kWave);
-        if (active) {
-          const int q = item - w->xoff[o];
-          const int ocl = tce - tcs;
-          const bool oabbr = ocl > 10 + kMaxEv;
-          int tp, outp;
-          if (!oabbr || q < 5) {
-            tp = rev ? tce - 1 - q : tcs + q;
-            outp = q;
-          } else {
-            const int q2 = q - 5;
-            tp = rev ? tcs + 4 - q2 : tce - 5 + q2;
-            outp = 5 + 1 + ond + 1 + q2;
-          }
-          // op covering target position tp: the last op whose target start is <= tp
-          int lo = 0, hi = kOpHalo + (int)nseg + kOpHalo - 1;
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (w->ots[mid] <= tp) lo = mid;
-            else hi = mid - 1;
-          }
-          const uint32_t ow = w->opw[lo];
-          const int ot = w->ots[lo];
-          const int off = tp - ot;
-          const uint32_t oty = ow >> 30;
-          const bool covered = ot != INT_MIN && ot <= tp && off < (int)op_tadv(ow);
-          uint8_t ch = 0;
-          if (covered) {
-            if (oty == PW_OP_MATCH) {
-              const int x = d.offset + w->oqs[lo] + off;  // aligned-strand query position
-              ch = (x < 0 || x >= L) ? 0 : (rev ? comp2(R[L - 1 - x]) : R[x]);
-            } else {
-              ch = to_lower(A.lits[w->ols[lo] + (oty == PW_OP_SUB ? 0u : (uint32_t)off)]);
-              if (rev) ch = tab->comp[ch];
-            }
-          }
-          LDS uint8_t* otx = w->tx + o * kTxStride;
-          otx[1 + outp] = ch;
-          if (!covered) otx[40] = 1;
-        }
-      }
-      wave_sync();
-      if (slow) {
-        int len = (int)npos;
-        if (abbr) {  // first5[len-10]last5
-          my_tx[1 + 5] = '[';
-          uint32_t v = (uint32_t)(g.cl - 10);
-          for (int q = ndig - 1; q >= 0; q--) {
-            my_tx[1 + 6 + q] = (uint8_t)('0' + v % 10u);
-            v /= 10u;
-          }
-          my_tx[1 + 6 + ndig] = ']';
-          len = 12 + ndig;
-        }
-        if (my_tx[40]) {  // the context reaches past the staged ops: walk the op stream
-          Rec rr;
-          rr.ops = ops;
-          rr.lits = A.lits;
-          rr.R = R;
-          rr.NS = nullptr;
-          rr.tab = tab;
-          rr.qw = nullptr;
-          rr.qlo = 0;
-          rr.qn = 0;
-          rr.opw = w->opw;
-          rr.op_lo = (int)sb - kOpHalo;
-          rr.op_n = nseg + 2 * kOpHalo;
-          rr.lit0 = rr.lit1 = 0;
-          rr.ls0 = 0;
-          rr.ln = 0;
-          rr.lw = nullptr;
-          rr.l_lo = 0;
-          rr.l_n = 0;
-          rr.L = L;
-          rr.offset = d.offset;
-          rr.T = T;
-          rr.n_ops = n_ops;
-          rr.rev = rev;
-          LdsSink<kTx - 1> ks;
-          ks.buf = my_tx + 1;
-          ks.junk = w->junk + lane;
-          ks.pos = 0;
-          emit_tctx_walk(ks, rr, typ, (int)n, sb + idx, wd[k], qs[k], ts[k], ls[k]);
-          len = ks.pos;
-        }
-        my_tx[0] = (uint8_t)len;
-        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(my_tx);
-        v4u t0, t1;
-        t0.x = t32[0];
-        t0.y = t32[1];
-        t0.z = t32[2];
-        t0.w = t32[3];
-        t1.x = t32[4];
-        t1.y = t32[5];
-        t1.z = t32[6];
-        t1.w = t32[7];
-        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
-        dtx[0] = t0;
-        dtx[1] = t1;
-      }
-      wave_sync();
+      // an S run, a long insertion) are rendered by tctx_kernel: flag the slot
+      if (slow) W.sflag[s] = 1;
     }
     ev += nev;
     prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;
@@ -1142,7 +1030,6 @@ struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
   uint32_t ostart[kWave + 1];       // line starts in the page
-  uint8_t junk[kWave];
   uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
 };
 
@@ -1168,7 +1055,7 @@ __device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
 // inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
 // chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).
-__global__ __launch_bounds__(kWave* kWaves, 3) void render_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
@@ -1220,9 +1107,10 @@ __global__ __launch_bounds__(kWave* kWaves, 3) void render_kernel(pw_report_args
       }
       r.ops = nullptr;
       r.n_ops = 0;
-      // per-lane window: 64 forward-query bytes from 24 before the event (16-byte aligned)
+      // per-lane window: 48 forward-query bytes from 8 before the event (16-byte aligned; covers
+      // [rloc - 8, rloc + 25], the reads of all but long deletions)
       const int rl = event_rloc(r.L, rev, typ, h.qp, n);
-      int x0 = rl - 24;
+      int x0 = rl - 8;
       if (x0 < 0) x0 = 0;
       const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;  // >= qseq (16-byte aligned)
 #pragma unroll
@@ -1240,15 +1128,24 @@ __global__ __launch_bounds__(kWave* kWaves, 3) void render_kernel(pw_report_args
       in.qp = h.qp;
       in.tloc = h.tloc;
       in.ls = h.ls;
-      in.tmode = ((h.fn >> 28) & 1u) || (PW_ABL & 64) ? 0 : 1;
+      in.tmode = (((h.fn >> 28) & 1u) | (uint32_t)(PW_ABL & 64)) ? 0 : 1;
       in.ll = (int)((h.fn >> 23) & 7u);
       in.rl = (int)((h.fn >> 20) & 7u);
+      // loads issued ahead of the line (their latency overlaps the query-window staging): the
+      // pre-rendered target context and the next-stop entry the indel stop scan ends on
       in.tx = W.tx + (uint64_t)kTx * s;
+      in.ns_pre = kNsNone;
+      if (typ != PW_OP_SUB && r.NS && !skip && !(PW_ABL & 128)) {
+        const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
+        const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
+        const int k0 = rl + dl + (15 - a - x);
+        if (a + x <= 15 && (r.L - rt) + x - dl > 17 && k0 >= 0 && k0 < r.L) in.ns_pre = r.NS[k0];
+      }
       in.j = in.wd = 0;
       in.qs = in.ts = 0;
       LineSink k;
       k.buf = my_line;
-      k.junk = w->junk + lane;
+      k.junk = my_line + kLine;  // (the stride's spare bytes)
       k.pos = 0;
       int rel = 0;
 #if PW_ABL & 1
@@ -1387,6 +1284,138 @@ __global__ __launch_bounds__(kWave* kWaves, 3) void render_kernel(pw_report_args
   }
 }
 
+// ------------------------------------------------------------------ tctx_kernel
+// Target contexts that are not a plain copy of query bytes (another event within 5 bases, an
+// S run, a long insertion; setTContext, pafreport.cpp:120-128, revCompl :631, abbreviation
+// :918-927).  A wavefront takes 256 consecutive slots, compacts the flagged ones (ballots over
+// the flag bytes) and gives each lane one event: the lane stages its event's op words, forward
+// query bytes and literal bytes in LDS windows (independent loads, one wait), then walks the op
+// stream from the event's head op through the windows (tseq is never materialised; reads
+// outside a window fall back to global memory) and stores the 32-byte record (length byte +
+// field) for render_kernel.
+constexpr int kTcOps = 12;   // op words staged per event, from head op - 6
+constexpr int kTcQ = 48;     // forward-query bytes staged (16-byte aligned, from centre - 24)
+constexpr int kTcLit = 32;   // literal bytes staged (4-byte aligned, from ls - 8)
+struct TctxLane {
+  uint32_t opw[kTcOps];
+  uint8_t qw[kTcQ];
+  uint8_t lw[kTcLit];
+  uint8_t out[kTx + 4];      // record + junk
+};
+struct TctxWave {
+  TctxLane ln[kWave];
+  uint32_t list[4 * kWave];  // compacted flagged slots of the wave's 256-slot group (offsets)
+};
+__global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, Work W) {
+  __shared__ SmallTables tab;
+  __shared__ __attribute__((aligned(16))) TctxWave tw[kWaves];
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, kWave * kWaves);
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  LDS TctxWave* w = (LDS TctxWave*)&tw[wv];
+  LDS TctxLane* me = &w->ln[lane];
+  const uint64_t n_groups = (W.n_chunks * kWave + 255) / 256;
+  const uint32_t* f32 = reinterpret_cast<const uint32_t*>(W.sflag);
+  const uint64_t nf32 = W.n_chunks * kWave / 4;
+  for (uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv; gi < n_groups; gi += (uint64_t)gridDim.x * kWaves) {
+    const uint64_t fi = gi * kWave + lane;
+    const uint32_t f4 = (fi < nf32 ? f32[fi] : 0u) & 0x01010101u;
+    const uint32_t cnt = (uint32_t)__popc(f4);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t total = bcast(incl, kWave - 1);
+    if (total == 0) continue;
+    uint32_t o = incl - cnt;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if ((f4 >> (8 * q)) & 1u) w->list[o++] = (uint32_t)(4 * lane + q);
+    wave_sync();
+    for (uint32_t b = 0; b < total; b += kWave) {
+      const bool act = b + (uint32_t)lane < total;
+      if (act) {
+        const uint64_t s = gi * 256 + w->list[b + lane];
+        const Hot h = W.hot[s];
+        const Cold cd = W.cold[s];
+        const pw_aln_desc d = A.desc[cd.ai];
+        const uint32_t qi = d.ref & 0x7FFFFFFFu;
+        Rec r;
+        r.ops = A.ops + d.op_begin;
+        r.lits = A.lits;
+        r.R = A.qseq + h.qb;
+        r.L = h.L;
+        r.NS = nullptr;
+        r.tab = tp;
+        r.offset = d.offset;
+        r.T = d.t_len;
+        r.n_ops = d.n_ops;
+        r.rev = (h.fn >> 29) & 1u;
+        (void)qi;
+        // stage the windows: op words [j - 6, j + 6), forward query bytes around the event,
+        // literal bytes around its first literal
+        const int j = (int)cd.j;
+        int o0 = j - kTcOps / 2;
+        if (o0 < 0) o0 = 0;
+        uint32_t ow[kTcOps];
+#pragma unroll
+        for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? r.ops[o0 + q] : 0u;
+        const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
+        int x0 = fc - kTcQ / 2;
+        if (x0 < 0) x0 = 0;
+        const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;
+        v4u qv[kTcQ / 16];
+#pragma unroll
+        for (int q = 0; q < kTcQ / 16; q++) qv[q] = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+        uint32_t l0 = h.ls >= 8u ? (h.ls - 8u) & ~3u : 0u;
+        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
+        uint32_t lv[kTcLit / 4];
+#pragma unroll
+        for (int q = 0; q < kTcLit / 4; q++) lv[q] = l32[q];
+#pragma unroll
+        for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
+#pragma unroll
+        for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];
+#pragma unroll
+        for (int q = 0; q < kTcLit / 4; q++) reinterpret_cast<LDS uint32_t*>(me->lw)[q] = lv[q];
+        r.opw = me->opw;
+        r.op_lo = o0;
+        r.op_n = (uint32_t)kTcOps;
+        r.qw = me->qw;
+        r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+        r.qn = kTcQ;
+        r.lw = me->lw;
+        r.l_lo = l0;
+        r.l_n = kTcLit;
+        r.lit0 = r.lit1 = 0;
+        r.ls0 = 0;
+        r.ln = 0;
+        const uint32_t wd = opword(r, cd.j);
+        int ne = (int)(h.fn & kNBig);
+        if ((uint32_t)ne == kNBig) ne = event_len(r, cd.j, wd);
+        LdsSink<kTx - 1> ks;
+        ks.buf = me->out + 1;
+        ks.junk = me->out + kTx;
+        ks.pos = 0;
+        emit_tctx_walk(ks, r, wd >> 30, ne, cd.j, wd, cd.qs, cd.ts, h.ls);
+        me->out[0] = (uint8_t)ks.pos;
+        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
+        v4u t0, t1;
+        t0.x = t32[0];
+        t0.y = t32[1];
+        t0.z = t32[2];
+        t0.w = t32[3];
+        t1.x = t32[4];
+        t1.y = t32[5];
+        t1.z = t32[6];
+        t1.w = t32[7];
+        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
+        dtx[0] = t0;
+        dtx[1] = t1;
+      }
+    }
+    wave_sync();
+  }
+}
+
 // ------------------------------------------------------------------ fixup_kernel
 // Lines longer than the LDS line buffer, one per thread, rewritten in place (their bytes were
 // reserved).  The record is read straight from global memory (no windows).
@@ -1438,6 +1467,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     in.ll = (int)((h.fn >> 23) & 7u);
     in.rl = (int)((h.fn >> 20) & 7u);
     in.tx = nullptr;
+    in.ns_pre = kNsNone;
     in.j = cd.j;
     in.wd = wd;
     in.qs = cd.qs;
@@ -1565,11 +1595,15 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
   pw::work_layout(static_cast<uint8_t*>(args->workspace), args->n_ev_slots, args->n_alns, &W);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;  // counters
+  if (W.n_chunks && hipMemsetAsync(W.sflag, 0, W.n_chunks * pw::kWave, st) != hipSuccess) return PW_E_HIP;
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
   if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;
   hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
+    uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;
+    if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
+    hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
     if (rg > (uint64_t)ncu * 3u) rg = (uint64_t)ncu * 3u;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);

@@ -1,0 +1,289 @@
+"""GapAssem column consensus on the HIP path, rows sharded over GPUs.
+
+The single-GPU product is the C++ driver pw_gapassem_run (gapassem_consensus CLI).  This module
+is the multi-GPU driver of the same computation, one process per GPU:
+
+  every rank    reads the PWL1 row headers (GASeq offset/seqlen/clp5/clp3/revcompl), derives
+                minoffset and the layout length (GSeqAlign bookkeeping, GapAssem.cpp:605-641,
+                694-716) and stages ITS rows (a contiguous, base-balanced block) in HBM;
+  pw_msa_count  buildMSA's toMSA/addNuc/addGap scatter of those rows -> partial [n_cols x 6]
+                int32 histograms + mincol/maxcol (GapAssem.cpp:551-591, 1088-1106);
+  collectives   one all-reduce(SUM) of the histograms and one all-reduce(MIN) of
+                (mincol, -maxcol, first bad row) — RCCL over xGMI with the "nccl" backend.
+                Integer sums are order-independent: the merged histograms are bit-identical to
+                a single-GPU count;
+  pw_msa_call   bestChar of every column (GapAssem.cpp:1048-1069), identical on every rank;
+  pw_msa_refine refineMSA's consensus string and, with removeConsGaps, the closed-form
+                removeColumn/removeBase/removeClipGaps edits of the rank's own rows
+                (GapAssem.cpp:1143-1181).
+Rank 0 writes the PWC1 result (edited rows gathered from their owners).  Messages and exit codes
+are the reference's (trimmed-row warnings :1096-1101, bad index GapAssem.h:366-370 -> 1, zero
+coverage :1121-1131 -> 5), in row order, as the single-GPU driver prints them.
+
+Device work goes through an engine: HipEngine is the product (libpwasm_amd.so on this rank's GPU;
+there is no CPU path).  Tests substitute a CPU engine to exercise the collective choreography on
+gloo without a GPU."""
+from __future__ import annotations
+
+import ctypes
+import struct
+
+import numpy as np
+
+INT_MAX = 2 ** 31 - 1
+
+
+class Layout:
+    """PWL1 rows (tests/pwl_format.md): every row's header; bases/gaps of the rows in `load`
+    (None = all)."""
+
+    def __init__(self, path: str, load=None):
+        with open(path, "rb") as f:
+            b = f.read(8)
+            if len(b) < 8 or b[:4] != b"PWL1" or struct.unpack("<I", b[4:8])[0] == 0:
+                raise ValueError("bad layout header")
+            (n,) = struct.unpack("<I", b[4:8])
+            hdr = np.zeros((n, 5), dtype=np.int64)
+            numgaps = np.zeros(n, dtype=np.int64)
+            self.seq, self.ofs = {}, {}
+            for r in range(n):
+                h = f.read(20)
+                if len(h) < 20:
+                    raise ValueError("bad row header")
+                hdr[r] = struct.unpack("<5i", h)
+                L = int(hdr[r, 1])
+                if L < 0:
+                    raise ValueError("bad row header")
+                seq = f.read(L)
+                ofs = np.frombuffer(f.read(2 * L), dtype="<i2")
+                if len(seq) != L or ofs.size != L:
+                    raise ValueError("truncated row")
+                numgaps[r] = int(ofs.sum(dtype=np.int64))  # setGap bookkeeping
+                if load is None or r in load:
+                    self.seq[r] = np.frombuffer(seq, dtype=np.uint8)
+                    self.ofs[r] = ofs.astype(np.int16)
+        self.n = n
+        self.offset, self.seqlen, self.clp5, self.clp3, self.rev = (hdr[:, i].copy() for i in range(5))
+        self.numgaps = numgaps
+        self.minoffset = int(self.offset.min())
+        self.length = max(int((self.offset + self.seqlen + self.numgaps).max()) - self.minoffset, 0)
+
+    def clips(self, r):
+        """clipL / clipR oriented by revcompl (GapAssem.cpp:557-564)."""
+        return (int(self.clp3[r]), int(self.clp5[r])) if self.rev[r] else (int(self.clp5[r]), int(self.clp3[r]))
+
+
+def shard_rows(seqlen, world: int):
+    """Contiguous row blocks with about equal bases per rank, every block non-empty when
+    world <= rows: [(lo, hi)] per rank."""
+    n = len(seqlen)
+    cum = np.concatenate([[0], np.cumsum(np.asarray(seqlen, dtype=np.int64))])
+    tot = int(cum[-1])
+    cuts = [0]
+    for k in range(1, world):
+        c = int(np.searchsorted(cum, tot * k / world, side="left"))
+        c = min(max(c, cuts[-1] + (1 if n >= world else 0)), n - (world - k) if n >= world else n)
+        cuts.append(c)
+    cuts.append(n)
+    return [(cuts[k], cuts[k + 1]) for k in range(world)]
+
+
+class HipEngine:
+    """Device work of one shard through the C-ABI (pw_msa_count / pw_msa_call / pw_msa_refine)."""
+
+    def __init__(self, device: str = "cuda:0"):
+        import torch
+        from pwasm_amd import lib
+        self.torch, self.lib, self.device = torch, lib(), device
+        self.stream = torch.cuda.current_stream(device)
+
+    def stage(self, lay: Layout, rows, ncols: int):
+        from pwasm_amd import MsaArgs, MsaRefineArgs
+        torch, dev = self.torch, self.device
+        rows = list(rows)
+        nr = len(rows)
+        if nr == 0:
+            raise ValueError("gapassem: a shard without rows")
+        lens = np.array([int(lay.seqlen[r]) for r in rows], dtype=np.int32)
+        row_off = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))])[:nr].astype(np.uint64)
+        seq = np.concatenate([lay.seq[r] for r in rows])
+        ofs = np.concatenate([lay.ofs[r] for r in rows])
+        cl = np.array([lay.clips(r)[0] for r in rows], dtype=np.int32)
+        cr = np.array([lay.clips(r)[1] for r in rows], dtype=np.int32)
+        col0 = np.array([int(lay.offset[r]) - lay.minoffset for r in rows], dtype=np.int32)
+        slot_base = np.zeros(nr + 1, dtype=np.int64)
+        nslots = int(self.lib.pw_msa_slots(lens.ctypes.data, nr, slot_base.ctypes.data))
+
+        def t(a):
+            a = np.ascontiguousarray(a)
+            if a.size == 0:
+                a = np.zeros(1, dtype=a.dtype)
+            return torch.from_numpy(a.view(np.uint8) if a.dtype == np.uint64 else a).to(dev)
+
+        def e(n, dt):
+            return torch.empty(max(int(n), 1), dtype=dt, device=dev)
+
+        d = {"seq": t(seq), "ofs": t(ofs), "row_off": t(row_off), "len": t(lens), "col0": t(col0), "cl": t(cl),
+             "cr": t(cr), "slot": t(slot_base), "scr": e(2 * nslots, torch.int32),
+             "counts": e(ncols * 6, torch.int32), "cons": e(ncols, torch.uint8), "mm": e(4, torch.int32),
+             "gp": e(ncols, torch.int32), "tg": e(self.lib.pw_msa_refine_tiles(ncols), torch.int32),
+             "cout": e(ncols, torch.uint8), "clen": e(1, torch.int32),
+             "roffs": t(np.array([int(lay.offset[r]) for r in rows], dtype=np.int32)),
+             "ofso": e(ofs.size, torch.int16), "offo": e(nr, torch.int32), "ngo": e(nr, torch.int64),
+             "ng0": t(np.array([int(lay.numgaps[r]) for r in rows], dtype=np.int64))}
+        a = MsaArgs()
+        a.seq, a.ofs, a.row_off, a.row_len = (d[k].data_ptr() for k in ("seq", "ofs", "row_off", "len"))
+        a.col0, a.clip_l, a.clip_r, a.slot_base = (d[k].data_ptr() for k in ("col0", "cl", "cr", "slot"))
+        a.scratch, a.counts, a.consensus, a.minmax = (d[k].data_ptr() for k in ("scr", "counts", "cons", "mm"))
+        a.n_slots, a.n_rows, a.n_cols = nslots, nr, ncols
+        ra = MsaRefineArgs()
+        ra.gap_prefix, ra.tile_gaps, ra.cons_out, ra.cons_len = (d[k].data_ptr() for k in ("gp", "tg", "cout", "clen"))
+        ra.row_offset, ra.ofs_out, ra.offset_out, ra.numgaps_out = (d[k].data_ptr()
+                                                                    for k in ("roffs", "ofso", "offo", "ngo"))
+        return dict(rows=rows, nr=nr, lens=lens, row_off=row_off, ncols=ncols, d=d, args=a, rargs=ra)
+
+    def _rc(self, name, rc):
+        if rc != 0:
+            raise RuntimeError(f"{name}: {rc}")
+
+    def count(self, st):
+        """-> (counts [ncols*6] int32, minmax [4] int32) device tensors; minmax[2] = first bad
+        row of this shard (local index) or INT_MAX."""
+        self._rc("pw_msa_count", self.lib.pw_msa_count(ctypes.byref(st["args"]), self.stream.cuda_stream))
+        return st["d"]["counts"], st["d"]["mm"]
+
+    def call(self, st):
+        """bestChar per column + first zero-coverage column (minmax[3]) from the merged counts."""
+        self._rc("pw_msa_call", self.lib.pw_msa_call(ctypes.byref(st["args"]), self.stream.cuda_stream))
+        return st["d"]["cons"], st["d"]["mm"]
+
+    def refine(self, st, remove_gaps: bool):
+        """Launch pw_msa_refine (device results stay in st["d"])."""
+        d, ra = st["d"], st["rargs"]
+        ra.remove_gaps = 1 if remove_gaps else 0
+        if remove_gaps:
+            d["ngo"].copy_(d["ng0"])
+        self._rc("pw_msa_refine", self.lib.pw_msa_refine(ctypes.byref(st["args"]), ctypes.byref(ra),
+                                                         self.stream.cuda_stream))
+
+    def refine_host(self, st, remove_gaps: bool):
+        """-> (consensus bytes, {row: (offset, numgaps, ofs)} for own rows when remove_gaps)."""
+        self.refine(st, remove_gaps)
+        d = st["d"]
+        clen = int(d["clen"].cpu().item())
+        cons = bytes(d["cout"][:clen].cpu().numpy())
+        rows = {}
+        if remove_gaps:
+            offo, ngo, ofso = d["offo"].cpu().numpy(), d["ngo"].cpu().numpy(), d["ofso"].cpu().numpy()
+            for k, r in enumerate(st["rows"]):
+                o = int(st["row_off"][k])
+                rows[r] = (int(offo[k]), int(ngo[k]), ofso[o:o + int(st["lens"][k])].copy())
+        return cons, rows
+
+
+def all_reduce(t, op, group=None):
+    """dist.all_reduce; device tensors under gloo (CPU-only collectives) go through the host."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def _bad_index_col(lay: Layout, r: int, ncols: int):
+    """First column toMSA touches out of range for row r (GapAssem.cpp:568-588)."""
+    cl, cr = lay.clips(r)
+    col = int(lay.offset[r]) - lay.minoffset
+    L = int(lay.seqlen[r])
+    for i, g in enumerate(lay.ofs[r].tolist()):
+        clipped = i < cl or i >= L - cr
+        for _ in range(g):
+            if not clipped and (col < 0 or col >= ncols):
+                return col
+            col += 1
+        if col < 0 or col >= ncols:
+            return col
+        col += 1
+    return None
+
+
+def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=None):
+    """refineMSA's consensus with rows sharded over the ranks of `group` (torch.distributed; a
+    single process when it is not initialised).  Returns (exit_code, stderr_text, pwc_bytes) on
+    rank 0 — the same bytes as the gapassem_consensus CLI — and (exit_code, "", None) elsewhere."""
+    import torch
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    hdr = Layout(layout_path, load=set())
+    lo, hi = shard_rows(hdr.seqlen, world)[rank]
+    lay = Layout(layout_path, load=set(range(lo, hi)))
+    ncols = lay.length
+    if ncols <= 0 or ncols > INT_MAX:
+        return 1, ("MSAColumns op[]: bad index 0 (size=%d)\n" % ncols) if rank == 0 else "", None
+    neg = any(int(lay.ofs[r].min(initial=0)) < 0 for r in range(lo, hi)) if remove_gaps else False
+    if world > 1 and remove_gaps:
+        flag = [None] * world
+        dist.all_gather_object(flag, neg, group=group)
+        neg = any(flag)
+    if neg:
+        return 2, "removeConsGaps with negative gap values is not supported on the HIP path\n" if rank == 0 else "", None
+    engine = engine or HipEngine()
+    st = engine.stage(lay, range(lo, hi), ncols)
+    counts, mm = engine.count(st)
+    mm_h = [int(x) for x in mm.cpu().tolist()]
+    bad = lo + mm_h[2] if mm_h[2] != INT_MAX else INT_MAX
+    if world > 1:
+        red = torch.tensor([mm_h[0], -mm_h[1], bad], dtype=torch.int64, device=counts.device)
+        all_reduce(counts, dist.ReduceOp.SUM, group)
+        all_reduce(red, dist.ReduceOp.MIN, group)
+        red = [int(x) for x in red.cpu().tolist()]
+        mm_h[0], mm_h[1], bad = red[0], -red[1], red[2]
+        mm.copy_(torch.tensor([mm_h[0], mm_h[1], INT_MAX, INT_MAX], dtype=torch.int32))
+    err = []
+    for r in range(min(hdr.n if bad == INT_MAX else bad + 1, hdr.n)):
+        if int(lay.seqlen[r] - lay.clp3[r] - lay.clp5[r]) < 1:
+            err.append("Warning: sequence row%u (length %d) was trimmed too badly (%d,%d) -- should be removed from "
+                       "MSA w/ row0!\n" % (r, lay.seqlen[r], lay.clp5[r], lay.clp3[r]))
+    if bad != INT_MAX:
+        col = _bad_index_col(lay, bad, ncols) if lo <= bad < hi else None
+        if world > 1:
+            cols = [None] * world
+            dist.all_gather_object(cols, col, group=group)
+            col = next(c for c in cols if c is not None)
+        err.append("MSAColumns op[]: bad index %d (size=%d)\n" % (col, ncols))
+        return 1, "".join(err) if rank == 0 else "", None
+    _, mm = engine.call(st)
+    zero = int(mm[3].item())
+    mincol, maxcol = mm_h[0], max(mm_h[1], 0)
+    if zero != INT_MAX:
+        err.append("WARNING: 0 coverage column %d (mincol=%d) found within alignment of %d seqs!\n"
+                   % (zero, mincol, hdr.n))
+        err.extend("row%u\n" % r for r in range(hdr.n))
+        return 5, "".join(err) if rank == 0 else "", None
+    cons_s, own, n_removed = b"", {}, 0
+    if mincol != INT_MAX:
+        cons_s, own = engine.refine_host(st, remove_gaps)
+        if remove_gaps:
+            n_removed = (maxcol - mincol + 1) - len(cons_s)
+    if world > 1 and remove_gaps:
+        parts = [None] * world
+        dist.all_gather_object(parts, own, group=group)
+        own = {k: v for p in parts for k, v in p.items()}
+    if rank != 0:
+        return 0, "", None
+    full = lay if (remove_gaps and own) or world == 1 else Layout(layout_path)
+    counts_h = counts.cpu().numpy().astype("<i4")
+    out = [b"PWC1", struct.pack("<6i", ncols, lay.minoffset, -1 if mincol == INT_MAX else mincol, maxcol, len(cons_s),
+                                n_removed), cons_s, counts_h.tobytes(), struct.pack("<I", hdr.n)]
+    for r in range(hdr.n):
+        if remove_gaps and r in own:
+            off, ng, ofs = own[r]
+        else:
+            off, ng, ofs = int(lay.offset[r]), int(lay.numgaps[r]), full.ofs[r]
+        out.append(struct.pack("<2i", off, ng))
+        out.append(np.asarray(ofs, dtype="<i2").tobytes())
+    return 0, "".join(err), b"".join(out)

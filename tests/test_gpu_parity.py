@@ -232,3 +232,96 @@ def test_sharded_run_on_gpu(built, tmp_path, world):
         got.append((shard.read_items(ip), gmap))
     out, err, rc = shard.merge_items(got)
     assert (rc, out, err) == run([ORACLE, "-r", fa, dup])
+
+
+# ---------------------------------------------------------------- GapAssem refineMSA, removeConsGaps
+def test_gapassem_remove_gaps_hand(built, tmp_path):
+    lay = tmp_path / "l.pwl"
+    write_pwl(lay, [(0, "ACGT", [0, 0, 1, 0], 0, 0, 0), (1, "CNGA", [0, 0, 1, 0], 0, 0, 0),
+                    (2, "-G", [0, 0], 0, 0, 0)])
+    assert ga_same(lay, tmp_path, ["--remove-gaps"]) == 0
+    r = read_pwc(tmp_path / "p.pwc")
+    assert r["cons"] == "ACGGA" and r["removed"] == 1
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gapassem_remove_gaps_random(built, tmp_path, seed):
+    from test_gapassem_refine import random_layout
+    rng = random.Random(500 + seed)
+    rows = random_layout(rng, rng.randint(2, 30), clip=seed % 2 == 1)
+    lay = tmp_path / "r.pwl"
+    write_pwl(lay, rows)
+    ga_same(lay, tmp_path, ["--remove-gaps", "--no-refine-clipping"])
+    ga_same(lay, tmp_path, ["--no-refine-clipping"])
+
+
+@pytest.mark.parametrize("scale", [0.0005, 0.005, 0.02])
+def test_gapassem_remove_gaps_synthetic(built, tmp_path, scale):
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", scale, "--rows", 40, "--out", lay])
+    assert rc == 0, err
+    assert ga_same(lay, tmp_path, ["--remove-gaps"]) == 0
+    assert read_pwc(tmp_path / "p.pwc")["removed"] > 0
+
+
+def test_gapassem_remove_gaps_negative_refused(built, tmp_path):
+    lay = tmp_path / "n.pwl"
+    write_pwl(lay, [(0, "ACGT", [0, -1, 0, 0], 0, 0, 0), (0, "ACGT", [0, 0, 0, 0], 0, 0, 0)])
+    rc, _, err = run([GA_CLI, lay, tmp_path / "p.pwc", "--remove-gaps"])
+    assert rc == 2 and b"negative gap" in err
+
+
+# ---------------------------------------------------------------- multi-GPU GapAssem driver
+def _ga_cli(lay, tmp_path, remove):
+    extra = ["--remove-gaps"] if remove else []
+    rc, _, err = run([GA_CLI, lay, tmp_path / "c.pwc", *extra])
+    return rc, err.decode(), (open(tmp_path / "c.pwc", "rb").read() if rc == 0 else None)
+
+
+@pytest.mark.parametrize("remove", [False, True])
+def test_gapassem_driver_single_rank_on_gpu(built, tmp_path, remove):
+    from pwasm_amd import gapassem
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.005, "--rows", 30, "--out", lay])
+    assert rc == 0, err
+    got = gapassem.consensus(str(lay), remove_gaps=remove)
+    assert got == _ga_cli(lay, tmp_path, remove)
+    assert got[0] == 0
+
+
+def _ga_rank(rank, world, port, lay, remove, q):
+    import torch.distributed as dist
+    from pwasm_amd import gapassem
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = gapassem.consensus(lay, remove_gaps=remove)  # HIP engine on cuda:0
+        if rank == 0:
+            q.put(res)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gapassem_sharded_on_gpu(built, tmp_path):
+    """Two ranks (both on cuda:0, gloo): partial histograms of each half of the rows on the GPU,
+    merged by the all-reduce, refined per shard — same bytes as the single-GPU CLI."""
+    import socket
+    import torch.multiprocessing as mp
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.003, "--rows", 12, "--out", lay])
+    assert rc == 0, err
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ga_rank, args=(r, 2, port, str(lay), True, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == _ga_cli(lay, tmp_path, True)
