@@ -57,6 +57,8 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     dev_name = f"cuda:{local}"
     torch.cuda.set_device(local)
+    if args.config == 5:
+        return bench_gapassem(args, world, rank, dev_name)
 
     # ---- data: this rank's shard (synthetic, seeded; generated outside the timed region)
     tmp = tempfile.mkdtemp(prefix=f"pwbench{rank}_")
@@ -156,6 +158,104 @@ def main():
                          "kernel": "pw_report_events (index+tctx+render+fixup+finalize)", "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_gapassem(args, world, rank, dev_name):
+    """BASELINE.json configs[4]: GapAssem consensus of one 200-row, ~1M-column layout (pwsynth
+    cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step = pw_msa_count on the
+    rank's rows + all-reduce of the [n_cols x 6] histograms and of mincol/-maxcol (RCCL) +
+    pw_msa_call + pw_msa_refine with removeConsGaps (the library default: consensus string +
+    row edits).  Throughput = layout bases per second (all rows, whole job)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from pwasm_amd import gapassem
+
+    tmp = tempfile.mkdtemp(prefix=f"pwga{rank}_")
+    lay_path = os.path.join(tmp, "l.pwl")
+    t0 = time.time()
+    subprocess.run([str(REPO / "synth/build/pwsynth"), "layout", "--config", "5", "--scale", str(args.scale),
+                    "--seed", "5", "--out", lay_path], check=True, stderr=subprocess.DEVNULL)
+    hdr = gapassem.Layout(lay_path, load=set())
+    lo, hi = gapassem.shard_rows(hdr.seqlen, world)[rank]
+    lay = gapassem.Layout(lay_path, load=set(range(lo, hi)))
+    eng = gapassem.HipEngine(dev_name)
+    st = eng.stage(lay, range(lo, hi), lay.length)
+    total_bases = int(hdr.seqlen.sum())
+    log(f"[rank {rank}] layout {hdr.n} rows, {lay.length} columns, {total_bases} bases; rows [{lo},{hi}) "
+        f"({time.time() - t0:.1f}s host prep)")
+    mm = st["d"]["mm"]
+    red = torch.empty(2, dtype=torch.int32, device=dev_name)
+
+    def step():
+        counts, _ = eng.count(st)
+        if world > 1:
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+            red[0] = mm[0]
+            red[1] = -mm[1]
+            dist.all_reduce(red, op=dist.ReduceOp.MIN)
+            mm[0] = red[0]
+            mm[1] = -red[1]
+        eng.call(st)
+        eng.refine(st, True)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    zero = int(mm[3].item())
+    assert zero == 2 ** 31 - 1 and int(mm[2].item()) == 2 ** 31 - 1, "layout errors"
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    t_el = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    max_el = t_el
+    if world > 1:
+        t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        max_el = float(t.item())
+    if rank == 0:
+        ncols = lay.length
+        # algorithmic bytes (SURVEY.md §8(d)): 16 B row descriptor + 3 B per base (base + int16
+        # gap) read, 24 B counts + 1 B consensus per column written; this rank's rows
+        own = int(lay.seqlen[lo:hi].sum())
+        alg = 16 * (hi - lo) + 3 * own + 25 * ncols
+        achieved = alg / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": "GapAssem layout bases called/sec (count + histogram all-reduce + bestChar + refineMSA)",
+            "value": total_bases * args.steps / max_el,
+            "unit": "bases/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": max_el * 1000.0 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (pwsynth layout cfg5, seed 5)",
+            "config": {"workload": f"cfg5: {hdr.n} rows x {ncols} columns, {total_bases} bases, removeConsGaps",
+                       "rows": int(hdr.n), "columns": int(ncols), "parallelism": f"rows sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "pw_msa_count+pw_msa_call+pw_msa_refine (rank 0)", "kernel_ms": round(kern_ms, 4),
+                         "alg_bytes_per_launch": alg},
+            "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

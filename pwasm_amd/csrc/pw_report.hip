@@ -64,6 +64,9 @@ constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, f
 constexpr uint32_t kNBig = (1u << 20) - 1;  // evtbases length field saturates here
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
+#ifndef PW_INDEX_OCC
+#define PW_INDEX_OCC 4
+#endif
 #ifndef PW_RENDER_OCC
 #define PW_RENDER_OCC 3
 #endif
@@ -799,19 +802,38 @@ __device__ __forceinline__ int ndigits(uint32_t v) {
          (v >= 10000000u) + (v >= 100000000u) + (v >= 1000000000u);
 }
 
-__device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
-                                             LDS IndexWave* w, uint32_t ai, int lane) {
-  const pw_aln_desc d = A.desc[ai];
+// A record's head, loaded one record ahead (index_kernel's loop): descriptor, query location,
+// next record's first event slot and the first 128 op words (2 per lane).
+struct RecPre {
+  pw_aln_desc d;
+  uint64_t qb, ev_next;
+  int L;
+  uint32_t w0, w1;
+};
+__device__ __forceinline__ void rec_pre(const pw_report_args& A, uint32_t ai, const pw_aln_desc& d, int lane,
+                                        RecPre& p) {
+  p.d = d;
   const uint32_t qi = d.ref & 0x7FFFFFFFu;
+  p.qb = A.qoff[qi];
+  p.L = A.qlen[qi];
+  p.ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
   const uint32_t* ops = A.ops + d.op_begin;
-  const uint64_t qb = A.qoff[qi];
+  p.w0 = (uint32_t)lane < d.n_ops ? ops[lane] : 0u;
+  p.w1 = (uint32_t)(lane + 64) < d.n_ops ? ops[lane + 64] : 0u;
+}
+
+__device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
+                                             LDS IndexWave* w, uint32_t ai, int lane, const RecPre& pre) {
+  const pw_aln_desc d = pre.d;
+  const uint32_t* ops = A.ops + d.op_begin;
+  const uint64_t qb = pre.qb;
   const uint8_t* R = A.qseq + qb;
-  const int L = A.qlen[qi];
+  const int L = pre.L;
   const bool rev = (d.ref & PW_REF_REVERSE) != 0;
   const int T = d.t_len;
   const uint32_t n_ops = d.n_ops;
   const uint64_t evb = d.ev_begin;
-  const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
+  const uint64_t ev_next = pre.ev_next;
   const uint32_t nmax = (uint32_t)(ev_next - evb);
   const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
 
@@ -831,7 +853,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const uint32_t idx = 64 * k + lane;
-      wd[k] = idx < nseg ? ops[sb + idx] : 0u;
+      wd[k] = sb == 0 ? (k == 0 ? pre.w0 : pre.w1) : (idx < nseg ? ops[sb + idx] : 0u);
       const uint32_t qa = idx < nseg ? op_qadv(wd[k]) : 0u, ta = idx < nseg ? op_tadv(wd[k]) : 0u,
                      la = idx < nseg ? op_ladv(wd[k]) : 0u;
       const uint32_t qi_ = wave_incl_scan(qa, lane), ti_ = wave_incl_scan(ta, lane), li_ = wave_incl_scan(la, lane);
@@ -973,8 +995,14 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
         }
       }
       // ---- target contexts that are not a plain query copy (another event within 5 bases,
-      // an S run, a long insertion) are rendered by tctx_kernel: flag the slot
-      if (slow) W.sflag[s] = 1;
+      // an S run, a long insertion) are rendered by tctx_kernel: flag the slot and leave the
+      // walk's start (head op, its query / target position, record geometry) in its tx record
+      if (slow) {
+        W.sflag[s] = 1;
+        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
+        dtx[0] = (v4u){d.op_begin, sb + (uint32_t)(64 * k + lane), n_ops, (uint32_t)qs[k]};
+        dtx[1] = (v4u){(uint32_t)ts[k], (uint32_t)T, (uint32_t)d.offset, 0u};
+      }
     }
     ev += nev;
     prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;
@@ -1010,15 +1038,32 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   }
 }
 
-__global__ __launch_bounds__(kWave* kWaves) void index_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves, PW_INDEX_OCC) void index_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, kWave * kWaves);
   __syncthreads();
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   LDS IndexWave* w = (LDS IndexWave*)&iw[wv];
-  for (uint32_t ai = blockIdx.x * kWaves + wv; ai < A.n_alns; ai += gridDim.x * kWaves) index_record(A, W, tp, w, ai, lane);
+  // records ai, ai + stride, ...: the next record's head loads are issued before this record is
+  // processed (its descriptor two records ahead), so their latency overlaps the work
+  const uint32_t stride = gridDim.x * kWaves;
+  uint32_t ai = blockIdx.x * kWaves + wv;
+  RecPre cur;
+  pw_aln_desc dn;
+  if (ai < A.n_alns) rec_pre(A, ai, A.desc[ai], lane, cur);
+  if (ai + stride < A.n_alns) dn = A.desc[ai + stride];
+  for (; ai < A.n_alns; ai += stride) {
+    const uint32_t an = ai + stride;
+    RecPre nxt;
+    pw_aln_desc dnn;
+    if (an < A.n_alns) rec_pre(A, an, dn, lane, nxt);
+    if (an + stride < A.n_alns) dnn = A.desc[an + stride];
+    index_record(A, W, tp, w, ai, lane, cur);
+    cur = nxt;
+    dn = dnn;
+  }
   // the padding slots of the last chunk are empty
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
   if (blockIdx.x == 0)
@@ -1061,7 +1106,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, kWave * kWaves);
   __syncthreads();
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
   LDS uint8_t* my_line = w->line + lane * kLStride;
   LDS uint8_t* my_qw = w->qw + lane * kQStride;
@@ -1295,11 +1340,9 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
 // field) for render_kernel.
 constexpr int kTcOps = 12;   // op words staged per event, from head op - 6
 constexpr int kTcQ = 48;     // forward-query bytes staged (16-byte aligned, from centre - 24)
-constexpr int kTcLit = 32;   // literal bytes staged (4-byte aligned, from ls - 8)
 struct TctxLane {
   uint32_t opw[kTcOps];
   uint8_t qw[kTcQ];
-  uint8_t lw[kTcLit];
   uint8_t out[kTx + 4];      // record + junk
 };
 struct TctxWave {
@@ -1312,7 +1355,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, kWave * kWaves);
   __syncthreads();
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   LDS TctxWave* w = (LDS TctxWave*)&tw[wv];
   LDS TctxLane* me = &w->ln[lane];
   const uint64_t n_groups = (W.n_chunks * kWave + 255) / 256;
@@ -1335,24 +1378,29 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
       if (act) {
         const uint64_t s = gi * 256 + w->list[b + lane];
         const Hot h = W.hot[s];
-        const Cold cd = W.cold[s];
-        const pw_aln_desc d = A.desc[cd.ai];
-        const uint32_t qi = d.ref & 0x7FFFFFFFu;
+        const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+        const v4u p0 = tp4[0], p1 = tp4[1];  // op_begin, j, n_ops, qs | ts, T, offset (index_kernel)
         Rec r;
-        r.ops = A.ops + d.op_begin;
+        r.ops = A.ops + p0.x;
         r.lits = A.lits;
         r.R = A.qseq + h.qb;
         r.L = h.L;
         r.NS = nullptr;
         r.tab = tp;
-        r.offset = d.offset;
-        r.T = d.t_len;
-        r.n_ops = d.n_ops;
+        r.offset = (int)p1.z;
+        r.T = (int)p1.y;
+        r.n_ops = p0.z;
         r.rev = (h.fn >> 29) & 1u;
-        (void)qi;
-        // stage the windows: op words [j - 6, j + 6), forward query bytes around the event,
-        // literal bytes around its first literal
-        const int j = (int)cd.j;
+        // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
+        // and forward query bytes around the event are staged in LDS
+        r.lit0 = h.l0;
+        r.lit1 = h.l1;
+        r.ls0 = h.ls;
+        r.ln = 8;
+        r.lw = nullptr;
+        r.l_lo = 0;
+        r.l_n = 0;
+        const int j = (int)p0.y;
         int o0 = j - kTcOps / 2;
         if (o0 < 0) o0 = 0;
         uint32_t ow[kTcOps];
@@ -1365,37 +1413,24 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         v4u qv[kTcQ / 16];
 #pragma unroll
         for (int q = 0; q < kTcQ / 16; q++) qv[q] = *reinterpret_cast<const v4u*>(a0 + 16 * q);
-        uint32_t l0 = h.ls >= 8u ? (h.ls - 8u) & ~3u : 0u;
-        const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
-        uint32_t lv[kTcLit / 4];
-#pragma unroll
-        for (int q = 0; q < kTcLit / 4; q++) lv[q] = l32[q];
 #pragma unroll
         for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
 #pragma unroll
         for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];
-#pragma unroll
-        for (int q = 0; q < kTcLit / 4; q++) reinterpret_cast<LDS uint32_t*>(me->lw)[q] = lv[q];
         r.opw = me->opw;
         r.op_lo = o0;
         r.op_n = (uint32_t)kTcOps;
         r.qw = me->qw;
         r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
         r.qn = kTcQ;
-        r.lw = me->lw;
-        r.l_lo = l0;
-        r.l_n = kTcLit;
-        r.lit0 = r.lit1 = 0;
-        r.ls0 = 0;
-        r.ln = 0;
-        const uint32_t wd = opword(r, cd.j);
+        const uint32_t wd = opword(r, (uint32_t)j);
         int ne = (int)(h.fn & kNBig);
-        if ((uint32_t)ne == kNBig) ne = event_len(r, cd.j, wd);
+        if ((uint32_t)ne == kNBig) ne = event_len(r, (uint32_t)j, wd);
         LdsSink<kTx - 1> ks;
         ks.buf = me->out + 1;
         ks.junk = me->out + kTx;
         ks.pos = 0;
-        emit_tctx_walk(ks, r, wd >> 30, ne, cd.j, wd, cd.qs, cd.ts, h.ls);
+        emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);
         me->out[0] = (uint8_t)ks.pos;
         const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
         v4u t0, t1;
