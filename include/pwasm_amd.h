@@ -49,12 +49,15 @@ typedef struct pw_aln_desc {
   uint32_t op_begin;   /* first op in ops[] */
   uint32_t n_ops;      /* ops of this record */
   uint32_t lit_begin;  /* first literal byte in lits[] */
-  uint32_t ref;        /* bits 0..30 query index; bit 31 = reverse strand ('-') */
+  uint32_t ref;        /* bits 0..29 query index; bit 30 = the query and this record's literal
+                          bytes are all A/C/G/T; bit 31 = reverse strand ('-') */
   int32_t offset;      /* start on the aligned-strand query (pafreport.cpp:486-490) */
   int32_t t_len;       /* tseq length implied by the cs string */
   uint64_t ev_begin;   /* first event slot of this record (prefix of pw_cs_totals.n_events_max) */
 } pw_aln_desc;
 #define PW_REF_REVERSE 0x80000000u
+#define PW_REF_ACGT 0x40000000u
+#define PW_REF_QMASK 0x3FFFFFFFu
 
 /* Text pages.  The event lines of 64 consecutive event slots (one chunk) form one page, written
  * at text[page.off, page.off + page.len).  A page normally lives at chunk * PW_PAGE_BYTES; a
@@ -147,7 +150,7 @@ typedef struct pw_msa_args {
   const int32_t* clip_l;    /* [n_rows] oriented left clip */
   const int32_t* clip_r;    /* [n_rows] oriented right clip */
   const int64_t* slot_base; /* [n_rows + 1] from pw_msa_slots */
-  int32_t* scratch;         /* [2 * n_slots] */
+  int32_t* scratch;         /* [3 * n_slots] (chunk sums, checkpoints, slot -> row) */
   int32_t* counts;          /* [n_cols][6] A,C,G,T,N,- (GAlnColumn::counts order) */
   uint8_t* consensus;       /* [n_cols] bestChar() per column ('-' for gap), 0 = no coverage */
   int32_t* minmax;          /* [4]: mincol, maxcol, first out-of-range row, first zero column */

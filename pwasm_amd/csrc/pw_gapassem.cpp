@@ -130,7 +130,7 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
   const uint64_t ntg = pw_msa_refine_tiles(ncols);
   bool ok = d_seq.alloc(seq.size()) && d_ofs.alloc(ofs.size()) && d_roff.alloc(nrows) && d_len.alloc(nrows) &&
             d_col0.alloc(nrows) && d_cl.alloc(nrows) && d_cr.alloc(nrows) && d_slot.alloc(nrows + 1) &&
-            d_scr.alloc(2 * nslots) && d_cnt.alloc((size_t)ncols * 6) && d_cons.alloc((size_t)ncols) && d_mm.alloc(4) &&
+            d_scr.alloc(3 * nslots) && d_cnt.alloc((size_t)ncols * 6) && d_cons.alloc((size_t)ncols) && d_mm.alloc(4) &&
             d_gp.alloc((size_t)ncols) && d_tg.alloc(ntg) && d_clen.alloc(1) && d_cout.alloc((size_t)ncols) &&
             (!remove_gaps || (d_roffs.alloc(nrows) && d_offo.alloc(nrows) && d_ngo.alloc(nrows) && d_ofso.alloc(ofs.size())));
   if (!ok) {

@@ -193,6 +193,19 @@ struct QueryDb {
   std::vector<int32_t> len;
   std::vector<uint8_t> seq;  // upper case (GASeq::allupper, pafreport.cpp:350)
   std::unordered_map<std::string, int> index;
+  std::vector<uint8_t> acgt;  // per query: all bases in {A,C,G,T}
+  bool all_acgt(int qi) const { return acgt[qi] != 0; }
+  static bool is_acgt_byte(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
+  // Each sequence starts 16-byte aligned and is followed by >= 64 zero bytes: the kernels'
+  // 16-byte-aligned LDS windows then read NUL past the end of a query, as the reference reads
+  // the string terminator (never the next query's bases).
+  void close_record() {
+    len.back() = (int32_t)(seq.size() - off.back());
+    bool ok = true;
+    for (size_t i = off.back(); i < seq.size() && ok; i++) ok = is_acgt_byte(seq[i]);
+    acgt.push_back(ok ? 1 : 0);
+    seq.resize((seq.size() + 15) / 16 * 16 + 64, 0);
+  }
   bool load(const char* path, std::string& err) {
     FILE* f = fopen(path, "rb");
     if (!f) {
@@ -207,7 +220,7 @@ struct QueryDb {
         size_t e = 1;
         while (e < l.size() && !isspace((unsigned char)l[e])) e++;
         std::string id = l.substr(1, e - 1);
-        if (have) len.back() = (int32_t)(seq.size() - off.back());
+        if (have) close_record();
         ids.push_back(id);
         off.push_back(seq.size());
         len.push_back(0);
@@ -227,7 +240,7 @@ struct QueryDb {
       }
     }
     if (!line.empty()) flush_line(line);
-    if (have) len.back() = (int32_t)(seq.size() - off.back());
+    if (have) close_record();
     fclose(f);
     return true;
   }
@@ -410,6 +423,10 @@ struct Packer {
       b.lits.resize(d.lit_begin + tot.n_lits);
       d.n_ops = tot.n_ops;
       d.t_len = tot.t_total;
+      // fast-path flag for the kernels: the query and this record's literal bytes are A/C/G/T
+      bool acgt = rc == PW_CS_OK && qdb->all_acgt((int)qi);
+      for (uint32_t i = 0; i < tot.n_lits && acgt; i++) acgt = QueryDb::is_acgt_byte(b.lits[d.lit_begin + i]);
+      if (acgt) d.ref |= PW_REF_ACGT;
       b.text_total += tot.text_bound;
       b.n_events_max += tot.n_events_max;
       if (rc != PW_CS_OK) {
@@ -822,7 +839,7 @@ uint64_t alg_bytes(const Batch& b, const QueryDb& q, bool skip_codan) {
                b.lits.size();
   std::vector<char> seen(q.len.size(), 0);
   for (const auto& d : b.desc) {
-    uint32_t qi = d.ref & 0x7FFFFFFFu;
+    uint32_t qi = d.ref & PW_REF_QMASK;
     if (!seen[qi]) {
       seen[qi] = 1;
       v += (uint64_t)q.len[qi] * (skip_codan ? 1u : 5u);

@@ -7,14 +7,16 @@
 //   GSeqAlign::buildMSA     GapAssem.cpp:1088-1106
 // The reference scatters row by row (one NucOri allocation per base).  Here the layout is
 // read once, column tile by column tile:
+//   K0 slot_rows:      row of every chunk slot (no per-chunk binary search later)
 //   K1 row_chunk_sums: per 256-base chunk of a row, sum of (1 + max(ofs,0))   (1 wave / chunk)
 //   K2 row_prefix:     per row, exclusive scan of the chunk sums -> layout column at which each
 //                      chunk's first gap run starts (checkpoints), row end column, bounds check
-//   K3 tile_counts:    one 256-thread workgroup per 2048-column tile keeps the tile's 6 x 2048
-//                      counters in LDS; its 4 waves walk the chunks of every row that overlaps
-//                      the tile (binary search on the checkpoints), re-derive columns with a
-//                      wave scan and add into LDS; then the tile writes counts + bestChar
-//                      coalesced and folds mincol / maxcol.
+//   K3 tile_counts:    one 1024-thread workgroup per 2048-column tile keeps the tile's 6 x 2048
+//                      counters in LDS; its 16 waves walk the chunks of every row that overlaps
+//                      the tile (first chunk interpolated from the checkpoints; the next chunk
+//                      loads while one is scanned), re-derive columns with a wave scan and add
+//                      into LDS; then the tile writes its counts coalesced and folds mincol /
+//                      maxcol.
 //                      (pw_msa_count stops here: with rows sharded over GPUs the partial
 //                      counts are summed by an all-reduce before the call)
 //   K4 call_columns:   bestChar of every column (pw_msa_call)
@@ -62,21 +64,20 @@ __device__ __forceinline__ int bin_of(uint8_t c) {
   }
 }
 
+// K0: the row of every slot (slot_row), one workgroup per row, coalesced
+__global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row) {
+  for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x)
+    for (int64_t k = A.slot_base[r] + threadIdx.x; k < A.slot_base[r + 1]; k += 256) slot_row[k] = (int32_t)r;
+}
+
 // per row: number of chunks = ceil(len / 256); chunk index space = prefix over rows
-__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum) {
+__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const int32_t* slot_row) {
   const int64_t* chunk_base = A.slot_base;
   const uint64_t n_chunks = A.n_slots;
   const int lane = threadIdx.x & 63;
   const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   for (uint64_t c = wid; c < n_chunks; c += (uint64_t)gridDim.x * 4) {
-    // find the row of chunk c (binary search in chunk_base[0..n_rows])
-    uint32_t lo = 0, hi = A.n_rows;
-    while (hi - lo > 1) {
-      uint32_t mid = (lo + hi) >> 1;
-      if ((uint64_t)chunk_base[mid] <= c) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t r = lo;
+    const uint32_t r = (uint32_t)slot_row[c];
     const int64_t k = (int64_t)c - chunk_base[r];
     const int len = A.row_len[r];
     const int64_t i0 = k * kChunk;
@@ -124,41 +125,64 @@ __global__ __launch_bounds__(64) void row_prefix(const pw_msa_args A, const int3
   }
 }
 
-// counts for one column tile
-__global__ __launch_bounds__(256) void tile_counts(const pw_msa_args A, const int32_t* ckpt) {
+// counts for one column tile: 16 waves, each walks the chunks of its rows that overlap the
+// tile; the next chunk's bases / gaps are loaded while the current one is scanned
+constexpr int kTileWaves = 16;
+__global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args A, const int32_t* ckpt) {
   const int64_t* chunk_base = A.slot_base;
   __shared__ int32_t cnt[6][kTileW];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * kTileW;
   const int c1 = min(c0 + kTileW, A.n_cols);
-  for (int i = tid; i < 6 * kTileW; i += 256) (&cnt[0][0])[i] = 0;
+  for (int i = tid; i < 6 * kTileW; i += 64 * kTileWaves) (&cnt[0][0])[i] = 0;
   __syncthreads();
   int my_min = INT_MAX, my_max = -1;
-  for (uint32_t r = wv; r < A.n_rows; r += 4) {
+  for (uint32_t r = wv; r < A.n_rows; r += kTileWaves) {
     const int64_t b = chunk_base[r], e = chunk_base[r + 1] - 1;  // [b, e) chunks, e = end slot
     if (b == e) continue;
     const int rs = ckpt[b], re = ckpt[e];  // row columns [rs, re)
     if (re <= c0 || rs >= c1) continue;
     const int len = A.row_len[r];
     const int cl = A.clip_l[r], cr = A.clip_r[r];
-    // first chunk whose columns reach c0: last k with ckpt[k] <= c0
-    int64_t lo = b, hi = e;
-    while (hi - lo > 1) {
-      int64_t mid = (lo + hi) >> 1;
-      if (ckpt[mid] <= c0) lo = mid;
-      else hi = mid;
+    // first chunk whose columns reach c0 (last k with ckpt[k] <= c0): interpolate, then step
+    int64_t k = b;
+    if (c0 > rs) {
+      k = b + (int64_t)((double)(c0 - rs) * (double)(e - b) / (double)(re - rs));
+      if (k > e - 1) k = e - 1;
+      while (k > b && ckpt[k] > c0) k--;
+      while (k + 1 < e && ckpt[k + 1] <= c0) k++;
     }
     const uint64_t roff = A.row_off[r];
-    for (int64_t k = lo; k < e && ckpt[k] < c1; k++) {
+    int col = ckpt[k];
+    int16_t g_nx[kChunk / 64];
+    uint8_t s_nx[kChunk / 64];
+    auto load = [&](int64_t kk) {
+      const int64_t ib = (kk - b) * kChunk;
+#pragma unroll
+      for (int j = 0; j < kChunk / 64; j++) {
+        const int64_t i = ib + j * 64 + lane;
+        g_nx[j] = i < len ? A.ofs[roff + i] : (int16_t)0;
+        s_nx[j] = i < len ? A.seq[roff + i] : (uint8_t)0;
+      }
+    };
+    load(k);
+    for (; k < e && col < c1; k++) {
+      int16_t gg[kChunk / 64];
+      uint8_t ss[kChunk / 64];
+#pragma unroll
+      for (int j = 0; j < kChunk / 64; j++) {
+        gg[j] = g_nx[j];
+        ss[j] = s_nx[j];
+      }
+      if (k + 1 < e) load(k + 1);
       const int64_t ib = (k - b) * kChunk;
-      int col = ckpt[k];
 #pragma unroll
       for (int j = 0; j < kChunk / 64; j++) {
         const int64_t i = ib + j * 64 + lane;
         const bool ok = i < len;
-        const int g0 = ok ? A.ofs[roff + i] : 0;
+        const int g0 = gg[j];
         const int g = g0 > 0 ? g0 : 0;
-        const uint8_t ch = ok ? A.seq[roff + i] : 0;
+        const uint8_t ch = ss[j];
         const int adv = ok ? 1 + g : 0;
         int incl = adv;
 #pragma unroll
@@ -194,7 +218,7 @@ __global__ __launch_bounds__(256) void tile_counts(const pw_msa_args A, const in
   __syncthreads();
   // the tile's counters, coalesced: column-major in LDS -> [col][6] rows in memory
   int32_t* dst = A.counts + (int64_t)c0 * 6;
-  for (int i = tid; i < (c1 - c0) * 6; i += 256) dst[i] = cnt[i % 6][i / 6];
+  for (int i = tid; i < (c1 - c0) * 6; i += 64 * kTileWaves) dst[i] = cnt[i % 6][i / 6];
 }
 
 // bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage
@@ -301,18 +325,13 @@ __device__ __forceinline__ int gx(const pw_msa_refine_args& R, int n_cols, int c
 }
 
 // K8: ofs' of every base, one wave per 256-base chunk (columns re-derived as in K3)
-__global__ __launch_bounds__(256) void row_edit(const pw_msa_args A, pw_msa_refine_args R, const int32_t* ckpt) {
+__global__ __launch_bounds__(256) void row_edit(const pw_msa_args A, pw_msa_refine_args R, const int32_t* ckpt,
+                                                const int32_t* slot_row) {
   const int64_t* chunk_base = A.slot_base;
   const int lane = threadIdx.x & 63;
   const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   for (uint64_t c = wid; c < A.n_slots; c += (uint64_t)gridDim.x * 4) {
-    uint32_t lo = 0, hi = A.n_rows;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if ((uint64_t)chunk_base[mid] <= c) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t r = lo;
+    const uint32_t r = (uint32_t)slot_row[c];
     const int64_t k = (int64_t)c - chunk_base[r];
     const int len = A.row_len[r];
     const int64_t ib = k * kChunk;
@@ -399,14 +418,16 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
+  int32_t* slot_row = a->scratch + 2 * a->n_slots;
   static const int32_t init[4] = {INT_MAX, -1, INT_MAX, INT_MAX};
   if (hipMemcpyAsync(a->minmax, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return PW_E_HIP;
+  hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row);
   const uint64_t nb1 = (a->n_slots + 3) / 4;
   hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 65536 ? nb1 : 65536)), dim3(256), 0, s, *a,
-                     chunk_sum);
+                     chunk_sum, slot_row);
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, chunk_sum, ckpt);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kTileW - 1) / pw::kTileW);
-  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(256), 0, s, *a, ckpt);
+  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kTileWaves), 0, s, *a, ckpt);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
@@ -436,8 +457,10 @@ extern "C" int pw_msa_refine(const pw_msa_args* a, const pw_msa_refine_args* r, 
   hipLaunchKernelGGL(pw::gap_scan, dim3(ntiles), dim3(256), 0, s, *a, *r);
   if (r->remove_gaps) {
     const int32_t* ckpt = a->scratch + a->n_slots;  // from pw_msa_count
+    const int32_t* slot_row = a->scratch + 2 * a->n_slots;
     const uint64_t nb = (a->n_slots + 3) / 4;
-    hipLaunchKernelGGL(pw::row_edit, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, *a, *r, ckpt);
+    hipLaunchKernelGGL(pw::row_edit, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, s, *a, *r, ckpt,
+                       slot_row);
     hipLaunchKernelGGL(pw::row_finish, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, *r);
   }
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;

@@ -61,7 +61,8 @@ constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
 constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, failed records)
-constexpr uint32_t kNBig = (1u << 20) - 1;  // evtbases length field saturates here
+constexpr uint32_t kNBig = (1u << 19) - 1;  // evtbases length field saturates here
+constexpr uint32_t kFnAcgt = 1u << 19;      // query + record literals all A/C/G/T (PW_REF_ACGT)
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
 #ifndef PW_INDEX_OCC
@@ -76,7 +77,8 @@ constexpr int kTx = 32;         // pre-rendered target-context record (length by
 
 // Render record of one event (index_kernel -> render_kernel), 32 bytes.
 //   fn: type (31-30) | reverse (29) | fast tctx (28) | first line of its record (27) |
-//       last line (26) | ll (25-23) | rl (22-20) | evtbases length (19-0, saturated)
+//       last line (26) | ll (25-23) | rl (22-20) | A/C/G/T only (19) | evtbases length (18-0,
+//       saturated)
 //   l0, l1: the event's first 8 literal bytes (SUB: target,query pairs; INS: inserted bases)
 struct Hot {
   uint32_t qb;    // forward query start in qseq
@@ -93,9 +95,10 @@ struct Cold {
   int32_t qs, ts;  // query / target position at the head op
 };
 __device__ __forceinline__ uint32_t hot_fn(uint32_t typ, bool rev, bool fast, bool first, bool last, int ll, int rl,
-                                           uint32_t n) {
+                                           bool acgt, uint32_t n) {
   return typ << 30 | (rev ? 1u << 29 : 0u) | (fast ? 1u << 28 : 0u) | (first ? 1u << 27 : 0u) |
-         (last ? 1u << 26 : 0u) | (uint32_t)(ll & 7) << 23 | (uint32_t)(rl & 7) << 20 | (n < kNBig ? n : kNBig);
+         (last ? 1u << 26 : 0u) | (uint32_t)(ll & 7) << 23 | (uint32_t)(rl & 7) << 20 | (acgt ? kFnAcgt : 0u) |
+         (n < kNBig ? n : kNBig);
 }
 
 // Byte tables read per event (LDS copy per workgroup).  The IUPAC code / 4096-entry codon
@@ -147,6 +150,7 @@ struct Rec {
   int T;                    // tseq length
   uint32_t n_ops;
   bool rev;
+  bool acgt;                // query and the record's literals are all A/C/G/T (register fast paths)
 };
 
 // Query byte x of the forward query, 0 outside [0, L) (the NUL / missing bytes).  The LDS
@@ -444,6 +448,102 @@ __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, 
   maa = translate(r.tab, m[0], m[1], m[2]);
 }
 
+// ---- 16-byte register images of query / modified-sequence bytes (indel fast path)
+typedef unsigned __int128 u128;
+// bytes qw[off, off + 16) of an LDS window (off >= 0; up to 4 bytes past off + 16 are read)
+__device__ __forceinline__ u128 lds16(const LDS uint8_t* qw, int off) {
+  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
+  const uint32_t sh = (uint32_t)off & 3u;
+  uint32_t d[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) d[i] = p[i];
+  u128 v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) v |= (u128)__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) << (32 * i);
+  return v;
+}
+__device__ __forceinline__ u128 low_bytes(int n) {  // bytes [0, n) set, 0 <= n <= 15
+  return n <= 0 ? (u128)0 : (((u128)1 << (8 * n)) - 1);
+}
+__device__ __forceinline__ uint32_t byte_at(u128 v, int p) { return (uint32_t)(v >> (8 * p)) & 0xFFu; }
+// every byte of v in [0, 15) is one of A, C, G, T (upper case: query and literals are)
+__device__ __forceinline__ bool acgt15(u128 v) {
+  bool ok = true;
+#pragma unroll
+  for (int p = 0; p < 15; p++) ok = ok && is_acgt(byte_at(v, p));
+  return ok;
+}
+// translateCodon of the codon at byte p of v (all ACGT): 2-bit codes, one codon64 lookup
+__device__ __forceinline__ uint8_t codon_at(const LDS SmallTables* t, u128 v, int p) {
+  const uint32_t c0 = (byte_at(v, p) >> 1) & 3u, c1 = (byte_at(v, p + 1) >> 1) & 3u, c2 = (byte_at(v, p + 2) >> 1) & 3u;
+  return t->codon64[c0 << 4 | c1 << 2 | c2];
+}
+// complement of A/C/G/T bytes (A<->T: ^0x15, C<->G: ^0x04; bit 1 tells them apart).  Maps no
+// other byte onto A/C/G/T, so a validity check after it still rejects non-ACGT input.
+__device__ __forceinline__ uint64_t comp_acgt8(uint64_t v) {
+  const uint64_t t = (v >> 1) & 0x0101010101010101ull;
+  return v ^ (t * 0x04ull | (t ^ 0x0101010101010101ull) * 0x15ull);
+}
+
+// The five codons of modseq and the four reference codons after the first (predictImpact's
+// scan, pafreport.cpp:854-870) from register images when the event's neighbourhood is in the
+// LDS window, inside the query and all A/C/G/T (the common case; anything else -> false and
+// the byte-wise path).  m(p) = Q[r_trloc + p] (p < a), X[p - a] (a <= p < a + x),
+// Q[r_trloc + p + dl - x] (after the event).
+__device__ __forceinline__ bool indel_codons_fast(const Rec& r, const Event& e, int a, int x, int dl, uint8_t (&mm)[5],
+                                                  uint8_t (&rr)[5]) {
+  if (!r.acgt || r.qn != kQWin || x > 8 || a + x > 15) return false;
+  if (x > 0 && (r.ln != 8 || e.ls != r.ls0)) return false;  // inserted bases not in registers
+  const int o0 = e.r_trloc - r.qlo, o1 = o0 + dl - x;
+  if (o0 < 0 || o1 < 0 || o0 + 16 > kQWin || o1 + 16 > kQWin) return false;
+  const u128 q0 = lds16(r.qw, o0), q1 = lds16(r.qw, o1);
+  u128 xs = 0;
+  if (x > 0) {
+    const uint64_t l64 = (uint64_t)r.lit1 << 32 | r.lit0;
+    uint64_t xv = r.rev ? comp_acgt8(__builtin_bswap64(l64) >> (8 * (8 - x))) : l64;
+    if (x < 8) xv &= (1ull << (8 * x)) - 1ull;
+    xs = (u128)xv << (8 * a);
+  }
+  const u128 ma = low_bytes(a), mx = low_bytes(a + x) & ~ma;
+  const u128 m = (q0 & ma) | (xs & mx) | (q1 & ~(ma | mx));
+  // (bytes past the query end are the zero padding: they only reach codons the scan does not
+  // use, 3c + 2 >= |modseq| or >= |r_trseq|)
+#pragma unroll
+  for (int c = 0; c < 5; c++) {
+    mm[c] = codon_at(r.tab, m, 3 * c);
+    rr[c] = c == 0 ? 0 : codon_at(r.tab, q0, 3 * c);
+  }
+  return true;
+}
+
+// S run of n <= 4 (predictImpact's substitution branch, pafreport.cpp:806-838) from register
+// images: q0 = Q[r_trloc, +16), m = q0 with evtbases at [p0, p0 + n); the modseq check
+// (:811-814) compares q0 with evtsub.  false -> the byte-wise path.
+__device__ __forceinline__ uint32_t pack_even4(uint64_t v) {  // bytes 0, 2, 4, 6 of v
+  return (uint32_t)(v & 0xFFu) | (uint32_t)((v >> 8) & 0xFF00u) | (uint32_t)((v >> 16) & 0xFF0000u) |
+         (uint32_t)((v >> 24) & 0xFF000000u);
+}
+__device__ __forceinline__ bool sub_image(const Rec& r, const Event& e, int p0, u128& q0, u128& m, int& modseq_err) {
+  // (codons up to byte 8 of q0 are read: all inside the query, none reaches the NUL)
+  if (!r.acgt || r.qn != kQWin || e.n > 4 || r.ln != 8 || e.ls != r.ls0 || e.r_trloc + 9 > r.L) return false;
+  const int o0 = e.r_trloc - r.qlo;
+  if (o0 < 0 || o0 + 16 > kQWin) return false;
+  q0 = lds16(r.qw, o0);
+  const uint64_t l64 = (uint64_t)r.lit1 << 32 | r.lit0;  // (target, query) pairs
+  uint32_t alt = pack_even4(l64), sub = pack_even4(l64 >> 8);
+  const int n = e.n;
+  if (r.rev) {  // evtbases / evtsub reversed and complemented (pafreport.cpp:636-637)
+    alt = (uint32_t)comp_acgt8(__builtin_bswap32(alt) >> (8 * (4 - n)));
+    sub = (uint32_t)comp_acgt8(__builtin_bswap32(sub) >> (8 * (4 - n)));
+  }
+  const uint32_t nm = n == 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+  const u128 place = (u128)nm << (8 * p0);
+  m = (q0 & ~place) | ((u128)(alt & nm) << (8 * p0));
+  const uint32_t diff = ((uint32_t)(q0 >> (8 * p0)) ^ sub) & nm;
+  modseq_err = diff ? (int)(__builtin_ctz(diff) >> 3) : -1;
+  return true;
+}
+
 // Indel consequence: predictImpact insert/cut + stop scan (pafreport.cpp:843-882), written to
 // the sink.  modseq = Q[r_trloc, rloc) + X + Q[s, L) with X the inserted bases (I) or nothing
 // (D; s = rloc + len).  Codons touching the prefix / X / the first five codons are translated
@@ -464,21 +564,23 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
     // the reference scans codons i = 0,3,..,12 (while i+2 < M), stopping at the first stop;
     // here all five codons and the four reference codons are read and translated at once
     // (independent reads, no loop-carried latency) and the scan is replayed on the results
-    uint8_t m[15];
-#pragma unroll
-    for (int p = 0; p < 15; p++) {
-      const uint8_t q = Rc(r, p < a ? e.r_trloc + p : sfx + p - a - x);
-      const int ii = p - a;
-      const uint32_t li = e.ls + (uint32_t)(r.rev ? x - 1 - ii : ii);
-      const uint8_t ib = (ii >= 0 && ii < x) ? litb(r, li) : (uint8_t)0;
-      m[p] = (ii >= 0 && ii < x) ? (r.rev ? r.tab->comp[ib] : ib) : q;
-    }
     uint8_t mm[5], rr[5];
+    if (!indel_codons_fast(r, e, a, x, dl, mm, rr)) {
+      uint8_t m[15];
 #pragma unroll
-    for (int c = 0; c < 5; c++) {
-      mm[c] = translate(r.tab, m[3 * c], m[3 * c + 1], m[3 * c + 2]);
-      rr[c] = c == 0 ? 0 : translate(r.tab, Rc(r, e.r_trloc + 3 * c), Rc(r, e.r_trloc + 3 * c + 1),
-                                     Rc(r, e.r_trloc + 3 * c + 2));
+      for (int p = 0; p < 15; p++) {
+        const uint8_t q = Rc(r, p < a ? e.r_trloc + p : sfx + p - a - x);
+        const int ii = p - a;
+        const uint32_t li = e.ls + (uint32_t)(r.rev ? x - 1 - ii : ii);
+        const uint8_t ib = (ii >= 0 && ii < x) ? litb(r, li) : (uint8_t)0;
+        m[p] = (ii >= 0 && ii < x) ? (r.rev ? r.tab->comp[ib] : ib) : q;
+      }
+#pragma unroll
+      for (int c = 0; c < 5; c++) {
+        mm[c] = translate(r.tab, m[3 * c], m[3 * c + 1], m[3 * c + 2]);
+        rr[c] = c == 0 ? 0 : translate(r.tab, Rc(r, e.r_trloc + 3 * c), Rc(r, e.r_trloc + 3 * c + 1),
+                                       Rc(r, e.r_trloc + 3 * c + 2));
+      }
     }
     int stopc = 5, nvalid = 0;
 #pragma unroll
@@ -582,6 +684,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   rel = e.rloc - e.r_trloc;
 
   // ---- "E\trloc\taapos(aa)\t"
+  if (!(PW_ABL & 256)) {
   k.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
   k.put('\t');
   wr_dig(k, (uint32_t)(e.rloc + 1));
@@ -591,8 +694,12 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   k.put(aa);
   k.put(')');
   k.put('\t');
+  }
   // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity
   const bool big = e.n > kMaxEv;
+  const uint8_t b0 = ev_base(r, e, 0);
+  bool same = true;
+  if (!(PW_ABL & 512)) {
   if (typ == PW_OP_SUB) {
     if (big) {
       k.put('[');
@@ -603,8 +710,6 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     }
   }
   if (typ != PW_OP_DEL) k.put(':');
-  const uint8_t b0 = ev_base(r, e, 0);
-  bool same = true;
   if (big) {
     k.put('[');
     wr_dig(k, (uint32_t)e.n);
@@ -618,11 +723,13 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     }
   }
   if (typ == PW_OP_DEL) k.put(':');
+  }
   k.put('\t');
   wr_dig(k, (uint32_t)(in.tloc + 1));
   k.put('\t');
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
-  if (in.tmode == 0) {
+  if (PW_ABL & 1024) {
+  } else if (in.tmode == 0) {
     emit_tctx_fast(k, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
   } else if (in.tmode == 1) {
     const int tl = in.tx[0];
@@ -642,6 +749,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   }
   if (c0 < 0) c0 = 0;  // L < 9 is reported by the host
   uint32_t rw0 = 0, rw1 = 0;
+  if (!(PW_ABL & 2048)) {
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const uint8_t c = Rc(r, c0 + q);
@@ -679,18 +787,27 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
 #pragma unroll
     for (int q = 0; q < 11; q++) k.put_if(q < sl, sw[q]);
   }
+  }
   k.put('\t');
   // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
   int modseq_err = -1;
   if (!skip) {
     if (typ == PW_OP_SUB) {
-      for (int i = 0; i < e.n; i++)
-        if (modseq_err < 0 && to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, e, i))) modseq_err = i;
       const int p0 = e.rloc - e.r_trloc;
+      u128 q0 = 0, mi = 0;
+      const bool fs = sub_image(r, e, p0, q0, mi, modseq_err);
+      if (!fs)
+        for (int i = 0; i < e.n; i++)
+          if (modseq_err < 0 && to_upper(Rc(r, e.rloc + i)) != to_upper(ev_sub(r, e, i))) modseq_err = i;
       bool any = false;
       for (int ao = p0 / 3; ao <= (p0 + e.n - 1) / 3; ao++) {
         uint8_t caa, cmaa;
-        sub_codon(r, e, ao, caa, cmaa);
+        if (fs) {
+          caa = codon_at(r.tab, q0, 3 * ao);
+          cmaa = codon_at(r.tab, mi, 3 * ao);
+        } else {
+          sub_codon(r, e, ao, caa, cmaa);
+        }
         if (caa != cmaa) {
           if (any) wr_lit(k, ", ");
           wr_lit(k, "AA");
@@ -813,7 +930,7 @@ struct RecPre {
 __device__ __forceinline__ void rec_pre(const pw_report_args& A, uint32_t ai, const pw_aln_desc& d, int lane,
                                         RecPre& p) {
   p.d = d;
-  const uint32_t qi = d.ref & 0x7FFFFFFFu;
+  const uint32_t qi = d.ref & PW_REF_QMASK;
   p.qb = A.qoff[qi];
   p.L = A.qlen[qi];
   p.ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
@@ -981,7 +1098,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           hh.qp = d.offset + qs[k];
           hh.tloc = rev ? T - ts[k] : ts[k];
           hh.ls = ls[k];
-          hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, n);
+          hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, (d.ref & PW_REF_ACGT) != 0, n);
           hh.l0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
           hh.l1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
           W.hot[s] = hh;
@@ -1140,6 +1257,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       r.ls0 = h.ls;
       r.ln = 8;
       r.rev = rev;
+      r.acgt = (h.fn & kFnAcgt) != 0;
       r.offset = 0;
       r.T = 0;
       r.qn = 0;
@@ -1391,6 +1509,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         r.T = (int)p1.y;
         r.n_ops = p0.z;
         r.rev = (h.fn >> 29) & 1u;
+        r.acgt = false;
         // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
         // and forward query bytes around the event are staged in LDS
         r.lit0 = h.l0;
@@ -1467,7 +1586,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     const Hot h = W.hot[f.s];
     const Cold cd = W.cold[f.s];
     const pw_aln_desc d = A.desc[cd.ai];
-    const uint32_t qi = d.ref & 0x7FFFFFFFu;
+    const uint32_t qi = d.ref & PW_REF_QMASK;
     Rec r;
     r.ops = A.ops + d.op_begin;
     r.lits = A.lits;
@@ -1491,6 +1610,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     r.T = d.t_len;
     r.n_ops = d.n_ops;
     r.rev = (d.ref & PW_REF_REVERSE) != 0;
+    r.acgt = false;
     const uint32_t wd = r.ops[cd.j];
     EvIn in;
     in.typ = wd >> 30;

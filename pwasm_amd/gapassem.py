@@ -124,7 +124,7 @@ class HipEngine:
             return torch.empty(max(int(n), 1), dtype=dt, device=dev)
 
         d = {"seq": t(seq), "ofs": t(ofs), "row_off": t(row_off), "len": t(lens), "col0": t(col0), "cl": t(cl),
-             "cr": t(cr), "slot": t(slot_base), "scr": e(2 * nslots, torch.int32),
+             "cr": t(cr), "slot": t(slot_base), "scr": e(3 * nslots, torch.int32),
              "counts": e(ncols * 6, torch.int32), "cons": e(ncols, torch.uint8), "mm": e(4, torch.int32),
              "gp": e(ncols, torch.int32), "tg": e(self.lib.pw_msa_refine_tiles(ncols), torch.int32),
              "cout": e(ncols, torch.uint8), "clen": e(1, torch.int32),

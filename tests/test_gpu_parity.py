@@ -325,3 +325,39 @@ def test_gapassem_sharded_on_gpu(built, tmp_path):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == _ga_cli(lay, tmp_path, True)
+
+
+# ---------------------------------------------------------------- reads past the query end
+def _comp(s):
+    return s.translate(str.maketrans("ACGT", "TGCA"))[::-1]
+
+
+def query_end_case(tmp_path):
+    """Events in the last, partial codon of a query that is followed by another query in the
+    FASTA: the codon reads run past the end (the reference reads the NUL terminator; DESIGN.md
+    D6), never into the next query's bases."""
+    qa = "ATGAAACCCGGGTTTAAACCCGGGTTTAAACG"  # 32 nt: the last codon is partial
+    qb = "GGGGGGGGGGGGGGGGGGGGGGGG"
+    fa = tmp_path / "q.fa"
+    fa.write_text(f">qa\n{qa}\n>qb\n{qb}\n")
+    alt = lambda c: "t" if c != "T" else "c"  # noqa: E731
+    rc_qa = _comp(qa)
+    recs = [
+        ("qa", 32, 0, 32, "+", "t1", 100, 10, 42, "32M", f":31*{alt(qa[31])}{qa[31].lower()}"),
+        ("qa", 32, 0, 32, "+", "t2", 100, 10, 40, "29M2I1M", f":29+{qa[29:31].lower()}:1"),
+        ("qa", 32, 0, 32, "-", "t3", 100, 5, 37, "32M", f":1*{alt(rc_qa[1])}{rc_qa[1].lower()}:30"),
+        ("qa", 32, 0, 32, "+", "t4", 100, 10, 43, "31M1D1M", f":31-a:1"),
+    ]
+    lines = []
+    for q, ql, qs, qe, st, t, tl, ts, te, cg, cs in recs:
+        lines.append("\t".join(map(str, [q, ql, qs, qe, st, t, tl, ts, te, 30, 32, 60, "NM:i:1", "AS:i:9",
+                                         f"cg:Z:{cg}", f"cs:Z:{cs}"])) + "\n")
+    paf = tmp_path / "e.paf"
+    paf.write_text("".join(lines))
+    return str(fa), str(paf)
+
+
+def test_reads_past_query_end(built, tmp_path):
+    fa, paf = query_end_case(tmp_path)
+    out = same(["-G", "-C", "-r", fa, paf])
+    assert out.count(b">") == 4 and b"(X)" in out
