@@ -249,8 +249,28 @@ __device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
 
 // ------------------------------------------------------------------ line sinks
 // LineSink writes into the lane's LDS line buffer; a store past the buffer or a masked-off
-// character goes to the lane's junk byte (no branch).  GlobalSink writes straight to global
-// memory (fixup_kernel lines, index_kernel target contexts).
+// character goes to the lane's junk byte (no branch).  A field is written through block(room,
+// f): when `room` bytes are left it gets a RawSink — no per-character bounds check, a masked
+// character is stored anyway and then overwritten, and runs of characters fold into the
+// immediate offsets of the byte stores.  GlobalSink writes straight to global memory
+// (fixup_kernel lines).
+struct RawSink {
+  LDS uint8_t* buf;
+  int pos;
+  __device__ __forceinline__ void put(uint8_t c) {
+    buf[pos] = c;
+    pos++;
+  }
+  __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
+    buf[pos] = c;
+    pos += pred ? 1 : 0;
+  }
+  __device__ __forceinline__ void put_at(int i, uint8_t c) { buf[i] = c; }
+  template <class F>
+  __device__ __forceinline__ void block(int, F&& f) {
+    f(*this);
+  }
+};
 template <int CAP>
 struct LdsSink {
   LDS uint8_t* buf;
@@ -265,6 +285,16 @@ struct LdsSink {
     pos += pred ? 1 : 0;
   }
   __device__ __forceinline__ void put_at(int i, uint8_t c) { *(i < CAP ? buf + i : junk) = c; }
+  template <class F>
+  __device__ __forceinline__ void block(int room, F&& f) {
+    if (pos + room <= CAP) {
+      RawSink u{buf, pos};
+      f(u);
+      pos = u.pos;
+    } else {
+      f(*this);
+    }
+  }
 };
 typedef LdsSink<kLine> LineSink;
 struct GlobalSink {
@@ -275,6 +305,10 @@ struct GlobalSink {
     if (pred) p[pos++] = c;
   }
   __device__ __forceinline__ void put_at(int i, uint8_t c) { p[i] = c; }
+  template <class F>
+  __device__ __forceinline__ void block(int, F&& f) {
+    f(*this);
+  }
 };
 
 // Write tseq[p0, p1) (the target segment, pafreport.cpp:543,575,588 — never materialised) to
@@ -645,17 +679,21 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
     }
   }
   if (stop_i >= 0) {
-    wr_lit(k, "premature stop at AA");
-    wr_dig(k, (uint32_t)(1 + (stop_i + e.r_trloc) / 3));
+    k.block(30, [&](auto& o) {
+      wr_lit(o, "premature stop at AA");
+      wr_dig(o, (uint32_t)(1 + (stop_i + e.r_trloc) / 3));
+    });
   } else if (aa4n > 0 && maa4n > 0) {
-    wr_lit(k, "frame shift ");
+    k.block(23, [&](auto& o) {
+      wr_lit(o, "frame shift ");
 #pragma unroll
-    for (int q = 0; q < 4; q++) k.put_if(q < aa4n, (uint8_t)(aa4 >> (8 * q)));
-    k.put('+');
-    k.put(':');
+      for (int q = 0; q < 4; q++) o.put_if(q < aa4n, (uint8_t)(aa4 >> (8 * q)));
+      o.put('+');
+      o.put(':');
 #pragma unroll
-    for (int q = 0; q < 4; q++) k.put_if(q < maa4n, (uint8_t)(maa4 >> (8 * q)));
-    k.put('+');
+      for (int q = 0; q < 4; q++) o.put_if(q < maa4n, (uint8_t)(maa4 >> (8 * q)));
+      o.put('+');
+    });
   }
 }
 
@@ -684,58 +722,66 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   rel = e.rloc - e.r_trloc;
 
   // ---- "E\trloc\taapos(aa)\t"
-  if (!(PW_ABL & 256)) {
-  k.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
-  k.put('\t');
-  wr_dig(k, (uint32_t)(e.rloc + 1));
-  k.put('\t');
-  wr_dig(k, (uint32_t)(aap0 + 1));
-  k.put('(');
-  k.put(aa);
-  k.put(')');
-  k.put('\t');
-  }
-  // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity
+  if (!(PW_ABL & 256))
+    k.block(27, [&](auto& o) {
+      o.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
+      o.put('\t');
+      wr_dig(o, (uint32_t)(e.rloc + 1));
+      o.put('\t');
+      wr_dig(o, (uint32_t)(aap0 + 1));
+      o.put('(');
+      o.put(aa);
+      o.put(')');
+      o.put('\t');
+    });
+  // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity; tloc
   const bool big = e.n > kMaxEv;
   const uint8_t b0 = ev_base(r, e, 0);
   bool same = true;
-  if (!(PW_ABL & 512)) {
-  if (typ == PW_OP_SUB) {
-    if (big) {
-      k.put('[');
-      wr_dig(k, (uint32_t)e.n);
-      k.put(']');
-    } else {
-      for (int i = 0; i < e.n; i++) k.put(ev_sub(r, e, i));
-    }
-  }
-  if (typ != PW_OP_DEL) k.put(':');
-  if (big) {
-    k.put('[');
-    wr_dig(k, (uint32_t)e.n);
-    k.put(']');
+  if (big)
     for (int i = 1; i < e.n; i++) same = same && ev_base(r, e, i) == b0;
-  } else {
-    for (int i = 0; i < e.n; i++) {
-      const uint8_t b = ev_base(r, e, i);
-      same = same && b == b0;
-      k.put(b);
+  k.block((big ? 27 : 2 * e.n + 1) + 12, [&](auto& o) {
+    if (!(PW_ABL & 512)) {
+      if (typ == PW_OP_SUB) {
+        if (big) {
+          o.put('[');
+          wr_dig(o, (uint32_t)e.n);
+          o.put(']');
+        } else {
+          for (int i = 0; i < e.n; i++) o.put(ev_sub(r, e, i));
+        }
+      }
+      if (typ != PW_OP_DEL) o.put(':');
+      if (big) {
+        o.put('[');
+        wr_dig(o, (uint32_t)e.n);
+        o.put(']');
+      } else {
+        for (int i = 0; i < e.n; i++) {
+          const uint8_t b = ev_base(r, e, i);
+          same = same && b == b0;
+          o.put(b);
+        }
+      }
+      if (typ == PW_OP_DEL) o.put(':');
     }
-  }
-  if (typ == PW_OP_DEL) k.put(':');
-  }
-  k.put('\t');
-  wr_dig(k, (uint32_t)(in.tloc + 1));
-  k.put('\t');
+    o.put('\t');
+    wr_dig(o, (uint32_t)(in.tloc + 1));
+    o.put('\t');
+  });
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
   if (PW_ABL & 1024) {
-  } else if (in.tmode == 0) {
-    emit_tctx_fast(k, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
-  } else if (in.tmode == 1) {
-    const int tl = in.tx[0];
-    for (int q = 0; q < tl; q++) k.put(in.tx[1 + q]);
-  } else {
+  } else if (in.tmode == 2) {
     emit_tctx_walk(k, r, typ, e.n, in.j, in.wd, in.qs, in.ts, in.ls);
+  } else {
+    k.block(10 + kMaxEv, [&](auto& o) {
+      if (in.tmode == 0) {
+        emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
+      } else {
+        const int tl = in.tx[0];
+        for (int q = 0; q < tl; q++) o.put(in.tx[1 + q]);
+      }
+    });
   }
   k.put('\t');
   // ---- query context (getRefContext, pafreport.cpp:721-733) + status
@@ -748,24 +794,14 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     c0 = r.L - 9;
   }
   if (c0 < 0) c0 = 0;  // L < 9 is reported by the host
-  uint32_t rw0 = 0, rw1 = 0;
   if (!(PW_ABL & 2048)) {
+    uint32_t rw0 = 0, rw1 = 0;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint8_t c = Rc(r, c0 + q);
-    k.put(c);
-    rw0 |= (uint32_t)c << (8 * q);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint8_t c = Rc(r, c0 + 4 + q);
-    k.put(c);
-    rw1 |= (uint32_t)c << (8 * q);
-  }
-  const uint32_t rw2 = Rc(r, c0 + 8);
-  k.put((uint8_t)rw2);
-  k.put('\t');
-  {
+    for (int q = 0; q < 4; q++) {
+      rw0 |= (uint32_t)Rc(r, c0 + q) << (8 * q);
+      rw1 |= (uint32_t)Rc(r, c0 + 4 + q) << (8 * q);
+    }
+    const uint32_t rw2 = Rc(r, c0 + 8);
     // homopolymer seed "cccc": first occurrence in the context (hpolyCheck, :742-746); motifs:
     // first in list order anywhere in it (mmotifCheck, :751-763)
     const uint64_t lo = (uint64_t)rw0 | ((uint64_t)rw1 << 32);
@@ -784,11 +820,20 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     const int st = (same && l >= 0 && l <= eloc && l + 4 >= eloc) ? 1 : (m0 ? 2 : (m1 ? 3 : (m2 ? 4 : (m3 ? 5 : 0))));
     const LDS uint8_t* sw = r.tab->status[st];  // one table row, no divergent literal writes
     const int sl = sw[11];
+    k.block(22, [&](auto& o) {
 #pragma unroll
-    for (int q = 0; q < 11; q++) k.put_if(q < sl, sw[q]);
+      for (int q = 0; q < 4; q++) o.put((uint8_t)(rw0 >> (8 * q)));
+#pragma unroll
+      for (int q = 0; q < 4; q++) o.put((uint8_t)(rw1 >> (8 * q)));
+      o.put((uint8_t)rw2);
+      o.put('\t');
+#pragma unroll
+      for (int q = 0; q < 11; q++) o.put_if(q < sl, sw[q]);
+      o.put('\t');
+    });
+  } else {
+    k.put('\t');
   }
-  }
-  k.put('\t');
   // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
   int modseq_err = -1;
   if (!skip) {
@@ -809,22 +854,24 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
           sub_codon(r, e, ao, caa, cmaa);
         }
         if (caa != cmaa) {
-          if (any) wr_lit(k, ", ");
-          wr_lit(k, "AA");
           const uint32_t ap = (uint32_t)(ao + e.rloc / 3);
-          wr_dig(k, ap);
-          k.put('|');
-          k.put(caa);
-          k.put(':');
-          k.put(cmaa);
-          if (cmaa == '.') {
-            wr_lit(k, "|premature stop at AA");
-            wr_dig(k, ap);
-          }
+          k.block(18 + (cmaa == '.' ? 31 : 0), [&](auto& o) {
+            if (any) wr_lit(o, ", ");
+            wr_lit(o, "AA");
+            wr_dig(o, ap);
+            o.put('|');
+            o.put(caa);
+            o.put(':');
+            o.put(cmaa);
+            if (cmaa == '.') {
+              wr_lit(o, "|premature stop at AA");
+              wr_dig(o, ap);
+            }
+          });
           any = true;
         }
       }
-      if (!any) wr_lit(k, "synonymous");
+      if (!any) k.block(10, [&](auto& o) { wr_lit(o, "synonymous"); });
     } else {
       indel_impact(k, r, e, in.ns_pre);
     }
