@@ -64,6 +64,7 @@ constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, f
 constexpr uint32_t kNBig = (1u << 19) - 1;  // evtbases length field saturates here
 constexpr uint32_t kFnAcgt = 1u << 19;      // query + record literals all A/C/G/T (PW_REF_ACGT)
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
+constexpr int kTxL = 36;        // LDS stride of a lane's copy (9 dwords: conflict-free stores)
 // Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
 #ifndef PW_INDEX_OCC
 #define PW_INDEX_OCC 4
@@ -229,7 +230,7 @@ struct EvIn {
   uint32_t ls;
   int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
   int ll, rl;
-  const uint8_t* tx;  // length byte + field (tmode 1)
+  const LDS uint8_t* tx;  // length byte + field (tmode 1), an LDS copy of the tx record
   int ns_pre;         // next_stop entry the indel scan needs, loaded ahead (kNsNone: not loaded)
   uint32_t j, wd;
   int qs, ts;
@@ -266,11 +267,23 @@ struct RawSink {
     pos += pred ? 1 : 0;
   }
   __device__ __forceinline__ void put_at(int i, uint8_t c) { buf[i] = c; }
+  // bytes 1.. of w, n of them (n <= 4 * N - 1): all stored at fixed offsets, then pos += n
+  template <int N>
+  __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
+#pragma unroll
+    for (int q = 0; q < 4 * N - 1; q++) buf[pos + q] = (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3)));
+    pos += n;
+  }
   template <class F>
   __device__ __forceinline__ void block(int, F&& f) {
     f(*this);
   }
 };
+template <class S, int N>
+__device__ __forceinline__ void put_span_checked(S& k, const uint32_t (&w)[N], int n) {
+#pragma unroll
+  for (int q = 0; q < 4 * N - 1; q++) k.put_if(q < n, (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3))));
+}
 template <int CAP>
 struct LdsSink {
   LDS uint8_t* buf;
@@ -285,6 +298,10 @@ struct LdsSink {
     pos += pred ? 1 : 0;
   }
   __device__ __forceinline__ void put_at(int i, uint8_t c) { *(i < CAP ? buf + i : junk) = c; }
+  template <int N>
+  __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
+    put_span_checked(*this, w, n);
+  }
   template <class F>
   __device__ __forceinline__ void block(int room, F&& f) {
     if (pos + room <= CAP) {
@@ -305,6 +322,10 @@ struct GlobalSink {
     if (pred) p[pos++] = c;
   }
   __device__ __forceinline__ void put_at(int i, uint8_t c) { p[i] = c; }
+  template <int N>
+  __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
+    put_span_checked(*this, w, n);
+  }
   template <class F>
   __device__ __forceinline__ void block(int, F&& f) {
     f(*this);
@@ -778,8 +799,11 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       if (in.tmode == 0) {
         emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
       } else {
-        const int tl = in.tx[0];
-        for (int q = 0; q < tl; q++) o.put(in.tx[1 + q]);
+        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
+        uint32_t tw[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) tw[q] = t32[q];
+        o.put_span(tw, (int)(tw[0] & 0xFFu));
       }
     });
   }
@@ -1238,6 +1262,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_INDEX_OCC) void index_kernel(pw_r
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
+  uint8_t txw[kWave * kTxL];        // per-lane copy of the event's tx record (tmode 1)
   uint32_t ostart[kWave + 1];       // line starts in the page
   uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
 };
@@ -1274,6 +1299,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
   LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
   LDS uint8_t* my_line = w->line + lane * kLStride;
   LDS uint8_t* my_qw = w->qw + lane * kQStride;
+  LDS uint8_t* my_tx = w->txw + lane * kTxL;
   const bool skip = A.skip_codan != 0;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
 
@@ -1287,6 +1313,15 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       const uint32_t typ = h.fn >> 30;
       const bool rev = (h.fn >> 29) & 1u;
       int n = (int)(h.fn & kNBig);
+      // the pre-rendered target context (tctx_kernel) is loaded first: its latency overlaps the
+      // query-window loads below
+      const bool use_tx = !(((h.fn >> 28) & 1u) | (uint32_t)(PW_ABL & 64));
+      v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
+      if (use_tx) {
+        const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+        t0 = tp4[0];
+        t1 = tp4[1];
+      }
       Rec r;
       r.lits = A.lits;
       r.R = A.qseq + h.qb;
@@ -1338,12 +1373,17 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       in.qp = h.qp;
       in.tloc = h.tloc;
       in.ls = h.ls;
-      in.tmode = (((h.fn >> 28) & 1u) | (uint32_t)(PW_ABL & 64)) ? 0 : 1;
+      in.tmode = use_tx ? 1 : 0;
       in.ll = (int)((h.fn >> 23) & 7u);
       in.rl = (int)((h.fn >> 20) & 7u);
       // loads issued ahead of the line (their latency overlaps the query-window staging): the
       // pre-rendered target context and the next-stop entry the indel stop scan ends on
-      in.tx = W.tx + (uint64_t)kTx * s;
+      in.tx = my_tx;
+      if (use_tx) {
+        LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(my_tx);
+        d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
+        d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
+      }
       in.ns_pre = kNsNone;
       if (typ != PW_OP_SUB && r.NS && !skip && !(PW_ABL & 128)) {
         const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
@@ -1619,61 +1659,95 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
 
 // ------------------------------------------------------------------ fixup_kernel
 // Lines longer than the LDS line buffer, one per thread, rewritten in place (their bytes were
-// reserved).  The record is read straight from global memory (no windows).
+// reserved).  The thread stages the same windows as render_kernel (query bytes around the event,
+// the tx record) plus 32 literal bytes in LDS, so only the line itself goes to global memory.
+constexpr int kFxLit = 32;
+struct FixLane {
+  uint8_t qw[kQWin];
+  uint8_t lw[kFxLit];
+  uint8_t tx[kTxL];
+};
 __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
+  __shared__ __attribute__((aligned(16))) FixLane fl[256];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, 256);
   __syncthreads();
+  LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x];
   const uint32_t n = min(W.ctr[1], W.fix_cap);
   const bool skip = A.skip_codan != 0;
   if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const Fixup f = W.fix[i];
     const Hot h = W.hot[f.s];
-    const Cold cd = W.cold[f.s];
-    const pw_aln_desc d = A.desc[cd.ai];
-    const uint32_t qi = d.ref & PW_REF_QMASK;
+    const uint32_t typ = h.fn >> 30;
+    const bool rev = (h.fn >> 29) & 1u;
+    const bool use_tx = !((h.fn >> 28) & 1u);
+    int ne = (int)(h.fn & kNBig);
     Rec r;
-    r.ops = A.ops + d.op_begin;
     r.lits = A.lits;
-    r.R = A.qseq + A.qoff[qi];
-    r.L = A.qlen[qi];
-    r.NS = A.next_stop ? A.next_stop + A.qoff[qi] : nullptr;
+    r.R = A.qseq + h.qb;
+    r.L = h.L;
+    r.NS = A.next_stop ? A.next_stop + h.qb : nullptr;
     r.tab = tp;
-    r.qw = nullptr;
-    r.qlo = 0;
-    r.qn = 0;
     r.opw = nullptr;
     r.op_lo = 0;
     r.op_n = 0;
-    r.lit0 = r.lit1 = 0;
-    r.ls0 = 0;
-    r.ln = 0;
-    r.lw = nullptr;
-    r.l_lo = 0;
-    r.l_n = 0;
-    r.offset = d.offset;
-    r.T = d.t_len;
-    r.n_ops = d.n_ops;
-    r.rev = (d.ref & PW_REF_REVERSE) != 0;
-    r.acgt = false;
-    const uint32_t wd = r.ops[cd.j];
+    r.lit0 = h.l0;
+    r.lit1 = h.l1;
+    r.ls0 = h.ls;
+    r.ln = 8;
+    r.rev = rev;
+    r.acgt = (h.fn & kFnAcgt) != 0;
+    r.offset = 0;
+    r.T = 0;
+    r.ops = nullptr;
+    r.n_ops = 0;
+    if ((uint32_t)ne == kNBig) {  // saturated length: from the op stream
+      const Cold cd = W.cold[f.s];
+      const pw_aln_desc d = A.desc[cd.ai];
+      r.ops = A.ops + d.op_begin;
+      r.n_ops = d.n_ops;
+      ne = event_len(r, cd.j, r.ops[cd.j]);
+    }
+    // windows: tx record, 48 query bytes from 8 before the event, 32 literal bytes from ls
+    if (use_tx) {
+      const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * f.s);
+      const v4u t0 = tp4[0], t1 = tp4[1];
+      LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(me->tx);
+      d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
+      d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
+    }
+    const int rl = event_rloc(r.L, rev, typ, h.qp, ne);
+    int x0 = rl - 8;
+    if (x0 < 0) x0 = 0;
+    const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;
+#pragma unroll
+    for (int q = 0; q < kQWin / 16; q++)
+      *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+    r.qw = me->qw;
+    r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+    r.qn = kQWin;
+    const uint32_t l0 = h.ls & ~3u;
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
+#pragma unroll
+    for (int q = 0; q < kFxLit / 4; q++) reinterpret_cast<LDS uint32_t*>(me->lw)[q] = l32[q];
+    r.lw = me->lw;
+    r.l_lo = l0;
+    r.l_n = kFxLit;
     EvIn in;
-    in.typ = wd >> 30;
-    in.n = event_len(r, cd.j, wd);
+    in.typ = typ;
+    in.n = ne;
     in.qp = h.qp;
     in.tloc = h.tloc;
     in.ls = h.ls;
-    in.tmode = ((h.fn >> 28) & 1u) ? 0 : 2;
+    in.tmode = use_tx ? 1 : 0;
     in.ll = (int)((h.fn >> 23) & 7u);
     in.rl = (int)((h.fn >> 20) & 7u);
-    in.tx = nullptr;
+    in.tx = me->tx;
     in.ns_pre = kNsNone;
-    in.j = cd.j;
-    in.wd = wd;
-    in.qs = cd.qs;
-    in.ts = cd.ts;
+    in.j = in.wd = 0;
+    in.qs = in.ts = 0;
     GlobalSink g;
     g.p = A.text + f.dst;
     g.pos = 0;
