@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (profiles/*.json)")
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_v11" / "summary.json"),
+                    help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
 
     import numpy as np
@@ -131,7 +132,7 @@ def main():
         alg_bytes = int(v.alg_bytes_in) + text_bytes
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
-        if args.traffic_json and os.path.exists(args.traffic_json):
+        if args.config == 2 and args.scale == 1.0 and args.traffic_json and os.path.exists(args.traffic_json):
             traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
         cpu = None
         if not args.no_cpu_baseline and world == 1:

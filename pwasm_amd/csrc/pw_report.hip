@@ -1677,7 +1677,12 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   const uint32_t n = min(W.ctr[1], W.fix_cap);
   const bool skip = A.skip_codan != 0;
   if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  // consecutive lines go to different workgroups, then to different waves: a wave gets one or
+  // two lines, not 64 divergent ones
+  const uint32_t q0 = threadIdx.x / kWave + kWaves * (threadIdx.x % kWave);
+  for (uint32_t q = q0;; q += 256) {
+    const uint32_t i = blockIdx.x + gridDim.x * q;
+    if (i >= n) break;
     const Fixup f = W.fix[i];
     const Hot h = W.hot[f.s];
     const uint32_t typ = h.fn >> 30;
