@@ -108,6 +108,7 @@ struct SmallTables {
   uint8_t comp[256];
   uint8_t codon64[64];
   uint8_t status[8][12];
+  uint8_t dig2[200];  // "00" .. "99"
 };
 
 // ------------------------------------------------------------------ wave primitives
@@ -248,6 +249,51 @@ __device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
   return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i) + 1)] : litb(r, e.ls + 2 * i + 1);
 }
 
+// ---- 16-byte register images of query / modified-sequence bytes (indel fast path)
+typedef unsigned __int128 u128;
+// bytes qw[off, off + 16) of an LDS window (off >= 0; up to 4 bytes past off + 16 are read)
+__device__ __forceinline__ u128 lds16(const LDS uint8_t* qw, int off) {
+  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
+  const uint32_t sh = (uint32_t)off & 3u;
+  uint32_t d[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) d[i] = p[i];
+  u128 v = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) v |= (u128)__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) << (32 * i);
+  return v;
+}
+__device__ __forceinline__ u128 low_bytes(int n) {  // bytes [0, n) set, 0 <= n <= 15
+  return n <= 0 ? (u128)0 : (((u128)1 << (8 * n)) - 1);
+}
+__device__ __forceinline__ uint32_t byte_at(u128 v, int p) { return (uint32_t)(v >> (8 * p)) & 0xFFu; }
+// every byte of v in [0, 15) is one of A, C, G, T (upper case: query and literals are)
+__device__ __forceinline__ bool acgt15(u128 v) {
+  bool ok = true;
+#pragma unroll
+  for (int p = 0; p < 15; p++) ok = ok && is_acgt(byte_at(v, p));
+  return ok;
+}
+// translateCodon of the codon at byte p of v (all ACGT): 2-bit codes, one codon64 lookup
+__device__ __forceinline__ uint8_t codon_at(const LDS SmallTables* t, u128 v, int p) {
+  const uint32_t c0 = (byte_at(v, p) >> 1) & 3u, c1 = (byte_at(v, p + 1) >> 1) & 3u, c2 = (byte_at(v, p + 2) >> 1) & 3u;
+  return t->codon64[c0 << 4 | c1 << 2 | c2];
+}
+// complement of A/C/G/T bytes (A<->T: ^0x15, C<->G: ^0x04; bit 1 tells them apart).  Maps no
+// other byte onto A/C/G/T, so a validity check after it still rejects non-ACGT input.
+__device__ __forceinline__ uint64_t comp_acgt8(uint64_t v) {
+  const uint64_t t = (v >> 1) & 0x0101010101010101ull;
+  return v ^ (t * 0x04ull | (t ^ 0x0101010101010101ull) * 0x15ull);
+}
+
+// bytes qw[off, off + 8) of an LDS window (off >= 0)
+__device__ __forceinline__ uint64_t lds8(const LDS uint8_t* qw, int off) {
+  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
+  const uint32_t sh = (uint32_t)off & 3u;
+  const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+  return (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) | (uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32;
+}
+
 // ------------------------------------------------------------------ line sinks
 // LineSink writes into the lane's LDS line buffer; a store past the buffer or a masked-off
 // character goes to the lane's junk byte (no branch).  A field is written through block(room,
@@ -274,6 +320,13 @@ struct RawSink {
     for (int q = 0; q < 4 * N - 1; q++) buf[pos + q] = (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3)));
     pos += n;
   }
+  // the first n bytes of w (all 4N stored at fixed offsets; the block reserved them)
+  template <int N>
+  __device__ __forceinline__ void put_bytes(const uint32_t (&w)[N], int n) {
+#pragma unroll
+    for (int q = 0; q < 4 * N; q++) buf[pos + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+    pos += n;
+  }
   template <class F>
   __device__ __forceinline__ void block(int, F&& f) {
     f(*this);
@@ -283,6 +336,11 @@ template <class S, int N>
 __device__ __forceinline__ void put_span_checked(S& k, const uint32_t (&w)[N], int n) {
 #pragma unroll
   for (int q = 0; q < 4 * N - 1; q++) k.put_if(q < n, (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3))));
+}
+template <class S, int N>
+__device__ __forceinline__ void put_bytes_checked(S& k, const uint32_t (&w)[N], int n) {
+#pragma unroll
+  for (int q = 0; q < 4 * N; q++) k.put_if(q < n, (uint8_t)(w[q >> 2] >> (8 * (q & 3))));
 }
 template <int CAP>
 struct LdsSink {
@@ -301,6 +359,10 @@ struct LdsSink {
   template <int N>
   __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
     put_span_checked(*this, w, n);
+  }
+  template <int N>
+  __device__ __forceinline__ void put_bytes(const uint32_t (&w)[N], int n) {
+    put_bytes_checked(*this, w, n);
   }
   template <class F>
   __device__ __forceinline__ void block(int room, F&& f) {
@@ -325,6 +387,10 @@ struct GlobalSink {
   template <int N>
   __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
     put_span_checked(*this, w, n);
+  }
+  template <int N>
+  __device__ __forceinline__ void put_bytes(const uint32_t (&w)[N], int n) {
+    put_bytes_checked(*this, w, n);
   }
   template <class F>
   __device__ __forceinline__ void block(int, F&& f) {
@@ -389,6 +455,21 @@ __device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
   for (uint32_t P = 10000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   k.put((uint8_t)('0' + v % 10u));
 }
+// "%d" through the digit-pair table for v < 10000 (two LDS reads, 4 bytes stored at fixed
+// offsets; needs 4 bytes of room); the division ladder otherwise
+template <class S>
+__device__ __forceinline__ void wr_num(S& k, const LDS SmallTables* t, uint32_t v) {
+  if (v < 10000u) {
+    const uint32_t hi = v / 100u, lo = v - 100u * hi;
+    const uint32_t p = (uint32_t)*reinterpret_cast<const LDS uint16_t*>(t->dig2 + 2 * hi) |
+                       (uint32_t)*reinterpret_cast<const LDS uint16_t*>(t->dig2 + 2 * lo) << 16;
+    const int nd = 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u);
+    const uint32_t w[1] = {p >> (8 * (4 - nd))};
+    k.put_bytes(w, nd);
+  } else {
+    wr_dig(k, v);
+  }
+}
 template <class S, int N>
 __device__ __forceinline__ void wr_lit(S& k, const char (&s)[N]) {
 #pragma unroll
@@ -447,6 +528,23 @@ __device__ __forceinline__ void emit_tctx_fast(S& k, const Rec& r, uint32_t typ,
   const int qpa = qp + (typ == PW_OP_SUB ? 1 : (typ == PW_OP_DEL ? n : 0));
   const int f1 = r.rev ? r.L - qpa - rl : qp - ll, n1 = r.rev ? rl : ll;
   const int f2 = r.rev ? r.L - qp : qpa, n2 = r.rev ? ll : rl;
+  const int o1 = f1 - r.qlo, o2 = f2 - r.qlo;
+  if (r.acgt && r.qn == kQWin && o1 >= 0 && o2 >= 0 && o1 + 8 <= kQWin && o2 + 8 <= kQWin && r.ln == 8 &&
+      ls == r.ls0 && nm <= 8) {
+    // register images (comp2 is the identity on A/C/G/T): 8 query bytes each side, the event's
+    // target bases from the literal registers, lower case
+    const uint64_t a = lds8(r.qw, o1), b = lds8(r.qw, o2);
+    const uint64_t l64 = (uint64_t)r.lit1 << 32 | r.lit0;
+    uint64_t m = typ == PW_OP_SUB ? (l64 & 0xFFull) : l64;
+    if (r.rev) m = nm > 0 ? comp_acgt8(__builtin_bswap64(m) >> (8 * (8 - nm))) : 0ull;
+    m |= 0x2020202020202020ull;
+    const uint32_t wa[2] = {(uint32_t)a, (uint32_t)(a >> 32)}, wm[2] = {(uint32_t)m, (uint32_t)(m >> 32)},
+                   wb[2] = {(uint32_t)b, (uint32_t)(b >> 32)};
+    k.put_bytes(wa, n1);
+    k.put_bytes(wm, nm);
+    k.put_bytes(wb, n2);
+    return;
+  }
   uint8_t c1[5], c2[5];
 #pragma unroll
   for (int q = 0; q < 5; q++) {
@@ -501,43 +599,6 @@ __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, 
   }
   aa = translate(r.tab, o[0], o[1], o[2]);
   maa = translate(r.tab, m[0], m[1], m[2]);
-}
-
-// ---- 16-byte register images of query / modified-sequence bytes (indel fast path)
-typedef unsigned __int128 u128;
-// bytes qw[off, off + 16) of an LDS window (off >= 0; up to 4 bytes past off + 16 are read)
-__device__ __forceinline__ u128 lds16(const LDS uint8_t* qw, int off) {
-  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
-  const uint32_t sh = (uint32_t)off & 3u;
-  uint32_t d[5];
-#pragma unroll
-  for (int i = 0; i < 5; i++) d[i] = p[i];
-  u128 v = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) v |= (u128)__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) << (32 * i);
-  return v;
-}
-__device__ __forceinline__ u128 low_bytes(int n) {  // bytes [0, n) set, 0 <= n <= 15
-  return n <= 0 ? (u128)0 : (((u128)1 << (8 * n)) - 1);
-}
-__device__ __forceinline__ uint32_t byte_at(u128 v, int p) { return (uint32_t)(v >> (8 * p)) & 0xFFu; }
-// every byte of v in [0, 15) is one of A, C, G, T (upper case: query and literals are)
-__device__ __forceinline__ bool acgt15(u128 v) {
-  bool ok = true;
-#pragma unroll
-  for (int p = 0; p < 15; p++) ok = ok && is_acgt(byte_at(v, p));
-  return ok;
-}
-// translateCodon of the codon at byte p of v (all ACGT): 2-bit codes, one codon64 lookup
-__device__ __forceinline__ uint8_t codon_at(const LDS SmallTables* t, u128 v, int p) {
-  const uint32_t c0 = (byte_at(v, p) >> 1) & 3u, c1 = (byte_at(v, p + 1) >> 1) & 3u, c2 = (byte_at(v, p + 2) >> 1) & 3u;
-  return t->codon64[c0 << 4 | c1 << 2 | c2];
-}
-// complement of A/C/G/T bytes (A<->T: ^0x15, C<->G: ^0x04; bit 1 tells them apart).  Maps no
-// other byte onto A/C/G/T, so a validity check after it still rejects non-ACGT input.
-__device__ __forceinline__ uint64_t comp_acgt8(uint64_t v) {
-  const uint64_t t = (v >> 1) & 0x0101010101010101ull;
-  return v ^ (t * 0x04ull | (t ^ 0x0101010101010101ull) * 0x15ull);
 }
 
 // The five codons of modseq and the four reference codons after the first (predictImpact's
@@ -702,7 +763,7 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
   if (stop_i >= 0) {
     k.block(30, [&](auto& o) {
       wr_lit(o, "premature stop at AA");
-      wr_dig(o, (uint32_t)(1 + (stop_i + e.r_trloc) / 3));
+      wr_num(o, r.tab, (uint32_t)(1 + (stop_i + e.r_trloc) / 3));
     });
   } else if (aa4n > 0 && maa4n > 0) {
     k.block(23, [&](auto& o) {
@@ -747,9 +808,9 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     k.block(27, [&](auto& o) {
       o.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
       o.put('\t');
-      wr_dig(o, (uint32_t)(e.rloc + 1));
+      wr_num(o, r.tab, (uint32_t)(e.rloc + 1));
       o.put('\t');
-      wr_dig(o, (uint32_t)(aap0 + 1));
+      wr_num(o, r.tab, (uint32_t)(aap0 + 1));
       o.put('(');
       o.put(aa);
       o.put(')');
@@ -787,7 +848,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       if (typ == PW_OP_DEL) o.put(':');
     }
     o.put('\t');
-    wr_dig(o, (uint32_t)(in.tloc + 1));
+    wr_num(o, r.tab, (uint32_t)(in.tloc + 1));
     o.put('\t');
   });
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
@@ -795,7 +856,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   } else if (in.tmode == 2) {
     emit_tctx_walk(k, r, typ, e.n, in.j, in.wd, in.qs, in.ts, in.ls);
   } else {
-    k.block(10 + kMaxEv, [&](auto& o) {
+    k.block(10 + kMaxEv + 4, [&](auto& o) {
       if (in.tmode == 0) {
         emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
       } else {
@@ -819,13 +880,21 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   }
   if (c0 < 0) c0 = 0;  // L < 9 is reported by the host
   if (!(PW_ABL & 2048)) {
-    uint32_t rw0 = 0, rw1 = 0;
+    uint32_t rw0 = 0, rw1 = 0, rw2 = 0;
+    const int oc = c0 - r.qlo;
+    if (r.qn == kQWin && oc >= 0 && oc + 16 <= kQWin) {  // one image from the window
+      const u128 im = lds16(r.qw, oc);
+      rw0 = (uint32_t)im;
+      rw1 = (uint32_t)(im >> 32);
+      rw2 = (uint32_t)(im >> 64) & 0xFFu;
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      rw0 |= (uint32_t)Rc(r, c0 + q) << (8 * q);
-      rw1 |= (uint32_t)Rc(r, c0 + 4 + q) << (8 * q);
+      for (int q = 0; q < 4; q++) {
+        rw0 |= (uint32_t)Rc(r, c0 + q) << (8 * q);
+        rw1 |= (uint32_t)Rc(r, c0 + 4 + q) << (8 * q);
+      }
+      rw2 = Rc(r, c0 + 8);
     }
-    const uint32_t rw2 = Rc(r, c0 + 8);
     // homopolymer seed "cccc": first occurrence in the context (hpolyCheck, :742-746); motifs:
     // first in list order anywhere in it (mmotifCheck, :751-763)
     const uint64_t lo = (uint64_t)rw0 | ((uint64_t)rw1 << 32);
@@ -842,17 +911,13 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       m3 = m3 || v4 == 0x43415447u;                 // "GTAC"
     }
     const int st = (same && l >= 0 && l <= eloc && l + 4 >= eloc) ? 1 : (m0 ? 2 : (m1 ? 3 : (m2 ? 4 : (m3 ? 5 : 0))));
-    const LDS uint8_t* sw = r.tab->status[st];  // one table row, no divergent literal writes
-    const int sl = sw[11];
-    k.block(22, [&](auto& o) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) o.put((uint8_t)(rw0 >> (8 * q)));
-#pragma unroll
-      for (int q = 0; q < 4; q++) o.put((uint8_t)(rw1 >> (8 * q)));
-      o.put((uint8_t)rw2);
-      o.put('\t');
-#pragma unroll
-      for (int q = 0; q < 11; q++) o.put_if(q < sl, sw[q]);
+    const LDS uint32_t* sw = reinterpret_cast<const LDS uint32_t*>(r.tab->status[st]);  // one table row
+    const uint32_t sv[3] = {sw[0], sw[1], sw[2]};
+    const int sl = (int)(sv[2] >> 24);
+    const uint32_t rv[3] = {rw0, rw1, rw2 | (uint32_t)'\t' << 8};
+    k.block(23, [&](auto& o) {
+      o.put_bytes(rv, 10);
+      o.put_bytes(sv, sl);
       o.put('\t');
     });
   } else {
@@ -882,14 +947,14 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
           k.block(18 + (cmaa == '.' ? 31 : 0), [&](auto& o) {
             if (any) wr_lit(o, ", ");
             wr_lit(o, "AA");
-            wr_dig(o, ap);
+            wr_num(o, r.tab, ap);
             o.put('|');
             o.put(caa);
             o.put(':');
             o.put(cmaa);
             if (cmaa == '.') {
               wr_lit(o, "|premature stop at AA");
-              wr_dig(o, ap);
+              wr_num(o, r.tab, ap);
             }
           });
           any = true;
@@ -974,6 +1039,10 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
   }
   for (int i = tid; i < 64; i += nthreads) d[offsetof(SmallTables, codon64) + i] = s[offsetof(Tables, codon64) + i];
   for (int i = tid; i < 96; i += nthreads) d[offsetof(SmallTables, status) + i] = s[offsetof(Tables, status) + i];
+  for (int i = tid; i < 100; i += nthreads) {
+    d[offsetof(SmallTables, dig2) + 2 * i] = (uint8_t)('0' + i / 10);
+    d[offsetof(SmallTables, dig2) + 2 * i + 1] = (uint8_t)('0' + i % 10);
+  }
 }
 
 // ------------------------------------------------------------------ index_kernel
