@@ -72,6 +72,9 @@ constexpr int kTxL = 36;        // LDS stride of a lane's copy (9 dwords: confli
 #ifndef PW_RENDER_OCC
 #define PW_RENDER_OCC 3
 #endif
+#ifndef PW_TXREG
+#define PW_TXREG 0
+#endif
 #ifndef PW_ABL
 #define PW_ABL 0
 #endif
@@ -90,7 +93,7 @@ struct Hot {
   uint32_t fn;
   uint32_t l0, l1;
 };
-// Cold record (fixups, record results), 16 bytes.
+// Cold record, 16 bytes: written only for a record's first / last line and saturated lengths.
 struct Cold {
   uint32_t ai, j;  // record, head op
   int32_t qs, ts;  // query / target position at the head op
@@ -231,7 +234,8 @@ struct EvIn {
   uint32_t ls;
   int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
   int ll, rl;
-  const LDS uint8_t* tx;  // length byte + field (tmode 1), an LDS copy of the tx record
+  const LDS uint8_t* tx;  // length byte + field (tmode 1), an LDS copy of the tx record, or
+  uint32_t txr[6];        // (tx == nullptr) the record's first 24 bytes in registers
   int ns_pre;         // next_stop entry the indel scan needs, loaded ahead (kNsNone: not loaded)
   uint32_t j, wd;
   int qs, ts;
@@ -860,10 +864,15 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       if (in.tmode == 0) {
         emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
       } else {
-        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
         uint32_t tw[6];
+        if (in.tx) {
+          const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
 #pragma unroll
-        for (int q = 0; q < 6; q++) tw[q] = t32[q];
+          for (int q = 0; q < 6; q++) tw[q] = t32[q];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 6; q++) tw[q] = in.txr[q];
+        }
         o.put_span(tw, (int)(tw[0] & 0xFFu));
       }
     });
@@ -1049,9 +1058,6 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
 constexpr int kOpWin = kSegOps + 2 * kOpHalo;
 struct IndexWave {
   uint32_t opw[kOpWin];            // op words of the segment + halo
-  int32_t ots[kOpWin];             // their target / query / literal starts
-  int32_t oqs[kOpWin];
-  uint32_t ols[kOpWin];
 };
 
 __device__ __forceinline__ int ndigits(uint32_t v) {
@@ -1121,32 +1127,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       ttot += bcast(ti_, 63);
       ltot += bcast(li_, 63);
       w->opw[kOpHalo + idx] = wd[k];
-      w->ots[kOpHalo + idx] = idx < nseg ? ts[k] : INT_MAX;
-      w->oqs[kOpHalo + idx] = qs[k];
-      w->ols[kOpHalo + idx] = ls[k];
     }
-    {  // halo: op words before / after the segment and their coordinates
-      const bool h = lane < 2 * kOpHalo;
-      const int j = lane < kOpHalo ? (int)sb - kOpHalo + lane : (int)(sb + nseg) + (lane - kOpHalo);
-      const bool valid = h && j >= 0 && (uint32_t)j < n_ops;
-      const uint32_t v = valid ? ops[j] : 0u;
-      const uint32_t qa = op_qadv(v), ta = op_tadv(v), la = op_ladv(v);
-      const uint32_t qi_ = wave_incl_scan(qa, lane), ti_ = wave_incl_scan(ta, lane), li_ = wave_incl_scan(la, lane);
-      const uint32_t q16 = bcast(qi_, kOpHalo - 1), t16 = bcast(ti_, kOpHalo - 1), l16 = bcast(li_, kOpHalo - 1);
-      const uint32_t qx = qi_ - qa, tx_ = ti_ - ta, lx = li_ - la;  // exclusive prefixes
-      if (h) {
-        const int pos = lane < kOpHalo ? lane : kOpHalo + (int)nseg + (lane - kOpHalo);
-        w->opw[pos] = v;
-        if (lane < kOpHalo) {  // before: segment start minus the advances from here to it
-          w->ots[pos] = valid ? tc - (int)(t16 - tx_) : INT_MIN;
-          w->oqs[pos] = qc - (int)(q16 - qx);
-          w->ols[pos] = lc - (l16 - lx);
-        } else {  // after: segment end plus the advances before
-          w->ots[pos] = valid ? tc + (int)ttot + (int)(tx_ - t16) : INT_MAX;
-          w->oqs[pos] = qc + (int)qtot + (int)(qx - q16);
-          w->ols[pos] = lc + ltot + (lx - l16);
-        }
-      }
+    if (lane < 2) {  // halo: the op words just before / after the segment (tctx_fast's neighbours)
+      const int j = lane == 0 ? (int)sb - 1 : (int)(sb + nseg);
+      w->opw[lane == 0 ? kOpHalo - 1 : kOpHalo + (int)nseg] = (j >= 0 && (uint32_t)j < n_ops) ? ops[j] : 0u;
     }
     // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads
     uint64_t subm[2], hm[2];
@@ -1242,12 +1226,14 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           hh.l0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
           hh.l1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
           W.hot[s] = hh;
-          Cold cd;
-          cd.ai = ai;
-          cd.j = j;
-          cd.qs = qs[k];
-          cd.ts = ts[k];
-          W.cold[s] = cd;
+          if (kidx == 0 || n >= kNBig) {  // only the first / last line and saturated lengths read it
+            Cold cd;
+            cd.ai = ai;
+            cd.j = j;
+            cd.qs = qs[k];
+            cd.ts = ts[k];
+            W.cold[s] = cd;
+          }
           slow = !fast && !(PW_ABL & 32);
         }
       }
@@ -1279,6 +1265,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     const uint64_t s_last = rev ? evb + nmax - ev : evb + ev - 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's store of that record first
     atomicOr(&W.hot[s_last].fn, rev ? 1u << 27 : 1u << 26);
+    W.cold[s_last].ai = ai;
   }
   if (lane == 0) {
     pw_aln_result res;
@@ -1331,10 +1318,23 @@ __global__ __launch_bounds__(kWave* kWaves, PW_INDEX_OCC) void index_kernel(pw_r
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
+#if !PW_TXREG
   uint8_t txw[kWave * kTxL];        // per-lane copy of the event's tx record (tmode 1)
+#endif
   uint32_t ostart[kWave + 1];       // line starts in the page
   uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
 };
+
+// the record owning event slot s: the last one whose first slot is <= s (error path only)
+__device__ __noinline__ uint32_t rec_of_slot(const pw_report_args& A, uint64_t s) {
+  uint32_t lo = 0, hi = A.n_alns - 1;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo + 1) / 2;
+    if (A.desc[mid].ev_begin <= s) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
 
 __device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
   Hot h;
@@ -1368,7 +1368,9 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
   LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
   LDS uint8_t* my_line = w->line + lane * kLStride;
   LDS uint8_t* my_qw = w->qw + lane * kQStride;
+#if !PW_TXREG
   LDS uint8_t* my_tx = w->txw + lane * kTxL;
+#endif
   const bool skip = A.skip_codan != 0;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
 
@@ -1447,12 +1449,17 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       in.rl = (int)((h.fn >> 20) & 7u);
       // loads issued ahead of the line (their latency overlaps the query-window staging): the
       // pre-rendered target context and the next-stop entry the indel stop scan ends on
+#if PW_TXREG
+      in.tx = nullptr;
+      in.txr[0] = t0.x, in.txr[1] = t0.y, in.txr[2] = t0.z, in.txr[3] = t0.w, in.txr[4] = t1.x, in.txr[5] = t1.y;
+#else
       in.tx = my_tx;
       if (use_tx) {
         LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(my_tx);
         d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
         d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
       }
+#endif
       in.ns_pre = kNsNone;
       if (typ != PW_OP_SUB && r.NS && !skip && !(PW_ABL & 128)) {
         const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
@@ -1475,7 +1482,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
 #endif
       linelen = k.pos;
       if (merr >= 0) {  // modseq error: first failing event of the record in output order
-        const uint32_t ai = W.cold[s].ai;
+        const uint32_t ai = rec_of_slot(A, s);
         const pw_aln_desc d = A.desc[ai];
         const uint64_t evb = d.ev_begin;
         const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
@@ -1819,6 +1826,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     in.ll = (int)((h.fn >> 23) & 7u);
     in.rl = (int)((h.fn >> 20) & 7u);
     in.tx = me->tx;
+#pragma unroll
+    for (int q = 0; q < 6; q++) in.txr[q] = 0;
     in.ns_pre = kNsNone;
     in.j = in.wd = 0;
     in.qs = in.ts = 0;
@@ -1955,7 +1964,7 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
     hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
-    if (rg > (uint64_t)ncu * 3u) rg = (uint64_t)ncu * 3u;
+    if (rg > (uint64_t)ncu * PW_RENDER_OCC) rg = (uint64_t)ncu * PW_RENDER_OCC;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);
   }
