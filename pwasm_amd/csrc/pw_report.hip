@@ -54,7 +54,7 @@ constexpr int kWaves = 4;       // wavefronts per workgroup (independent; they s
 constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
 constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
 constexpr int kQWin = 48;       // render_kernel: forward-query window per lane (bytes)
-constexpr int kQStride = 48;    // ... its LDS stride
+constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dword reads at most 2-way)
 constexpr int kLine = 96;       // render_kernel: per-lane report-line buffer (bytes)
 constexpr int kLStride = 100;   // ... its LDS stride (25 dwords: per-lane byte stores conflict-free)
 constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
