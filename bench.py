@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_v11" / "summary.json"),
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_v13" / "summary.json"),
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
 
