@@ -14,9 +14,11 @@ event duration vs 8 TB/s) and the CPU baseline: the single-threaded oracle resta
 (oracle/pafreport_oracle, kind "port") on a bounded sample of the same workload, 1 core.
 """
 import argparse
+import filecmp
 import json
 import os
 import pathlib
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -41,9 +43,13 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_v13" / "summary.json"),
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle diff + end-to-end CLI run")
+    ap.add_argument("--remove-gaps", action="store_true", help="cfg5: MSAColumns::removeConsGaps=true")
+    ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
+    if args.traffic_json is None:  # the newest committed profile of the same command (profiles/run_prof.sh)
+        args.traffic_json = latest_profile(args.config)
 
     import numpy as np
     import torch
@@ -128,15 +134,51 @@ def main():
         tot_events = int(e.item())
 
     if rank == 0:
-        # algorithmic bytes of one launch: inputs + report text written
-        alg_bytes = int(v.alg_bytes_in) + text_bytes
+        report = {}
+        # algorithmic bytes of one pass, SURVEY.md §8(d): 16 B per record descriptor, 4 B per packed
+        # op, 1 B per literal, 32 B per event record, 13 B per base of each distinct query (the base
+        # + 3 frame next-stop int32 entries; 1 B when the codon pass is skipped, -F / -N)
+        desc = batch.array("desc").view(np.uint32).reshape(-1, 8)
+        qlen = batch.array("qlen").astype(np.int64)
+        uq = np.unique(desc[:, 3] & 0x3FFFFFFF)
+        per_base = 1 if v.skip_codan else 13
+        alg_bytes = int(16 * v.n_alns + 4 * v.n_ops + v.n_lits + 32 * n_events + per_base * int(qlen[uq].sum()))
+        # the report-text variant: inputs + the text actually written
+        alg_text = int(v.alg_bytes_in) + text_bytes
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        prof = {}
         if args.config == 2 and args.scale == 1.0 and args.traffic_json and os.path.exists(args.traffic_json):
-            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(fa, paf, args.cpu_sample, tmp)
+            prof = json.load(open(args.traffic_json))
+        traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
+        flags_cli = ["-G", "-C"] if flags else []
+        parity, cpu, e2e = None, None, None
+        if not args.no_parity:
+            # the benchmarked batch itself, copied back once (outside the timed region) and
+            # diffed byte for byte against the oracle on the same input
+            got = os.path.join(tmp, "hip.txt")
+            rc = batch.write_report_from(dev, got)
+            want = os.path.join(tmp, "oracle.txt")
+            el = run_oracle(flags_cli, fa, paf, want)
+            parity = "ok" if rc == 0 and filecmp.cmp(got, want, shallow=False) else "FAIL"
+            n_or = count_events(want)
+            if not args.no_cpu_baseline and args.cpu_sample >= v.n_alns:
+                cpu = {"value": n_or / el, "unit": "events/s", "cores": 1, "kind": "port",
+                       "sample": f"the whole benchmarked batch ({v.n_alns} records, {n_or} events, {el:.1f} s, "
+                                 f"oracle/pafreport_oracle pinned to one core)"}
+            # end to end: the drop-in CLI (PAF text in, report file out) on the same input
+            cli_out = os.path.join(tmp, "cli.txt")
+            t0 = time.perf_counter()
+            p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", cli_out],
+                               stderr=subprocess.PIPE)
+            cli_s = time.perf_counter() - t0
+            cli_ok = p.returncode == 0 and filecmp.cmp(cli_out, want, shallow=False)
+            e2e = {"cli_wall_s": round(cli_s, 3), "events_per_s": n_or / cli_s, "parity": "ok" if cli_ok else "FAIL",
+                   "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf -o report.txt (PAF text -> report file, "
+                          f"{os.path.getsize(paf)} B in, {os.path.getsize(want)} B out)"}
+            if not cli_ok:
+                parity = "FAIL"
+        if cpu is None and not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(flags_cli, fa, paf, args.cpu_sample, tmp)
         out = {
             "metric": "cs-events classified/sec (whole node) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": tot_events * args.steps / max_el,
@@ -153,12 +195,18 @@ def main():
             "config": {"workload": f"cfg{args.config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
                                    f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU",
                        "records_per_gpu": int(v.n_alns), "events_per_gpu": n_events, "scale": args.scale,
-                       "parallelism": f"shard-by-target x{world}"},
+                       "parallelism": "independent per-rank batches" if world > 1 else "single GPU"},
+            "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "pw_report_events (index+tctx+render+fixup+finalize)", "kernel_ms": round(kern_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_formula": "SURVEY 8(d): 16*n_alns + 4*n_ops + n_lits + 32*E + 13*sum(L unique queries)",
+                         "achieved_text_variant": round(alg_text / (kern_ms * 1e-3) / 1e9, 2),
+                         "alg_bytes_text_variant": alg_text,
+                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd")},
             "cpu_baseline": cpu,
+            "e2e": e2e,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -169,14 +217,17 @@ def bench_gapassem(args, world, rank, dev_name):
     """BASELINE.json configs[4]: GapAssem consensus of one 200-row, ~1M-column layout (pwsynth
     cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step = pw_msa_count on the
     rank's rows + all-reduce of the [n_cols x 6] histograms and of mincol/-maxcol (RCCL) +
-    pw_msa_call + pw_msa_refine with removeConsGaps (the library default: consensus string +
-    row edits).  Throughput = layout bases per second (all rows, whole job)."""
+    pw_msa_call + pw_msa_refine (consensus string; with --remove-gaps also the removeConsGaps row
+    edits).  Default removeConsGaps=false: pafreport's setting (pafreport.cpp:31,203), which is
+    also what the linear-time CPU oracle can time at full size.  Throughput = layout bases per
+    second (all rows, whole job)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from pwasm_amd import gapassem
 
+    remove = bool(args.remove_gaps)
     tmp = tempfile.mkdtemp(prefix=f"pwga{rank}_")
     lay_path = os.path.join(tmp, "l.pwl")
     t0 = time.time()
@@ -203,7 +254,7 @@ def bench_gapassem(args, world, rank, dev_name):
             mm[0] = red[0]
             mm[1] = -red[1]
         eng.call(st)
-        eng.refine(st, True)
+        eng.refine(st, remove)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -230,13 +281,34 @@ def bench_gapassem(args, world, rank, dev_name):
         t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         max_el = float(t.item())
+    parity = None
+    if not args.no_parity:
+        # the whole layout through the same driver (outside the timed region): PWC1 bytes vs the
+        # GapAssem oracle (refineMSA restated, GapAssem.cpp:1133-1198)
+        rc, _, got = gapassem.consensus(lay_path, remove_gaps=remove)
     if rank == 0:
+        cpu = None
+        if not args.no_parity:
+            want = os.path.join(tmp, "oracle.pwc")
+            pin, cpu0 = pin_cmd()
+            t0 = time.perf_counter()
+            p = subprocess.run(pin + [str(REPO / "oracle/build/gapassem_oracle"), lay_path, want,
+                                      *(["--remove-gaps"] if remove else [])])
+            el = time.perf_counter() - t0
+            parity = "ok" if rc == 0 and p.returncode == 0 and open(want, "rb").read() == got else "FAIL"
+            if not args.no_cpu_baseline and not remove:
+                cpu = {"value": total_bases / el, "unit": "bases/s", "cores": 1, "kind": "port",
+                       "sample": f"the whole layout ({hdr.n} rows, {total_bases} bases, {el:.1f} s; "
+                                 f"oracle/gapassem_oracle, removeConsGaps=false, pinned to cpu {cpu0})"}
         ncols = lay.length
         # algorithmic bytes: 16 B row descriptor + 3 B per base (base + int16
         # gap) read, 24 B counts + 1 B consensus per column written; this rank's rows
         own = int(lay.seqlen[lo:hi].sum())
         alg = 16 * (hi - lo) + 3 * own + 25 * ncols
         achieved = alg / (kern_ms * 1e-3) / 1e9
+        prof = {}
+        if args.traffic_json and os.path.exists(args.traffic_json) and args.scale == 1.0 and not remove:
+            prof = json.load(open(args.traffic_json))
         out = {
             "metric": "GapAssem layout bases called/sec (count + histogram all-reduce + bestChar + refineMSA)",
             "value": total_bases * args.steps / max_el,
@@ -250,40 +322,78 @@ def bench_gapassem(args, world, rank, dev_name):
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (pwsynth layout cfg5, seed 5)",
-            "config": {"workload": f"cfg5: {hdr.n} rows x {ncols} columns, {total_bases} bases, removeConsGaps",
+            "config": {"workload": f"cfg5: {hdr.n} rows x {ncols} columns, {total_bases} bases, "
+                                   f"removeConsGaps={'true' if remove else 'false'}",
                        "rows": int(hdr.n), "columns": int(ncols), "parallelism": f"rows sharded x{world}"},
+            "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": "pw_msa_count+pw_msa_call+pw_msa_refine (rank 0)", "kernel_ms": round(kern_ms, 4),
-                         "alg_bytes_per_launch": alg},
-            "cpu_baseline": None,
+                         "alg_bytes_per_launch": alg,
+                         "alg_formula": "SURVEY 8(d): sum_rows(16 + 3*seqlen) + 25*n_cols",
+                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd")},
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(fa, paf, n_rec, tmp):
-    """Time the single-threaded oracle (C restatement of pafreport) on the first n_rec records."""
+def latest_profile(config):
+    """profiles/r<round>_v<k>/summary.json of the newest profile taken with this --config."""
+    import re
+    best, key = None, None
+    for d in (REPO / "profiles").glob("r*_v*"):
+        m = re.fullmatch(r"r(\d+)_v(\d+)", d.name)
+        f = d / "summary.json"
+        if not m or not f.exists():
+            continue
+        try:
+            cfg = int(json.load(open(f)).get("config", 2))
+        except (ValueError, OSError):
+            continue
+        k = (int(m.group(1)), int(m.group(2)))
+        if cfg == config and (key is None or k > key):
+            best, key = str(f), k
+    return best
+
+
+def pin_cmd():
+    cpu0 = sorted(os.sched_getaffinity(0))[0]
+    return (["taskset", "-c", str(cpu0)] if shutil.which("taskset") else []), cpu0
+
+
+def run_oracle(flags_cli, fa, paf, outp):
+    """The single-threaded oracle (C restatement of pafreport) on one core; returns seconds."""
+    pin, _ = pin_cmd()
+    t0 = time.perf_counter()
+    subprocess.run(pin + [str(REPO / "oracle/build/pafreport_oracle"), *flags_cli, "-r", fa, paf, "-o", outp],
+                   check=True)
+    return time.perf_counter() - t0
+
+
+def count_events(path):
+    lines = hdr = 0
+    with open(path, "rb") as f:
+        for line in f:
+            lines += 1
+            hdr += line.startswith(b">")
+    return lines - hdr
+
+
+def cpu_baseline(flags_cli, fa, paf, n_rec, tmp):
+    """Time the single-threaded oracle on the first n_rec records."""
     sample = os.path.join(tmp, "sample.paf")
     with open(paf) as f, open(sample, "w") as g:
         for i, line in enumerate(f):
             if i >= n_rec:
                 break
             g.write(line)
-    oracle = str(REPO / "oracle/build/pafreport_oracle")
     outp = os.path.join(tmp, "cpu.txt")
-    cpu0 = sorted(os.sched_getaffinity(0))[0]
-    pin = ["taskset", "-c", str(cpu0)] if subprocess.run(["which", "taskset"], stdout=subprocess.DEVNULL).returncode == 0 else []
-    t0 = time.perf_counter()
-    subprocess.run(pin + [oracle, "-G", "-C", "-r", fa, sample, "-o", outp], check=True)
-    el = time.perf_counter() - t0
-    lines = hdr = 0
-    with open(outp, "rb") as f:
-        for line in f:
-            lines += 1
-            hdr += line.startswith(b">")
-    ev = lines - hdr
+    el = run_oracle(flags_cli, fa, sample, outp)
+    ev = count_events(outp)
+    _, cpu0 = pin_cmd()
     return {"value": ev / el, "unit": "events/s", "cores": 1, "kind": "port",
             "sample": f"first {n_rec} records of the same batch ({ev} events, {el:.1f} s, pinned to cpu {cpu0})"}
 

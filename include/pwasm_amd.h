@@ -89,9 +89,15 @@ typedef struct pw_aln_result {
 #define PW_REC_OK 0
 #define PW_REC_MISMATCH 1 /* "Error: base mismatch ..." (pafreport.cpp:551-554) */
 #define PW_REC_MODSEQ 2   /* "Error: modseq[%d] not matching ..." (pafreport.cpp:812-813) */
+#define PW_REC_OVERFLOW 3 /* event slots or text capacity exceeded (caller sizing bug) */
+#define PW_REC_LAYOUT 4   /* descriptor violates the pw_report_args contract (qoff / ev_begin) */
 
 /* Arguments of pw_report_events (all pointers are device pointers).  qseq and lits must stay
- * readable for PW_DEV_PAD bytes past their last element (16-byte LDS staging loads). */
+ * readable for PW_DEV_PAD bytes past their last element (16-byte LDS staging loads).
+ * Contract checked per record on the device (violations -> PW_REC_LAYOUT, no events):
+ *   qoff[q] is a multiple of 16 and < 2^36 (64 GiB of concatenated queries);
+ *   desc[].ev_begin is non-decreasing: record i owns slots [ev_begin(i), ev_begin(i+1)), the
+ *   last record [ev_begin, n_ev_slots) (the prefix sum of pw_cs_totals.n_events_max). */
 #define PW_DEV_PAD 256
 typedef struct pw_report_args {
   const pw_aln_desc* desc;  /* [n_alns] */

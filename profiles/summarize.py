@@ -6,7 +6,11 @@ or of the GapAssem calls).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so traffic is taken as
-2*FETCH + WRITE (an upper bound for the narrower, uncalibrated accesses)."""
+2*FETCH + WRITE (an upper bound for the narrower, uncalibrated accesses).
+
+Occupancy (achieved waves per SIMD, per kernel) = 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8) /
+(4 * CUs): SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md, SQ PMC units) summed over every
+wave, GRBM_GUI_ACTIVE counts busy cycles summed over the 8 XCDs."""
 import collections
 import csv
 import glob
@@ -15,7 +19,10 @@ import os
 import sys
 
 
-def main(src, out):
+N_CU = 256
+
+
+def main(src, out, bench_args=""):
     stats = list(csv.DictReader(open(f"{src}/trace/run_kernel_stats.csv")))
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")):
@@ -28,7 +35,10 @@ def main(src, out):
     pw = [k for k in kern if k["name"].startswith("pw::")]
     fetch = sum(per[k].get("FETCH_SIZE", 0) for k in per) * 1024
     write = sum(per[k].get("WRITE_SIZE", 0) for k in per) * 1024
+    a = bench_args.split()
     res = {
+        "bench_args": bench_args,
+        "config": int(a[a.index("--config") + 1]) if "--config" in a else 2,
         "kernels": kern,
         "pass_us": sum(k["avg_us"] for k in pw),
         "pmc_per_launch": per,
@@ -41,20 +51,29 @@ def main(src, out):
     for k, c in per.items():
         if c.get("SQ_LDS_IDX_ACTIVE"):
             c["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
+        if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_WAVE_CYCLES"):
+            c["occupancy_waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8) / (4 * N_CU)
+    res["occupancy_waves_per_simd"] = {k: round(c["occupancy_waves_per_simd"], 2) for k, c in per.items()
+                                       if "occupancy_waves_per_simd" in c}
+    # the bench's HIP-event bracket covers pw_report_events only (the stop table is built before it)
+    rep = [k for k in per if not k.startswith("pw::stop_table")]
+    res["hbm_bytes_per_report_pass"] = sum(2 * per[k].get("FETCH_SIZE", 0) + per[k].get("WRITE_SIZE", 0) for k in rep) * 1024
+    res["report_pass_us"] = sum(k["avg_us"] for k in pw if not k["name"].startswith("pw::stop_table"))
     json.dump(res, open(out + ".json", "w"), indent=1)
     with open(out + ".md", "w") as f:
         f.write(f"# rocprofv3 summary: {os.path.basename(src)}\n\n| kernel | calls | avg us | % |\n|---|---|---|---|\n")
         for k in kern:
             f.write(f"| {k['name'][:60]} | {k['calls']} | {k['avg_us']:.1f} | {k['pct']:.2f} |\n")
         f.write(f"\npw:: kernels per pass: {res['pass_us']:.1f} us\n")
+        f.write("achieved waves/SIMD: " + ", ".join(f"{k} {v}" for k, v in res["occupancy_waves_per_simd"].items()) + "\n")
         f.write(f"HBM bytes per pass (2*FETCH + WRITE): {res['hbm_bytes_per_launch'] / 1e6:.1f} MB "
                 f"(FETCH {fetch / 1e6:.1f} MB raw, WRITE {write / 1e6:.1f} MB)\n")
         for k, c in sorted(per.items()):
             f.write(f"\n## {k} (per launch)\n\n")
             for n, v in sorted(c.items()):
-                f.write(f"- {n}: {v:,.3f}\n" if n.endswith("frac") else f"- {n}: {v:,.1f}\n")
+                f.write(f"- {n}: {v:,.3f}\n" if (n.endswith("frac") or n.startswith("occupancy")) else f"- {n}: {v:,.1f}\n")
     print(json.dumps({k: v for k, v in res.items() if k != "pmc_per_launch"}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], " ".join(sys.argv[3:]))

@@ -696,8 +696,9 @@ int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_a
     fputs(b.msgs[rh.post_msg].c_str(), err);
     return 1;
   }
-  if (r.err == 3) {
-    fprintf(err, "pafreport: internal error: report slot overflow\n");
+  if (r.err == PW_REC_OVERFLOW || r.err == PW_REC_LAYOUT) {
+    fprintf(err, "pafreport: internal error: %s\n",
+            r.err == PW_REC_OVERFLOW ? "report slot overflow" : "batch layout rejected by the device");
     return 2;
   }
   fwrite(b.hdr.data() + rh.hdr_off, 1, rh.hdr_len, out);

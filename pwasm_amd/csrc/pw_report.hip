@@ -65,19 +65,8 @@ constexpr uint32_t kNBig = (1u << 19) - 1;  // evtbases length field saturates h
 constexpr uint32_t kFnAcgt = 1u << 19;      // query + record literals all A/C/G/T (PW_REF_ACGT)
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 constexpr int kTxL = 36;        // LDS stride of a lane's copy (9 dwords: conflict-free stores)
-// Timing-only ablations for experiment builds (tools/exp_build.sh); 0 in the product build.
-#ifndef PW_INDEX_OCC
-#define PW_INDEX_OCC 4
-#endif
-#ifndef PW_RENDER_OCC
-#define PW_RENDER_OCC 3
-#endif
-#ifndef PW_TXREG
-#define PW_TXREG 0
-#endif
-#ifndef PW_ABL
-#define PW_ABL 0
-#endif
+constexpr int kIndexOcc = 4;    // index_kernel: waves per SIMD the register budget is sized for
+constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)
 
 // Render record of one event (index_kernel -> render_kernel), 32 bytes.
 //   fn: type (31-30) | reverse (29) | fast tctx (28) | first line of its record (27) |
@@ -85,7 +74,7 @@ constexpr int kTxL = 36;        // LDS stride of a lane's copy (9 dwords: confli
 //       saturated)
 //   l0, l1: the event's first 8 literal bytes (SUB: target,query pairs; INS: inserted bases)
 struct Hot {
-  uint32_t qb;    // forward query start in qseq
+  uint32_t qb;    // forward query start in qseq, in 16-byte units (qoff is 16-byte aligned)
   int32_t L;      // query length
   int32_t qp;     // offset + qpos at the event (aligned strand)
   int32_t tloc;   // printed tloc - 1 (pafreport.cpp:639)
@@ -234,8 +223,7 @@ struct EvIn {
   uint32_t ls;
   int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
   int ll, rl;
-  const LDS uint8_t* tx;  // length byte + field (tmode 1), an LDS copy of the tx record, or
-  uint32_t txr[6];        // (tx == nullptr) the record's first 24 bytes in registers
+  const LDS uint8_t* tx;  // length byte + field (tmode 1): an LDS copy of the tx record
   int ns_pre;         // next_stop entry the indel scan needs, loaded ahead (kNsNone: not loaded)
   uint32_t j, wd;
   int qs, ts;
@@ -808,8 +796,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   rel = e.rloc - e.r_trloc;
 
   // ---- "E\trloc\taapos(aa)\t"
-  if (!(PW_ABL & 256))
-    k.block(27, [&](auto& o) {
+  k.block(27, [&](auto& o) {
       o.put(typ == PW_OP_SUB ? 'S' : (typ == PW_OP_INS ? 'I' : 'D'));
       o.put('\t');
       wr_num(o, r.tab, (uint32_t)(e.rloc + 1));
@@ -827,37 +814,34 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   if (big)
     for (int i = 1; i < e.n; i++) same = same && ev_base(r, e, i) == b0;
   k.block((big ? 27 : 2 * e.n + 1) + 12, [&](auto& o) {
-    if (!(PW_ABL & 512)) {
-      if (typ == PW_OP_SUB) {
-        if (big) {
-          o.put('[');
-          wr_dig(o, (uint32_t)e.n);
-          o.put(']');
-        } else {
-          for (int i = 0; i < e.n; i++) o.put(ev_sub(r, e, i));
-        }
-      }
-      if (typ != PW_OP_DEL) o.put(':');
+    if (typ == PW_OP_SUB) {
       if (big) {
         o.put('[');
         wr_dig(o, (uint32_t)e.n);
         o.put(']');
       } else {
-        for (int i = 0; i < e.n; i++) {
-          const uint8_t b = ev_base(r, e, i);
-          same = same && b == b0;
-          o.put(b);
-        }
+        for (int i = 0; i < e.n; i++) o.put(ev_sub(r, e, i));
       }
-      if (typ == PW_OP_DEL) o.put(':');
     }
+    if (typ != PW_OP_DEL) o.put(':');
+    if (big) {
+      o.put('[');
+      wr_dig(o, (uint32_t)e.n);
+      o.put(']');
+    } else {
+      for (int i = 0; i < e.n; i++) {
+        const uint8_t b = ev_base(r, e, i);
+        same = same && b == b0;
+        o.put(b);
+      }
+    }
+    if (typ == PW_OP_DEL) o.put(':');
     o.put('\t');
     wr_num(o, r.tab, (uint32_t)(in.tloc + 1));
     o.put('\t');
   });
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
-  if (PW_ABL & 1024) {
-  } else if (in.tmode == 2) {
+  if (in.tmode == 2) {
     emit_tctx_walk(k, r, typ, e.n, in.j, in.wd, in.qs, in.ts, in.ls);
   } else {
     k.block(10 + kMaxEv + 4, [&](auto& o) {
@@ -865,14 +849,9 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
         emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
       } else {
         uint32_t tw[6];
-        if (in.tx) {
-          const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
+        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
 #pragma unroll
-          for (int q = 0; q < 6; q++) tw[q] = t32[q];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 6; q++) tw[q] = in.txr[q];
-        }
+        for (int q = 0; q < 6; q++) tw[q] = t32[q];
         o.put_span(tw, (int)(tw[0] & 0xFFu));
       }
     });
@@ -888,7 +867,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     c0 = r.L - 9;
   }
   if (c0 < 0) c0 = 0;  // L < 9 is reported by the host
-  if (!(PW_ABL & 2048)) {
+  {
     uint32_t rw0 = 0, rw1 = 0, rw2 = 0;
     const int oc = c0 - r.qlo;
     if (r.qn == kQWin && oc >= 0 && oc + 16 <= kQWin) {  // one image from the window
@@ -929,8 +908,6 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       o.put_bytes(sv, sl);
       o.put('\t');
     });
-  } else {
-    k.put('\t');
   }
   // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
   int modseq_err = -1;
@@ -1091,22 +1068,25 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   const uint32_t* ops = A.ops + d.op_begin;
   const uint64_t qb = pre.qb;
   const uint8_t* R = A.qseq + qb;
+  // the render record keeps qb / 16 in 32 bits and the event slots [ev_begin, next ev_begin)
+  // must be a non-empty-or-empty range inside the batch (pwasm_amd.h, pw_report_args)
+  const bool layout_ok = (qb & 15u) == 0 && (qb >> 36) == 0 && pre.ev_next >= d.ev_begin && pre.ev_next <= A.n_ev_slots;
   const int L = pre.L;
   const bool rev = (d.ref & PW_REF_REVERSE) != 0;
   const int T = d.t_len;
   const uint32_t n_ops = d.n_ops;
   const uint64_t evb = d.ev_begin;
   const uint64_t ev_next = pre.ev_next;
-  const uint32_t nmax = (uint32_t)(ev_next - evb);
+  const uint32_t nmax = layout_ok ? (uint32_t)(ev_next - evb) : 0u;
   const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
 
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
   bool prev_sub = false;
   uint32_t ev = 0;
-  int err = PW_REC_OK, err_a = 0, err_b = 0, err_c = 0;
+  int err = layout_ok ? PW_REC_OK : PW_REC_LAYOUT, err_a = 0, err_b = 0, err_c = 0;
 
-  for (uint32_t sb = 0; sb < n_ops; sb += kSegOps) {
+  for (uint32_t sb = 0; layout_ok && sb < n_ops; sb += kSegOps) {
     const uint32_t nseg = (n_ops - sb) < (uint32_t)kSegOps ? (n_ops - sb) : (uint32_t)kSegOps;
     // ---- op words (2 per lane) + wave scans of the query / target / literal advances
     uint32_t wd[2];
@@ -1217,7 +1197,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           const uint32_t la = ls[k] >> 2, sh = ls[k] & 3u;
           const uint32_t w0 = lits32[la], w1 = lits32[la + 1], w2 = lits32[la + 2];
           Hot hh;
-          hh.qb = (uint32_t)qb;
+          hh.qb = (uint32_t)(qb >> 4);
           hh.L = L;
           hh.qp = d.offset + qs[k];
           hh.tloc = rev ? T - ts[k] : ts[k];
@@ -1234,7 +1214,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
             cd.ts = ts[k];
             W.cold[s] = cd;
           }
-          slow = !fast && !(PW_ABL & 32);
+          slow = !fast;
         }
       }
       // ---- target contexts that are not a plain query copy (another event within 5 bases,
@@ -1255,11 +1235,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     wave_sync();
   }
   if (ev > nmax) {  // host event bound violated (cannot happen: every head is a counted op)
-    err = 3;
+    err = PW_REC_OVERFLOW;
     ev = nmax;
   }
   // empty slots: merged '*' runs, or everything after a failure
-  const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;
+  const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;  // (none if !layout_ok)
   for (uint64_t s = h0 + lane; s < h1; s += kWave) W.hot[s].fn = kNoEv;
   if (lane == 0 && ev > 0 && err == PW_REC_OK) {
     const uint64_t s_last = rev ? evb + nmax - ev : evb + ev - 1;
@@ -1282,7 +1262,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   }
 }
 
-__global__ __launch_bounds__(kWave* kWaves, PW_INDEX_OCC) void index_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
@@ -1318,9 +1298,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_INDEX_OCC) void index_kernel(pw_r
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
-#if !PW_TXREG
   uint8_t txw[kWave * kTxL];        // per-lane copy of the event's tx record (tmode 1)
-#endif
   uint32_t ostart[kWave + 1];       // line starts in the page
   uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
 };
@@ -1358,7 +1336,7 @@ __device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
 // inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
 // chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).
-__global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
@@ -1368,9 +1346,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
   LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
   LDS uint8_t* my_line = w->line + lane * kLStride;
   LDS uint8_t* my_qw = w->qw + lane * kQStride;
-#if !PW_TXREG
   LDS uint8_t* my_tx = w->txw + lane * kTxL;
-#endif
   const bool skip = A.skip_codan != 0;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
 
@@ -1386,7 +1362,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       int n = (int)(h.fn & kNBig);
       // the pre-rendered target context (tctx_kernel) is loaded first: its latency overlaps the
       // query-window loads below
-      const bool use_tx = !(((h.fn >> 28) & 1u) | (uint32_t)(PW_ABL & 64));
+      const bool use_tx = !((h.fn >> 28) & 1u);
       v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
       if (use_tx) {
         const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
@@ -1395,9 +1371,9 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       }
       Rec r;
       r.lits = A.lits;
-      r.R = A.qseq + h.qb;
+      r.R = A.qseq + ((uint64_t)h.qb << 4);
       r.L = h.L;
-      r.NS = A.next_stop ? A.next_stop + h.qb : nullptr;
+      r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;
       r.tab = tp;
       r.opw = nullptr;
       r.op_lo = 0;
@@ -1437,7 +1413,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       }
       r.qw = my_qw;
       r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
-      r.qn = (PW_ABL & 4) ? 0 : kQWin;
+      r.qn = kQWin;
       EvIn in;
       in.typ = typ;
       in.n = n;
@@ -1449,19 +1425,14 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       in.rl = (int)((h.fn >> 20) & 7u);
       // loads issued ahead of the line (their latency overlaps the query-window staging): the
       // pre-rendered target context and the next-stop entry the indel stop scan ends on
-#if PW_TXREG
-      in.tx = nullptr;
-      in.txr[0] = t0.x, in.txr[1] = t0.y, in.txr[2] = t0.z, in.txr[3] = t0.w, in.txr[4] = t1.x, in.txr[5] = t1.y;
-#else
       in.tx = my_tx;
       if (use_tx) {
         LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(my_tx);
         d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
         d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
       }
-#endif
       in.ns_pre = kNsNone;
-      if (typ != PW_OP_SUB && r.NS && !skip && !(PW_ABL & 128)) {
+      if (typ != PW_OP_SUB && r.NS && !skip) {
         const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
         const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
         const int k0 = rl + dl + (15 - a - x);
@@ -1474,12 +1445,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
       k.junk = my_line + kLine;  // (the stride's spare bytes)
       k.pos = 0;
       int rel = 0;
-#if PW_ABL & 1
-      const int merr = -1;
-      k.pos = 76;
-#else
-      const int merr = emit_event(k, r, in, skip || (PW_ABL & 2), rel);
-#endif
+      const int merr = emit_event(k, r, in, skip, rel);
       linelen = k.pos;
       if (merr >= 0) {  // modseq error: first failing event of the record in output order
         const uint32_t ai = rec_of_slot(A, s);
@@ -1530,7 +1496,7 @@ __global__ __launch_bounds__(kWave* kWaves, PW_RENDER_OCC) void render_kernel(pw
         A.results[ai].page_last = (uint32_t)c;
       }
     }
-    if (ok && B > 0 && !(PW_ABL & 16)) {
+    if (ok && B > 0) {
       // long lines -> fixup list (one wave-aggregated atomic)
       const bool need = linelen > kLine;
       const uint64_t nm = __ballot(need);
@@ -1664,7 +1630,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         Rec r;
         r.ops = A.ops + p0.x;
         r.lits = A.lits;
-        r.R = A.qseq + h.qb;
+        r.R = A.qseq + ((uint64_t)h.qb << 4);
         r.L = h.L;
         r.NS = nullptr;
         r.tab = tp;
@@ -1767,9 +1733,9 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     int ne = (int)(h.fn & kNBig);
     Rec r;
     r.lits = A.lits;
-    r.R = A.qseq + h.qb;
+    r.R = A.qseq + ((uint64_t)h.qb << 4);
     r.L = h.L;
-    r.NS = A.next_stop ? A.next_stop + h.qb : nullptr;
+    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;
     r.tab = tp;
     r.opw = nullptr;
     r.op_lo = 0;
@@ -1826,8 +1792,6 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     in.ll = (int)((h.fn >> 23) & 7u);
     in.rl = (int)((h.fn >> 20) & 7u);
     in.tx = me->tx;
-#pragma unroll
-    for (int q = 0; q < 6; q++) in.txr[q] = 0;
     in.ns_pre = kNsNone;
     in.j = in.wd = 0;
     in.qs = in.ts = 0;
@@ -1845,7 +1809,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W)
   if (ai >= A.n_alns) return;
   pw_aln_result r = A.results[ai];
   if (W.ctr[2]) {
-    r.err = 3;
+    r.err = PW_REC_OVERFLOW;
   } else if (r.err == PW_REC_OK) {
     if (r.n_events) {  // bytes of the lines, across the pages they span
       uint64_t len;
@@ -1964,7 +1928,7 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
     hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
-    if (rg > (uint64_t)ncu * PW_RENDER_OCC) rg = (uint64_t)ncu * PW_RENDER_OCC;
+    if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);
   }

@@ -1,0 +1,173 @@
+"""GPU parity at the benchmarked sizes and on the rare device paths.
+
+* cfg2 in full (100k records, -G -C), cfg3 at 100k records, cfg4 at real 1-5 Mb contigs (five
+  records, auto -F, whole report diffed; the smallest also with -G -C), cfg5 at full size
+  (200 rows x 1M columns, removeConsGaps=false): HIP CLI vs oracle, byte for byte.
+* cfg4 property checks that do not depend on the oracle: one event line per cs event head after
+  the S-merge (pafreport.cpp:556-560), rloc non-decreasing within a record (tdiffs.Reverse()
+  for '-' records, :643), 9-nt query contexts (:721-733), target contexts <= 22 bytes or
+  first5[n]last5 (:918-927).
+* Event lengths >= 2^19 - 1 (the render record's saturated length field: the Cold record /
+  op-stream path), and the modseq check failing on a reverse-strand substitution at a 'U' base
+  (comp is not an involution there: U -> A -> T; pafreport.cpp:811-814).
+Parity bar: bit-exact."""
+import os
+import random
+import re
+
+import pytest
+
+from conftest import CLI, GA_CLI, GA_ORACLE, ORACLE, SYNTH, run, synth_paf
+from test_gpu_parity import same
+
+pytestmark = pytest.mark.gpu
+
+
+def test_cfg2_full(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 2)
+    out = same(["-G", "-C", "-r", fa, paf])
+    assert out.count(b">") == 100000
+
+
+def test_cfg3_100k(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 3, scale=0.01)
+    out = same(["-G", "-C", "-r", fa, paf])
+    assert out.count(b">") >= 100000
+
+
+def _cs_heads(cs):
+    """Event heads of a short cs string after the S-merge of directly consecutive '*' ops."""
+    n, prev_sub = 0, False
+    for m in re.finditer(r":\d+|\*[a-z]{2}|[-+][a-z]+", cs):
+        op = m.group(0)[0]
+        if op == ":":
+            if m.group(0) != ":0":  # (a ':0' between '*' ops keeps them contiguous)
+                prev_sub = False
+            continue
+        if op == "*":
+            if not prev_sub:
+                n += 1
+            prev_sub = True
+        else:
+            n += 1
+            prev_sub = False
+    return n
+
+
+def _check_report_properties(paf, report):
+    recs = [ln.split("\t") for ln in open(paf).read().splitlines() if ln and not ln.startswith("#")]
+    blocks = report.decode().split(">")[1:]
+    assert len(blocks) == len(recs)
+    for f, blk in zip(recs, blocks):
+        cs = next(x[5:] for x in f if x.startswith("cs:Z:"))
+        lines = blk.rstrip("\n").split("\n")[1:]
+        assert len(lines) == _cs_heads(cs)
+        last = -1
+        for ln in lines:
+            c = ln.split("\t")
+            assert c[0] in ("S", "I", "D")
+            rloc = int(c[1])
+            assert rloc >= last
+            last = rloc
+            assert len(c[6]) == 9 and c[6].isupper()
+            assert len(c[5]) <= 22 or re.fullmatch(r"[A-Za-z]{5}\[\d+\][A-Za-z]{5}", c[5])
+
+
+def test_cfg4_megabase_contigs(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 4, extra=["--ncds", 5, "--recs", 1])
+    lens = [int(ln.split("\t")[1]) for ln in open(paf)]
+    assert len(lens) == 5 and min(lens) >= 1000000
+    out = same(["-r", fa, paf], timeout=600)  # auto -F (FASTA > 120 kB): the config's mode
+    assert out.count(b"\n") > 50000
+    _check_report_properties(paf, out)
+    # the smallest contig with the codon pass forced on (the oracle's O(L)-per-event suffix
+    # copies, pafreport.cpp:908, keep this to one record)
+    one = tmp_path / "one.paf"
+    lines = open(paf).read().splitlines(keepends=True)
+    one.write_text(lines[lens.index(min(lens))])
+    same(["-G", "-C", "-r", fa, str(one)], timeout=600)
+
+
+def test_cfg5_full_layout(built, tmp_path):
+    lay = tmp_path / "l.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--seed", 5, "--out", lay])
+    assert rc == 0, err
+    ro, _, eo = run([GA_ORACLE, lay, tmp_path / "o.pwc"])
+    rp, _, ep = run([GA_CLI, lay, tmp_path / "p.pwc"])
+    assert (rp, ep) == (ro, eo) and ro == 0
+    a, b = tmp_path / "o.pwc", tmp_path / "p.pwc"
+    assert os.path.getsize(a) == os.path.getsize(b)
+    with open(a, "rb") as x, open(b, "rb") as y:
+        while True:
+            u, v = x.read(1 << 24), y.read(1 << 24)
+            assert u == v
+            if not u:
+                break
+
+
+# ---------------------------------------------------------------- rare device paths
+def _rand_cds(rng, n):
+    s = "ATG" + "".join(rng.choice("ACGT") for _ in range(n - 6))
+    return s + "TAA"
+
+
+def _comp(s):
+    return s.translate(str.maketrans("ACGTU", "TGCAA"))[::-1]
+
+
+def _paf_line(q, ql, qs, qe, strand, t, tl, ts, te, cg, cs):
+    return "\t".join(map(str, [q, ql, qs, qe, strand, t, tl, ts, te, 10, 20, 60, "NM:i:1", "AS:i:5",
+                               f"cg:Z:{cg}", f"cs:Z:{cs}"])) + "\n"
+
+
+def test_event_length_past_render_field(built, tmp_path):
+    """Deletions / insertions of >= 2^19 - 1 bases: the render record's length field saturates
+    and the kernels take the event length from the op stream via the Cold record."""
+    rng = random.Random(99)
+    L = 600000
+    q = _rand_cds(rng, L)
+    (tmp_path / "q.fa").write_text(f">big\n{q}\n")
+    big = 530000
+    a, b = 30000, 30000 + big
+    ins = "".join(rng.choice("acgt") for _ in range(big))
+    lines = [
+        # forward: a deletion of `big` query bases (cs '+', event 'D') and a substitution after it
+        _paf_line("big", L, 0, L, "+", "t1", 2 * L, 100, 100 + L - big, f"{a}M{big}I{L - b}M",
+                  f":{a}+{q[a:b].lower()}:10*{'c' if q[b + 10] != 'C' else 'g'}{q[b + 10].lower()}:{L - b - 11}"),
+        # forward: an insertion of `big` target bases (cs '-', event 'I')
+        _paf_line("big", L, 0, L, "+", "t2", 2 * L, 100, 100 + L + big, f"{a}M{big}D{L - a}M",
+                  f":{a}-{ins}:{L - a}"),
+        # reverse strand: both on the aligned (reverse-complement) strand
+        _paf_line("big", L, 0, L, "-", "t3", 2 * L, 100, 100 + L - big, f"{a}M{big}I{L - b}M",
+                  f":{a}+{_comp(q)[a:b].lower()}:{L - b}"),
+        _paf_line("big", L, 0, L, "-", "t4", 2 * L, 100, 100 + L + big, f"{a}M{big}D{L - a}M",
+                  f":{a}-{ins}:{L - a}"),
+    ]
+    (tmp_path / "a.paf").write_text("".join(lines))
+    for flags in (["-G", "-C"], []):
+        out = same([*flags, "-r", "q.fa", "a.paf"], cwd=str(tmp_path), timeout=600)
+        assert out.count(b">") == 4 and b"[530000]" in out
+
+
+def test_modseq_mismatch_reverse_u(built, tmp_path):
+    """A reverse-strand substitution at a 'U' of the query passes the cs base check (comp(U) =
+    A on the aligned strand) but fails predictImpact's modseq check (comp(A) = T != U): the
+    reference prints the lines before it and exits 1."""
+    rng = random.Random(5)
+    q = list(_rand_cds(rng, 60))
+    q[30] = "U"
+    q = "".join(q)
+    (tmp_path / "q.fa").write_text(f">qu\n{q}\n")
+    rc_q = _comp(q)  # aligned strand of '-' records
+    assert rc_q[29] == "A"
+    alt = lambda c: "t" if c.upper() != "T" else "c"  # noqa: E731
+    cs = f":10*{alt(rc_q[10])}{rc_q[10].lower()}:18*{alt(rc_q[29])}{rc_q[29].lower()}:30"
+    lines = [
+        _paf_line("qu", 60, 0, 60, "+", "t0", 200, 10, 70, "60M", f":5*{alt(q[5])}{q[5].lower()}:54"),
+        _paf_line("qu", 60, 0, 60, "-", "t1", 200, 10, 70, "60M", cs),
+        _paf_line("qu", 60, 0, 60, "+", "t2", 200, 10, 70, "60M", ":60"),
+    ]
+    (tmp_path / "a.paf").write_text("".join(lines))
+    rc, out, err = run([ORACLE, "-r", "q.fa", "a.paf"], cwd=str(tmp_path))
+    assert rc == 1 and b"modseq" in err
+    same(["-r", "q.fa", "a.paf"], cwd=str(tmp_path))
