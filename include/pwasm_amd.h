@@ -260,6 +260,35 @@ int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_a
                          const pw_page* pages_host, const char* path);
 void pw_batch_free(pw_batch* b);
 
+/* ---------------------------------------------------------------- multi-GPU
+ * Shard by target genome: rank `shard` of `nshards` packs only the PAF lines whose target name
+ * (column 6) has crc32 % nshards == shard (lines with fewer than 7 columns: shard 0; comment
+ * lines: nowhere).  Gene-mode q~t dedupe (pafreport.cpp:319-334) is keyed by the target, so it
+ * stays shard-local; every item keeps its global input line.  pw_batch_from_files(...) ==
+ * pw_batch_from_files_shard(..., 0, 1, ...). */
+pw_batch* pw_batch_from_files_shard(const char* fasta, const char* paf, uint32_t flags, uint32_t shard,
+                                    uint32_t nshards, char* errbuf, size_t errlen);
+/* Merge the PWI1 item streams of all shards (pw_batch_write_items) by global input line up to
+ * the first item that ends the run; stdout bytes to out_path (NULL = stdout), stderr bytes to
+ * err_path (NULL = stderr).  Returns the exit code the single-process run ends with (>= 0) or a
+ * negative PW_E_* status. */
+int pw_items_merge(const char* const* paths, uint32_t n, const char* out_path, const char* err_path);
+
+/* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
+ * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its
+ * genome index (first-appearance order) and aligned target bases.  Device: one row per genome
+ * from the per-record results of pw_report_events (rows are overwritten).  The multi-GPU driver
+ * all-gathers the rows of every rank (RCCL) before rank 0 writes the merged table. */
+typedef struct pw_genome_row {
+  uint32_t records;   /* alignments to this target */
+  uint32_t events;    /* report event lines */
+  uint64_t t_bases;   /* aligned target bases (sum of tend - tstart) */
+} pw_genome_row;
+uint32_t pw_batch_genomes(pw_batch* b, uint64_t* names_bytes);
+int pw_batch_genomes_get(const pw_batch* b, uint32_t* genome_of, int32_t* t_aln, char* names);
+int pw_genome_table(const pw_aln_result* results, const uint32_t* genome_of, const int32_t* t_aln, uint32_t n_alns,
+                    pw_genome_row* rows, uint32_t n_genomes, void* stream);
+
 const char* pw_version(void);
 
 #ifdef __cplusplus

@@ -126,6 +126,14 @@ _SIGS = {
     "pw_batch_free": (None, [ctypes.c_void_p]),
     "pw_version": (ctypes.c_char_p, []),
     "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
+    "pw_batch_from_files_shard": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                                                    ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    "pw_items_merge": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32, ctypes.c_char_p,
+                                      ctypes.c_char_p]),
+    "pw_batch_genomes": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
 }
 
 _lib = None
@@ -166,10 +174,11 @@ def pack_cs(cs: str, offset: int, qlen: int):
 class HostBatch:
     """A PAF batch packed by the C++ pre-pass (pw_batch_from_files), arrays viewable as numpy."""
 
-    def __init__(self, fasta: str, paf: str, flags: int = 0):
+    def __init__(self, fasta: str, paf: str, flags: int = 0, shard: int = 0, nshards: int = 1):
+        """shard / nshards: pack only this rank's lines (target-name hash, pw_batch_from_files_shard)."""
         L = lib()
         err = ctypes.create_string_buffer(4096)
-        h = L.pw_batch_from_files(fasta.encode(), paf.encode(), flags, err, 4096)
+        h = L.pw_batch_from_files_shard(fasta.encode(), paf.encode(), flags, shard, nshards, err, 4096)
         if not h:
             raise RuntimeError("pw_batch_from_files: " + err.value.decode(errors="replace"))
         self._h = h
@@ -209,6 +218,22 @@ class HostBatch:
     def write_items_from(self, dev: dict, path: str) -> int:
         return self.write_items(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), dev["pages"].cpu().numpy(),
                                 path)
+
+    def genomes(self):
+        """-> (genome index per record [n_alns] uint32, aligned target bases [n_alns] int32,
+        target names) for the per-genome tables."""
+        import numpy as np
+        L = lib()
+        nb = ctypes.c_uint64(0)
+        ng = int(L.pw_batch_genomes(self._h, ctypes.byref(nb)))
+        n = int(self.view.n_alns)
+        gof = np.zeros(max(n, 1), dtype=np.uint32)
+        taln = np.zeros(max(n, 1), dtype=np.int32)
+        names = ctypes.create_string_buffer(max(int(nb.value), 1))
+        if L.pw_batch_genomes_get(self._h, gof.ctypes.data, taln.ctypes.data, names) != 0:
+            raise RuntimeError("pw_batch_genomes_get failed")
+        nm = names.raw[: int(nb.value)].split(b"\0")[:ng]
+        return gof[:n], taln[:n], nm
 
     def close(self):
         if self._h:
@@ -286,6 +311,16 @@ def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
     dev["results"] = torch.empty(max(int(v.n_alns), 1) * ctypes.sizeof(AlnResult), dtype=torch.uint8,
                                  device=device)
     return dev
+
+
+def items_merge(paths, out_path=None, err_path=None) -> int:
+    """pw_items_merge: the merged stdout / stderr of all shards' item streams; returns the exit code."""
+    arr = (ctypes.c_char_p * len(paths))(*[str(p).encode() for p in paths])
+    return lib().pw_items_merge(arr, len(paths), str(out_path).encode() if out_path else None,
+                                str(err_path).encode() if err_path else None)
+
+
+GENOME_ROW = 16  # sizeof(pw_genome_row)
 
 
 def version() -> str:

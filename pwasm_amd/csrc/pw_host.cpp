@@ -4,13 +4,23 @@
 // reference's order, from the per-record results the GPU returns; there is no CPU fallback:
 // without a usable gfx950 device the CLI stops with an error.
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <future>
+#include <mutex>
 #include <string>
+#include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -33,16 +43,32 @@ std::string strf(const char* fmt, ...) {
   return s;
 }
 
-// gclib parseInt: skip blanks, optional sign, digits; false (p unchanged) if no digit.
-bool parse_int(const char*& p, int& out) {
+// gclib parseInt on the string [p, end): skip blanks, optional sign, digits; false (p
+// unchanged) if no digit.
+bool parse_int(const char*& p, const char* end, int& out) {
   const char* q = p;
-  while (*q == ' ' || *q == '\t') q++;
+  while (q < end && (*q == ' ' || *q == '\t')) q++;
   const char* start = q;
-  if (*q == '-' || *q == '+') q++;
+  if (q < end && (*q == '-' || *q == '+')) q++;
   const char* dig = q;
-  while (*q >= '0' && *q <= '9') q++;
+  while (q < end && *q >= '0' && *q <= '9') q++;
   if (q == dig) return false;
-  out = (int)strtol(start, nullptr, 10);
+  if (q - dig <= 9) {  // cannot overflow: the value directly
+    int v = 0;
+    for (const char* d = dig; d < q; d++) v = v * 10 + (*d - '0');
+    out = *start == '-' ? -v : v;
+    p = q;
+    return true;
+  }
+  char tmp[48];  // strtol on a bounded copy (same overflow behaviour as the reference's strtol)
+  const size_t n = (size_t)(q - start);
+  if (n < sizeof tmp) {
+    memcpy(tmp, start, n);
+    tmp[n] = 0;
+    out = (int)strtol(tmp, nullptr, 10);
+  } else {
+    out = (int)(*start == '-' ? LONG_MIN : LONG_MAX);
+  }
   p = q;
   return true;
 }
@@ -63,8 +89,9 @@ constexpr uint64_t kBoundSub = 190, kBoundIndel = 140;
 // Mirrors the cs loop of PAFAlignment::PAFAlignment (pafreport.cpp:536-626) without touching
 // the query: only lengths, literal bytes and the positions needed for the reference's
 // bounds-free reads are produced.
-extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap,
-                          uint8_t* lits, size_t lits_cap, pw_cs_totals* tot, int32_t* err_pos) {
+// cs = [cs, cs_end): the tag's field (the reference strdup's it out of the split line).
+static int pack_cs_n(const char* cs, const char* cs_end, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap,
+                     uint8_t* lits, size_t lits_cap, pw_cs_totals* tot, int32_t* err_pos) {
   if (!cs || !tot) return PW_CS_PARSE;
   int qpos = 0, tpos = 0;
   uint32_t nops = 0, nlits = 0, nev = 0;
@@ -80,13 +107,13 @@ extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t
     ops[nops++] = w;
     return true;
   };
-  while (*p != 0 && rc == PW_CS_OK) {
+  while (p < cs_end && rc == PW_CS_OK) {
     const char op = *p;
     p++;
     switch (op) {
       case ':': {
         int cl = 0;
-        if (!parse_int(p, cl)) {
+        if (!parse_int(p, cs_end, cl)) {
           fail(PW_CS_PARSE, p);
           break;
         }
@@ -105,7 +132,7 @@ extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t
         break;
       }
       case '*': {
-        if (p[0] == 0 || p[1] == 0) {
+        if (p + 2 > cs_end || p[0] == 0 || p[1] == 0) {
           fail(PW_CS_PARSE, p);
           break;
         }
@@ -129,7 +156,7 @@ extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t
       }
       case '-': {
         const char* s0 = p;
-        while (is_alpha((unsigned char)*p)) p++;
+        while (p < cs_end && is_alpha((unsigned char)*p)) p++;
         const uint32_t n = (uint32_t)(p - s0);
         if (n == 0) {
           fail(PW_CS_EMPTY, p);
@@ -147,7 +174,7 @@ extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t
       }
       case '+': {
         const char* s0 = p;
-        while (is_alpha((unsigned char)*p)) p++;
+        while (p < cs_end && is_alpha((unsigned char)*p)) p++;
         const int n = (int)(p - s0);
         if (n == 0) {
           fail(PW_CS_EMPTY, p);
@@ -184,15 +211,74 @@ extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t
   return rc;
 }
 
+extern "C" int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap,
+                          uint8_t* lits, size_t lits_cap, pw_cs_totals* tot, int32_t* err_pos) {
+  return pack_cs_n(cs, cs ? cs + strlen(cs) : nullptr, offset, qlen, ops, ops_cap, lits, lits_cap, tot, err_pos);
+}
+
 // ================================================================= batch structures
 namespace {
+
+// Growable array of trivially copyable T without value-initialisation (the batch arrays are
+// written once, in parallel, after being sized).
+template <class T>
+struct PodVec {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;
+  PodVec() = default;
+  PodVec(PodVec&& o) noexcept { swap(o); }
+  PodVec(const PodVec&) = delete;
+  PodVec& operator=(const PodVec&) = delete;
+  ~PodVec() { free(p); }
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    size_t nc = std::max(c, cap + cap / 2 + 16);
+    T* q = (T*)realloc(p, nc * sizeof(T));
+    if (!q) {
+      fprintf(stderr, "pafreport: host allocation failed\n");
+      abort();
+    }
+    p = q;
+    cap = nc;
+  }
+  void resize(size_t m) {
+    reserve(m);
+    n = m;
+  }
+  void clear() { n = 0; }
+  void push_back(const T& v) {
+    if (n == cap) reserve(n + 1);
+    p[n++] = v;
+  }
+  void append(const T* v, size_t k) {
+    reserve(n + k);
+    if (k) memcpy(p + n, v, k * sizeof(T));
+    n += k;
+  }
+  void swap(PodVec& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+  }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T* data() { return p; }
+  const T* data() const { return p; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T& back() { return p[n - 1]; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
 
 struct QueryDb {
   std::vector<std::string> ids;
   std::vector<uint64_t> off;
   std::vector<int32_t> len;
   std::vector<uint8_t> seq;  // upper case (GASeq::allupper, pafreport.cpp:350)
-  std::unordered_map<std::string, int> index;
+  std::unordered_map<std::string_view, int> index;  // first record of each id (built after load)
   std::vector<uint8_t> acgt;  // per query: all bases in {A,C,G,T}
   bool all_acgt(int qi) const { return acgt[qi] != 0; }
   static bool is_acgt_byte(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
@@ -219,12 +305,10 @@ struct QueryDb {
       if (!l.empty() && l[0] == '>') {
         size_t e = 1;
         while (e < l.size() && !isspace((unsigned char)l[e])) e++;
-        std::string id = l.substr(1, e - 1);
         if (have) close_record();
-        ids.push_back(id);
+        ids.push_back(l.substr(1, e - 1));
         off.push_back(seq.size());
         len.push_back(0);
-        if (!index.count(id)) index.emplace(id, (int)ids.size() - 1);
         have = true;
       } else if (have) {
         for (char c : l) seq.push_back(up((unsigned char)c));
@@ -242,23 +326,78 @@ struct QueryDb {
     if (!line.empty()) flush_line(line);
     if (have) close_record();
     fclose(f);
+    index.reserve(ids.size() * 2);
+    for (size_t i = 0; i < ids.size(); i++) index.emplace(std::string_view(ids[i]), (int)i);
     return true;
   }
 };
 
+// Worker threads of the host pre-pass: PW_THREADS, else OMP_NUM_THREADS, else the CPUs this
+// process may run on (at most 16: a GPU box gives each GPU a 16-CPU share).
+int host_threads() {
+  for (const char* v : {"PW_THREADS", "OMP_NUM_THREADS"}) {
+    const char* e = getenv(v);
+    if (e && atoi(e) > 0) return std::min(atoi(e), 256);
+  }
+  cpu_set_t cs;
+  int n = 0;
+  if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
+  if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(n, 16));
+}
+
+template <class F>
+void parallel_for(int nt, F&& f) {
+  if (nt <= 1) {
+    f(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve((size_t)nt - 1);
+  for (int t = 1; t < nt; t++) th.emplace_back([&f, t] { f(t); });
+  f(0);
+  for (auto& x : th) x.join();
+}
+
+// CRC-32 (IEEE, as zlib.crc32): the shard of a PAF line is crc32(target name) % world
+// (pwasm_amd/shard.py:shard_of).
+uint32_t crc32_ieee(const char* p, size_t n) {
+  static uint32_t tab[256];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[i] = c;
+    }
+  });
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = tab[(c ^ (uint8_t)p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+uint64_t fnv1a(const char* p, size_t n, uint64_t h = 1469598103934665603ull) {
+  for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 1099511628211ull;
+  return h;
+}
+
 struct Options {
   bool fullgenome = false, skip_codan = false, verbose = false;
   bool single_query_gene = false;  // rlabel "" (pafreport.cpp:378-379)
+  uint32_t shard = 0, nshards = 1;  // multi-GPU: only lines whose target hashes to `shard`
 };
 
-struct RecHost {
-  uint32_t line_off, line_len;  // original line in the batch text (for messages)
-  uint32_t hdr_off, hdr_len;    // header line in the header pool
-  int32_t pre_msg = -1;         // message index: fatal before the cs loop
-  int32_t cs_msg = -1;          // fatal from the host cs parse (after GPU mismatch)
-  int32_t post_msg = -1;        // fatal from the CIGAR loop / length checks
-  uint16_t n_softclip = 0;
-  int32_t qlen = 0;
+struct RecHost {                // (trivial: lives in PodVec; pack_line sets every field)
+  uint64_t line_off;            // original line in the batch buffer (NUL-terminated; messages)
+  uint64_t hdr_off;             // header line in the header pool
+  uint32_t hdr_len;
+  int32_t pre_msg;              // message index: fatal before the cs loop (-1: none)
+  int32_t cs_msg;               // fatal from the host cs parse (after GPU mismatch)
+  int32_t post_msg;             // fatal from the CIGAR loop / length checks
+  uint16_t n_softclip;
+  int32_t qlen;
+  uint32_t tname_off, tname_len;  // target name (per-genome tables of the multi-GPU driver)
+  int32_t t_aln;                // aligned target bases (t_alnend - t_alnstart)
 };
 
 // Ordered log of what a batch prints: messages, records, a terminating fatal.
@@ -268,19 +407,28 @@ struct LogItem {
   uint64_t line;  // 0-based input line it came from (shard merge order)
 };
 
+struct LineRef {
+  uint64_t off;  // into Batch::buf
+  uint32_t len;
+};
+
+// One batch: its input lines (the buffer keeps them, NUL-terminated, for messages) and the
+// packed device arrays.  A thread's share of a batch is packed into a Batch of its own
+// (without buf) and then appended here (Batch::append).
 struct Batch {
-  std::string text;     // raw lines of this batch (messages quote them)
-  std::string hdr;      // report headers
+  PodVec<char> buf;
+  PodVec<LineRef> lines;
+  uint64_t line0 = 0;   // global input line of lines[0]
+  PodVec<char> hdr;     // report headers
   std::vector<std::string> msgs;
-  std::vector<LogItem> log;
-  std::vector<RecHost> recs;
-  std::vector<pw_aln_desc> desc;
-  std::vector<uint32_t> ops;
-  std::vector<uint8_t> lits;
+  PodVec<LogItem> log;
+  PodVec<RecHost> recs;
+  PodVec<pw_aln_desc> desc;
+  PodVec<uint32_t> ops;
+  PodVec<uint8_t> lits;
   uint64_t text_total = 0, n_events_max = 0;
   bool fatal = false;
-  void clear() {
-    text.clear();
+  void clear_out() {
     hdr.clear();
     msgs.clear();
     log.clear();
@@ -290,6 +438,11 @@ struct Batch {
     lits.clear();
     text_total = n_events_max = 0;
     fatal = false;
+  }
+  void clear() {
+    buf.clear();
+    lines.clear();
+    clear_out();
   }
   uint32_t add_msg(std::string m) {
     msgs.push_back(std::move(m));
@@ -303,97 +456,332 @@ struct Batch {
   }
 };
 
+// Append parts (packed by threads over consecutive line ranges) to `b`, in order, up to and
+// including the first part that ended in a fatal error; the offsets each part holds into its
+// own arrays are rebased in parallel.
+void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
+  size_t np = parts.size();
+  for (size_t i = 0; i < parts.size(); i++)
+    if (parts[i].fatal) {
+      np = i + 1;
+      break;
+    }
+  std::vector<uint64_t> o_desc(np + 1), o_ops(np + 1), o_lits(np + 1), o_hdr(np + 1), o_msg(np + 1), o_log(np + 1),
+      o_ev(np + 1), o_txt(np + 1);
+  for (size_t i = 0; i < np; i++) {
+    const Batch& p = parts[i];
+    o_desc[i + 1] = o_desc[i] + p.desc.size();
+    o_ops[i + 1] = o_ops[i] + p.ops.size();
+    o_lits[i + 1] = o_lits[i] + p.lits.size();
+    o_hdr[i + 1] = o_hdr[i] + p.hdr.size();
+    o_msg[i + 1] = o_msg[i] + p.msgs.size();
+    o_log[i + 1] = o_log[i] + p.log.size();
+    o_ev[i + 1] = o_ev[i] + p.n_events_max;
+    o_txt[i + 1] = o_txt[i] + p.text_total;
+  }
+  const size_t d0 = b.desc.size(), op0 = b.ops.size(), l0 = b.lits.size(), h0 = b.hdr.size(), m0 = b.msgs.size(),
+               g0 = b.log.size();
+  const uint64_t e0 = b.n_events_max;
+  b.desc.resize(d0 + o_desc[np]);
+  b.recs.resize(d0 + o_desc[np]);
+  b.ops.resize(op0 + o_ops[np]);
+  b.lits.resize(l0 + o_lits[np]);
+  b.hdr.resize(h0 + o_hdr[np]);
+  b.msgs.resize(m0 + o_msg[np]);
+  b.log.resize(g0 + o_log[np]);
+  b.n_events_max += o_ev[np];
+  b.text_total += o_txt[np];
+  std::atomic<size_t> next{0};
+  parallel_for(std::min<int>(nt, (int)np), [&](int) {
+    for (size_t i; (i = next.fetch_add(1)) < np;) {
+      Batch& p = parts[i];
+      const uint32_t dop = (uint32_t)(op0 + o_ops[i]), dlit = (uint32_t)(l0 + o_lits[i]);
+      const uint64_t dev = e0 + o_ev[i];
+      for (size_t k = 0; k < p.desc.size(); k++) {
+        pw_aln_desc d = p.desc[k];
+        d.op_begin += dop;
+        d.lit_begin += dlit;
+        d.ev_begin += dev;
+        b.desc[d0 + o_desc[i] + k] = d;
+        RecHost r = p.recs[k];
+        r.hdr_off += h0 + o_hdr[i];
+        const int32_t dm = (int32_t)(m0 + o_msg[i]);
+        if (r.pre_msg >= 0) r.pre_msg += dm;
+        if (r.cs_msg >= 0) r.cs_msg += dm;
+        if (r.post_msg >= 0) r.post_msg += dm;
+        b.recs[d0 + o_desc[i] + k] = r;
+      }
+      if (!p.ops.empty()) memcpy(&b.ops[op0 + o_ops[i]], p.ops.data(), p.ops.size() * 4);
+      if (!p.lits.empty()) memcpy(&b.lits[l0 + o_lits[i]], p.lits.data(), p.lits.size());
+      if (!p.hdr.empty()) memcpy(&b.hdr[h0 + o_hdr[i]], p.hdr.data(), p.hdr.size());
+      for (size_t k = 0; k < p.msgs.size(); k++) b.msgs[m0 + o_msg[i] + k] = std::move(p.msgs[k]);
+      for (size_t k = 0; k < p.log.size(); k++) {
+        LogItem it = p.log[k];
+        it.idx += (uint32_t)(it.kind == 1 ? d0 + o_desc[i] : m0 + o_msg[i]);
+        b.log[g0 + o_log[i] + k] = it;
+      }
+    }
+  });
+  b.fatal = b.fatal || parts[np - 1].fatal;
+}
+
 const char* CIGAR_ERROR = "Error parsing cigar string from line: %s (cigar position: %s)\n";
 const char* CS_ERROR = "Error parsing cs string from line: %s (cs position: %s)\n";
+
+// Line classes of the pre-scan (kind) and the gene-mode dedupe verdict (dup).
+enum : uint8_t { kLineSkip = 0, kLineShort = 1, kLineSelf = 2, kLineRec = 3 };
+enum : uint8_t { kDupNo = 0, kDupSilent = 1, kDupWarn = 2 };
+struct LineInfo {
+  uint8_t kind, dup;
+  uint64_t khash;  // hash of "q~t" (gene mode)
+};
+
+// Pre-scan of one line: enough fields to classify it (pafreport.cpp:304-317); the shard filter.
+// Field starts follow strsplit (a field starts after every tab that is not the last byte).
+LineInfo classify(const char* s, uint32_t n, const Options& opt) {
+  LineInfo li{kLineSkip, kDupNo, 0};
+  if (n > 0 && s[0] == '#') return li;
+  uint32_t fs[16];
+  int nf = 0;
+  bool after = true;
+  for (uint32_t i = 0; i < n && nf < 16; i++) {
+    if (after) fs[nf++] = i;
+    after = s[i] == '\t';
+  }
+  if (opt.nshards > 1) {  // shard.py:shard_of — column 6 of a Python split on tabs, else rank 0
+    const char* t5 = nullptr;
+    size_t t5n = 0;
+    int tabs = 0;
+    for (uint32_t i = 0; i < n; i++)
+      if (s[i] == '\t') {
+        tabs++;
+        if (tabs == 5) t5 = s + i + 1;
+        if (tabs == 6) {
+          t5n = (size_t)(s + i - t5);
+          break;
+        }
+      }
+    const uint32_t sh = tabs >= 6 ? crc32_ieee(t5, t5n) % opt.nshards : 0u;
+    if (sh != opt.shard) return li;
+  }
+  if (nf < 15) {
+    li.kind = kLineShort;
+    return li;
+  }
+  auto fend = [&](int k) -> uint32_t {
+    const char* e = (const char*)memchr(s + fs[k], '\t', n - fs[k]);
+    return e ? (uint32_t)(e - s) : n;
+  };
+  const uint32_t q0 = fs[0], q1 = fend(0), t0 = fs[5], t1 = fend(5);
+  if (q1 - q0 == t1 - t0 && memcmp(s + q0, s + t0, q1 - q0) == 0) {
+    li.kind = kLineSelf;
+    return li;
+  }
+  li.kind = kLineRec;
+  if (!opt.fullgenome) li.khash = fnv1a(s + t0, t1 - t0, fnv1a("~", 1, fnv1a(s + q0, q1 - q0)));
+  return li;
+}
 
 struct Packer {
   const QueryDb* qdb;
   Options opt;
-  std::unordered_map<std::string, int> alnpairs;  // q~t (gene mode), persists across batches
-  std::vector<char*> t;
+  int nt = 1;
+  // q~t pairs seen (gene mode), persisting across batches; partitioned by key hash so that the
+  // threads dedupe in parallel while each partition still sees its keys in input order
+  struct PairSet {
+    std::unordered_map<uint64_t, uint32_t> by_hash;  // key hash -> first key with that hash
+    PodVec<char> keys;                               // key bytes, back to back
+    PodVec<uint64_t> koff;                           // [k, k+1): key k
+    PodVec<int> count;                               // times seen after the first
+    std::unordered_map<std::string, int> spill;      // keys whose hash another key owns
+    // times `key` was seen before (0 = first occurrence, now recorded)
+    int seen(const char* key, size_t n, uint64_t h) {
+      auto it = by_hash.find(h);
+      if (it == by_hash.end()) {
+        by_hash.emplace(h, (uint32_t)count.size());
+        if (koff.empty()) koff.push_back(0);
+        keys.append(key, n);
+        koff.push_back(keys.size());
+        count.push_back(0);
+        return 0;
+      }
+      const uint32_t k = it->second;
+      if (koff[k + 1] - koff[k] == n && memcmp(keys.data() + koff[k], key, n) == 0) return ++count[k];
+      auto jt = spill.find(std::string(key, n));
+      if (jt == spill.end()) {
+        spill.emplace(std::string(key, n), 0);
+        return 0;
+      }
+      return ++jt->second;
+    }
+  };
+  std::vector<PairSet> alnpairs;
   uint64_t n_lines = 0;  // input lines seen (across batches)
 
-  // Handle one input line (pafreport.cpp:304-382).  Returns false after a fatal error.
-  bool add_line(Batch& b, const char* line0, size_t n) {
-    b.cur_line = n_lines++;
-    if (n > 0 && line0[0] == '#') return true;
-    const uint32_t loff = (uint32_t)b.text.size();
-    b.text.append(line0, n);
-    b.text.push_back('\0');
-    const char* lstr = b.text.data() + loff;  // the untouched copy (lstr)
-    std::string work(line0, n);               // split copy
-    char* s = &work[0];
-    t.clear();
-    bool after = true;
-    for (size_t i = 0; i < n; i++) {  // strsplit(line, t, '\t')
-      if (after) t.push_back(s + i);
-      after = false;
-      if (s[i] == '\t') {
-        s[i] = 0;
-        after = true;
+  // Pack the lines of b (b.lines, b.line0) into b's arrays (pafreport.cpp:304-382 per line).
+  void pack(Batch& b) {
+    static const bool prof = getenv("PW_PROFILE_HOST") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_0 = prof ? now() : 0;
+    const size_t nl = b.lines.size();
+    b.line0 = n_lines;
+    n_lines += nl;
+    if (nl == 0) return;
+    if ((int)alnpairs.size() != nt) alnpairs.resize((size_t)nt);
+    std::vector<LineInfo> info(nl);
+    // ---- phase 0: classify (parallel)
+    parallel_for(nt, [&](int t) {
+      for (size_t i = nl * (size_t)t / (size_t)nt; i < nl * (size_t)(t + 1) / (size_t)nt; i++)
+        info[i] = classify(b.buf.data() + b.lines[i].off, b.lines[i].len, opt);
+    });
+    const double t_1 = prof ? now() : 0;
+    // ---- phase 1: gene-mode q~t dedupe, first occurrence in input order (pafreport.cpp:319-334)
+    size_t stop = nl;  // lines after the first short line are never reached
+    for (size_t i = 0; i < nl; i++)
+      if (info[i].kind == kLineShort) {
+        stop = i + 1;
+        break;
       }
-    }
-    const int numt = (int)t.size();
-    if (numt < 15) {
-      b.log_fatal(strf("Error: invalid PAF fline (num. fields=%d):\n%s\n", numt, lstr));
-      return false;
-    }
-    const bool reverse = t[4][0] == '-';
-    const char* r_id = t[0];
-    const int r_len = atoi(t[1]), r_alnstart = atoi(t[2]), r_alnend = atoi(t[3]);
-    const char* t_id = t[5];
-    const int t_alnstart = atoi(t[7]), t_alnend = atoi(t[8]);
-    if (strcmp(r_id, t_id) == 0) {
-      if (opt.verbose) b.log_msg("Skipping alignment of qry seq to itself.\n");
-      return true;
-    }
     if (!opt.fullgenome) {
-      std::string key(r_id);
-      key.push_back('~');
-      key.append(t_id);
-      auto it = alnpairs.find(key);
-      if (it == alnpairs.end()) alnpairs.emplace(std::move(key), 0);
-      else {
-        ++it->second;
-        if (it->second == 1) b.log_msg(strf("Warning: alignment %s to %s already seen, ignoring \n", r_id, t_id));
-        return true;
+      parallel_for(nt, [&](int t) {
+        auto& m = alnpairs[(size_t)t];
+        std::string key;
+        for (size_t i = 0; i < stop; i++) {
+          LineInfo& li = info[i];
+          if (li.kind != kLineRec || li.khash % (uint64_t)nt != (uint64_t)t) continue;
+          const char* s = b.buf.data() + b.lines[i].off;
+          const char* q1 = strchr(s, '\t');
+          const char* t0 = q1;  // field 5 starts after the 5th tab
+          for (int k = 0; k < 4; k++) t0 = strchr(t0 + 1, '\t');
+          t0++;
+          const char* t1 = strchr(t0, '\t');
+          key.assign(s, (size_t)(q1 - s));
+          key.push_back('~');
+          key.append(t0, (size_t)(t1 - t0));
+          const int c = m.seen(key.data(), key.size(), li.khash);
+          if (c > 0) li.dup = c == 1 ? kDupWarn : kDupSilent;
+        }
+      });
+    }
+    const double t_2 = prof ? now() : 0;
+    // ---- phase 2: pack consecutive line ranges (balanced by bytes) in parallel
+    const int np = (int)std::min<size_t>((size_t)nt * 4, std::max<size_t>(stop / 64, 1));
+    std::vector<size_t> cut((size_t)np + 1, stop);
+    cut[0] = 0;
+    {
+      const uint64_t tot = b.lines[stop - 1].off + b.lines[stop - 1].len - b.lines[0].off;
+      size_t i = 0;
+      for (int k = 1; k < np; k++) {
+        const uint64_t target = b.lines[0].off + tot * (uint64_t)k / (uint64_t)np;
+        while (i < stop && b.lines[i].off < target) i++;
+        cut[(size_t)k] = std::max(i, cut[(size_t)k - 1]);
       }
     }
-    auto qit = qdb->index.find(r_id);
+    std::vector<Batch> parts((size_t)np);
+    std::atomic<int> next{0};
+    parallel_for(std::min(nt, np), [&](int) {
+      std::vector<uint32_t> fs;
+      for (int k; (k = next.fetch_add(1)) < np;) {
+        Batch& p = parts[(size_t)k];
+        for (size_t i = cut[(size_t)k]; i < cut[(size_t)k + 1] && !p.fatal; i++) {
+          p.cur_line = b.line0 + i;
+          pack_line(p, b.buf.data(), b.lines[i], info[i], fs);
+        }
+      }
+    });
+    const double t_3 = prof ? now() : 0;
+    append_parts(b, parts, nt);
+    if (prof)
+      fprintf(stderr, "[pack] %zu lines, %d threads: classify %.3f dedupe %.3f pack %.3f append %.3f s\n", nl, nt,
+              t_1 - t_0, t_2 - t_1, t_3 - t_2, now() - t_3);
+  }
+
+  // One input line (pafreport.cpp:304-382).
+  void pack_line(Batch& b, const char* base, const LineRef& lr, const LineInfo& li, std::vector<uint32_t>& fs) {
+    const char* s = base + lr.off;  // the untouched, NUL-terminated line (lstr)
+    const uint32_t n = lr.len;
+    if (li.kind == kLineSkip) return;
+    fs.clear();
+    bool after = true;
+    for (uint32_t i = 0; i < n; i++) {  // strsplit(line, t, '\t')
+      if (after) fs.push_back(i);
+      after = s[i] == '\t';
+    }
+    const int numt = (int)fs.size();
+    if (li.kind == kLineShort) {
+      b.log_fatal(strf("Error: invalid PAF fline (num. fields=%d):\n%s\n", numt, s));
+      return;
+    }
+    if (li.kind == kLineSelf) {
+      if (opt.verbose) b.log_msg("Skipping alignment of qry seq to itself.\n");
+      return;
+    }
+    // field k = [fld(k), fend(k)) (strsplit turns the tab after it, or a trailing tab, into NUL)
+    auto fend = [&](int k) -> const char* {
+      return k + 1 < numt ? s + fs[(size_t)k + 1] - 1 : (n > 0 && s[n - 1] == '\t' ? s + n - 1 : s + n);
+    };
+    auto fld = [&](int k) { return s + fs[(size_t)k]; };
+    auto fint = [&](const char* p, const char* e) {  // atoi of the field's own bytes
+      char tmp[32];
+      const size_t m = std::min<size_t>((size_t)(e - p), sizeof tmp - 1);
+      memcpy(tmp, p, m);
+      tmp[m] = 0;
+      return atoi(tmp);
+    };
+    auto fi = [&](int k) { return fint(fld(k), fend(k)); };
+    const bool reverse = fld(4)[0] == '-';
+    const char* r_id = fld(0);
+    const int r_idn = (int)(fend(0) - r_id);
+    const int r_len = fi(1), r_alnstart = fi(2), r_alnend = fi(3);
+    const char* t_id = fld(5);
+    const int t_idn = (int)(fend(5) - t_id);
+    const int t_alnstart = fi(7), t_alnend = fi(8);
+    if (li.dup != kDupNo) {
+      if (li.dup == kDupWarn)
+        b.log_msg(strf("Warning: alignment %.*s to %.*s already seen, ignoring \n", r_idn, r_id, t_idn, t_id));
+      return;
+    }
+    auto qit = qdb->index.find(std::string_view(r_id, (size_t)r_idn));
     if (qit == qdb->index.end()) {
-      b.log_fatal(strf("Error: could not retrieve sequence for %s !\n", r_id));
-      return false;
+      b.log_fatal(strf("Error: could not retrieve sequence for %.*s !\n", r_idn, r_id));
+      return;
     }
     const int qi = qit->second;
     const int L = qdb->len[qi];
     if (r_len != L) {
       b.log_fatal(strf("Error: ref seq len in this PAF line (%d) differs from loaded sequence length(%d)!\n%s\n",
-                       r_len, L, lstr));
-      return false;
+                       r_len, L, s));
+      return;
     }
     // ---- record
     RecHost rh;
-    rh.line_off = loff;
-    rh.line_len = (uint32_t)n;
+    rh.pre_msg = rh.cs_msg = rh.post_msg = -1;
+    rh.n_softclip = 0;
+    rh.line_off = lr.off;
     rh.qlen = L;
+    rh.tname_off = (uint32_t)(t_id - s);
+    rh.tname_len = (uint32_t)t_idn;
+    rh.t_aln = t_alnend - t_alnstart;
     const int offset = reverse ? r_len - r_alnend : r_alnstart;
     const int eff_t_len = t_alnend - t_alnstart;
     int edist = -1, alnscore = 0;
-    const char* cigar = nullptr;
-    const char* cs = nullptr;
+    const char *cigar = nullptr, *cigar_end = nullptr, *cs = nullptr, *cs_end = nullptr;
     int got = 0;
     for (int i = 12; i < numt; ++i) {  // tag scan, pafreport.cpp:495-520
-      if (!strncmp(t[i], "NM:i:", 5)) {
-        edist = atoi(t[i] + 5);
+      const char* f = fld(i);
+      if (!strncmp(f, "NM:i:", 5)) {
+        edist = fint(f + 5, std::max(f + 5, fend(i)));
         got |= 1;
-      } else if (!strncmp(t[i], "AS:i:", 5)) {
-        alnscore = atoi(t[i] + 5);
+      } else if (!strncmp(f, "AS:i:", 5)) {
+        alnscore = fint(f + 5, std::max(f + 5, fend(i)));
         got |= 2;
-      } else if (!strncmp(t[i], "cg:Z:", 5)) {
-        cigar = t[i] + 5;
+      } else if (!strncmp(f, "cg:Z:", 5)) {
+        cigar = f + 5;
+        cigar_end = fend(i);
         got |= 4;
-      } else if (!strncmp(t[i], "cs:Z:", 5)) {
-        cs = t[i] + 5;
+      } else if (!strncmp(f, "cs:Z:", 5)) {
+        cs = f + 5;
+        cs_end = fend(i);
         got |= 8;
       } else continue;
       if (got == 15) break;
@@ -406,19 +794,19 @@ struct Packer {
     d.offset = offset;
     d.t_len = 0;
     d.ev_begin = b.n_events_max;
-    if (cigar == nullptr || cigar[0] == 0) {
-      rh.pre_msg = (int32_t)b.add_msg(strf(CIGAR_ERROR, lstr, "(null)"));
+    if (cigar == nullptr || cigar == cigar_end) {
+      rh.pre_msg = (int32_t)b.add_msg(strf(CIGAR_ERROR, s, "(null)"));
     } else if (cs == nullptr) {
-      rh.pre_msg = (int32_t)b.add_msg(strf("Error: cs tag missing at line:\n%s\n", lstr));
+      rh.pre_msg = (int32_t)b.add_msg(strf("Error: cs tag missing at line:\n%s\n", s));
     } else {
       // pack cs (grow the arrays to the worst case first: one op per cs byte)
-      const size_t cslen = strlen(cs);
+      const size_t cslen = (size_t)(cs_end - cs);
       b.ops.resize(d.op_begin + cslen + 1);
       b.lits.resize(d.lit_begin + cslen + 1);
       pw_cs_totals tot;
       int32_t epos = 0;
-      int rc = pw_pack_cs(cs, offset, L, b.ops.data() + d.op_begin, cslen + 1, b.lits.data() + d.lit_begin,
-                          cslen + 1, &tot, &epos);
+      int rc = pack_cs_n(cs, cs_end, offset, L, b.ops.data() + d.op_begin, cslen + 1, b.lits.data() + d.lit_begin,
+                         cslen + 1, &tot, &epos);
       b.ops.resize(d.op_begin + tot.n_ops);
       b.lits.resize(d.lit_begin + tot.n_lits);
       d.n_ops = tot.n_ops;
@@ -430,15 +818,15 @@ struct Packer {
       b.text_total += tot.text_bound;
       b.n_events_max += tot.n_events_max;
       if (rc != PW_CS_OK) {
-        const char* at = cs + epos;
+        const std::string at(cs + epos, cs_end);
         std::string m;
         switch (rc) {
-          case PW_CS_PARSE: m = strf(CS_ERROR, lstr, at); break;
-          case PW_CS_SPLICED: m = strf("Error: spliced alignments not supported! at line:\n%s\n", lstr); break;
-          case PW_CS_UNHANDLED: m = strf("Error: unhandled event at %s in cs, line:\n%s\n", at, lstr); break;
-          case PW_CS_EMPTY: m = strf("Error: empty indel in cs string at line:\n%s\n", lstr); break;
-          case PW_CS_BOUNDS: m = strf("Error: cs string extends beyond query sequence at line:\n%s\n", lstr); break;
-          default: m = strf("Error: cs string too long at line:\n%s\n", lstr); break;
+          case PW_CS_PARSE: m = strf(CS_ERROR, s, at.c_str()); break;
+          case PW_CS_SPLICED: m = strf("Error: spliced alignments not supported! at line:\n%s\n", s); break;
+          case PW_CS_UNHANDLED: m = strf("Error: unhandled event at %s in cs, line:\n%s\n", at.c_str(), s); break;
+          case PW_CS_EMPTY: m = strf("Error: empty indel in cs string at line:\n%s\n", s); break;
+          case PW_CS_BOUNDS: m = strf("Error: cs string extends beyond query sequence at line:\n%s\n", s); break;
+          default: m = strf("Error: cs string too long at line:\n%s\n", s); break;
         }
         rh.cs_msg = (int32_t)b.add_msg(std::move(m));
       } else {
@@ -446,17 +834,17 @@ struct Packer {
         const char* p = cigar;
         int qpos = 0, tpos = 0;
         std::string err;
-        while (*p != '\0') {
+        while (p < cigar_end) {
           int cl = 0;
-          if (!parse_int(p, cl)) {
-            err = strf(CIGAR_ERROR, lstr, p);
+          if (!parse_int(p, cigar_end, cl)) {
+            err = strf(CIGAR_ERROR, s, std::string(p, cigar_end).c_str());
+            break;
+          }
+          if (p >= cigar_end) {
+            err = strf(CIGAR_ERROR, s, "");
             break;
           }
           const char cop = *p;
-          if (cop == '\0') {
-            err = strf(CIGAR_ERROR, lstr, p);
-            break;
-          }
           bool bad = false;
           switch (cop) {
             case 'X':
@@ -475,7 +863,7 @@ struct Packer {
             case 'D':
             case 'N': tpos += cl; break;
             default:
-              err = strf("Error: unhandled cigar_op %c (len %d) in %s\n", cop, cl, lstr);
+              err = strf("Error: unhandled cigar_op %c (len %d) in %s\n", cop, cl, s);
               bad = true;
           }
           if (bad) break;
@@ -484,30 +872,114 @@ struct Packer {
         if (err.empty()) {
           if (eff_t_len != tpos || tot.t_total != tpos)
             err = strf("Error: tseq alignment length mismatch (%d vs %d(%d-%d)) at line:%s\n", tpos, eff_t_len,
-                       t_alnend, t_alnstart, lstr);
+                       t_alnend, t_alnstart, s);
           else if (r_alnend - r_alnstart != qpos)
             err = strf("Error: ref alignment length mismatch (%d vs %d-%d) at line:%s\n", qpos, r_alnend,
-                       r_alnstart, lstr);
+                       r_alnstart, s);
         }
         if (!err.empty()) rh.post_msg = (int32_t)b.add_msg(std::move(err));
       }
     }
     // header (printDiffInfo, pafreport.cpp:886-892; labels :366-379)
-    std::string tlabel = strf("%s:%d-%d%c", t_id, t_alnstart, t_alnend, reverse ? '-' : '+');
-    std::string rlabel(r_id);
-    if (opt.fullgenome) rlabel += strf(":%d-%d", r_alnstart, r_alnend);
-    if (opt.single_query_gene) rlabel.clear();
     const double cov = ((r_alnend - r_alnstart) * 100.00) / r_len;
-    std::string hdr = rlabel.empty()
-                          ? strf(">%s coverage:%.2f score=%d edit_distance=%d\n", tlabel.c_str(), cov, alnscore, edist)
-                          : strf(">%s--%s coverage:%.2f score=%d edit_distance=%d\n", rlabel.c_str(), tlabel.c_str(),
-                                 cov, alnscore, edist);
-    rh.hdr_off = (uint32_t)b.hdr.size();
-    rh.hdr_len = (uint32_t)hdr.size();
-    b.hdr += hdr;
+    char hb[512];
+    // (the common full-length case prints "100.00" without the float formatter)
+    int hn;
+    if (opt.single_query_gene)
+      hn = snprintf(hb, sizeof hb, ">%.*s:%d-%d%c coverage:%.2f score=%d edit_distance=%d\n", t_idn, t_id, t_alnstart,
+                    t_alnend, reverse ? '-' : '+', cov, alnscore, edist);
+    else if (opt.fullgenome)
+      hn = snprintf(hb, sizeof hb, ">%.*s:%d-%d--%.*s:%d-%d%c coverage:%.2f score=%d edit_distance=%d\n", r_idn, r_id,
+                    r_alnstart, r_alnend, t_idn, t_id, t_alnstart, t_alnend, reverse ? '-' : '+', cov, alnscore, edist);
+    else
+      hn = snprintf(hb, sizeof hb, ">%.*s--%.*s:%d-%d%c coverage:%.2f score=%d edit_distance=%d\n", r_idn, r_id, t_idn,
+                    t_id, t_alnstart, t_alnend, reverse ? '-' : '+', cov, alnscore, edist);
+    rh.hdr_off = b.hdr.size();
+    if (hn >= 0 && (size_t)hn < sizeof hb) {
+      b.hdr.append(hb, (size_t)hn);
+    } else {  // long names
+      std::string rl = opt.single_query_gene ? std::string() : std::string(r_id, (size_t)r_idn);
+      if (!rl.empty() && opt.fullgenome) rl += strf(":%d-%d", r_alnstart, r_alnend);
+      const std::string tl = strf("%.*s:%d-%d%c", t_idn, t_id, t_alnstart, t_alnend, reverse ? '-' : '+');
+      const std::string h = rl.empty() ? strf(">%s coverage:%.2f score=%d edit_distance=%d\n", tl.c_str(), cov, alnscore, edist)
+                                       : strf(">%s--%s coverage:%.2f score=%d edit_distance=%d\n", rl.c_str(), tl.c_str(),
+                                              cov, alnscore, edist);
+      b.hdr.append(h.data(), h.size());
+    }
+    rh.hdr_len = (uint32_t)(b.hdr.size() - rh.hdr_off);
     b.desc.push_back(d);
     b.recs.push_back(rh);
     b.log.push_back({1, (uint32_t)b.recs.size() - 1, b.cur_line});
+  }
+};
+
+// ----------------------------------------------------------------- input chunks (GLineReader)
+// Reads the PAF in chunks of about `target` bytes that end on a line end; splits them into
+// lines as GLineReader::getLine does (\n, \r or \r\n end a line; a last line without an end is
+// a line when non-empty) and NUL-terminates every line in place.
+struct ChunkReader {
+  FILE* f;
+  bool eof = false;
+  PodVec<char> carry;
+  explicit ChunkReader(FILE* ff) : f(ff) {
+    struct stat st;  // a regular file: reserve it whole up front (no regrowth copies)
+    if (fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_size > 0) carry.reserve((size_t)st.st_size + 1);
+  }
+  bool next(Batch& b, size_t target) {
+    b.buf.swap(carry);
+    carry.clear();
+    if (eof && b.buf.empty()) return false;
+    size_t cut;
+    for (;;) {
+      if (!eof && b.buf.size() < target) {
+        const size_t want = std::min<size_t>(std::max<size_t>(target - b.buf.size(), 1 << 20), 256u << 20);
+        const size_t o = b.buf.size();
+        b.buf.resize(o + want);
+        const size_t got = fread(b.buf.data() + o, 1, want, f);
+        b.buf.resize(o + got);
+        if (got < want) eof = true;
+        if (!eof && b.buf.size() < target) continue;
+      }
+      const size_t sz = b.buf.size();
+      if (eof) {
+        cut = sz;
+        break;
+      }
+      const char* nl = (const char*)memrchr(b.buf.data(), '\n', sz);
+      if (nl) {
+        cut = (size_t)(nl - b.buf.data()) + 1;
+        break;
+      }
+      const char* cr = (const char*)memrchr(b.buf.data(), '\r', sz);
+      if (cr && (size_t)(cr - b.buf.data()) + 1 < sz) {
+        cut = (size_t)(cr - b.buf.data()) + 1;
+        break;
+      }
+      target += target / 2 + (1 << 20);  // one line longer than the chunk: read on
+    }
+    carry.append(b.buf.data() + cut, b.buf.size() - cut);
+    b.buf.resize(cut);
+    b.buf.push_back('\0');
+    char* s = b.buf.data();
+    const size_t n = cut;
+    const bool has_cr = memchr(s, '\r', n) != nullptr;
+    size_t p = 0;
+    while (p < n) {
+      size_t e;
+      if (!has_cr) {
+        const char* q = (const char*)memchr(s + p, '\n', n - p);
+        e = q ? (size_t)(q - s) : n;
+      } else {
+        e = p;
+        while (e < n && s[e] != '\n' && s[e] != '\r') e++;
+      }
+      if (e == n && e == p) break;  // nothing after the last line end
+      b.lines.push_back({p, (uint32_t)(e - p)});
+      size_t nx = e + 1;
+      if (e < n && s[e] == '\r' && e + 1 < n && s[e + 1] == '\n') nx = e + 2;
+      s[e] = '\0';
+      p = nx;
+    }
     return true;
   }
 };
@@ -676,7 +1148,7 @@ int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_a
   }
   const RecHost& rh = b.recs[it.idx];
   const pw_aln_result& r = res[it.idx];
-  const char* lstr = b.text.data() + rh.line_off;
+  const char* lstr = b.buf.data() + rh.line_off;
   if (rh.pre_msg >= 0) {
     fputs(b.msgs[rh.pre_msg].c_str(), err);
     return 1;
@@ -726,52 +1198,6 @@ int emit(const Batch& b, const uint8_t* text, const pw_aln_result* res, const pw
   }
   return -1;
 }
-
-// ----------------------------------------------------------------- GLineReader
-struct LineReader {
-  FILE* f;
-  std::vector<char> buf;
-  size_t pos = 0, end = 0;
-  bool eof = false;
-  std::string line;
-  explicit LineReader(FILE* ff) : f(ff), buf(1 << 22) {}
-  int getc_() {
-    if (pos == end) {
-      if (eof) return EOF;
-      end = fread(buf.data(), 1, buf.size(), f);
-      pos = 0;
-      if (end == 0) {
-        eof = true;
-        return EOF;
-      }
-    }
-    return (unsigned char)buf[pos++];
-  }
-  // \n, \r or \r\n end a line (gclib GLineReader::getLine)
-  bool next() {
-    line.clear();
-    int c;
-    while ((c = getc_()) != EOF) {
-      if (c == '\n') return true;
-      if (c == '\r') {
-        int d = getc_();
-        if (d != '\n' && d != EOF) pos--;  // unget
-        return true;
-      }
-      // fast path: copy a run of plain bytes
-      line.push_back((char)c);
-      while (pos < end) {
-        char ch = buf[pos];
-        if (ch == '\n' || ch == '\r') break;
-        size_t e = pos;
-        while (e < end && buf[e] != '\n' && buf[e] != '\r') e++;
-        line.append(buf.data() + pos, e - pos);
-        pos = e;
-      }
-    }
-    return !line.empty();
-  }
-};
 
 #define USAGE                                                             \
   "Usage:\n\
@@ -940,35 +1366,46 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   if (!dev.init(qdb, skip_codan)) return 2;
   Packer pk;
   pk.qdb = &qdb;
+  pk.nt = host_threads();
   pk.opt.fullgenome = fullgenome;
   pk.opt.skip_codan = skip_codan;
   pk.opt.verbose = verbose;
   pk.opt.single_query_gene = (qdb.ids.size() == 1 && !fullgenome);
-  LineReader lr(in.f);
-  Batch b;
+  // Pipeline: while the GPU runs batch k and its report is written, batch k + 1 is read and
+  // packed (by pk.nt threads); nothing past a fatal batch is packed.
+  ChunkReader rd(in.f);
+  Batch bb[2];
   std::vector<uint8_t> text_h;
   std::vector<pw_aln_result> res_h;
   std::vector<pw_page> pages_h;
-  const size_t kBatchBytes = 256u << 20, kBatchRecs = 1u << 20;
-  bool more = true;
-  while (more) {
-    b.clear();
-    while (b.text.size() < kBatchBytes && b.desc.size() < kBatchRecs) {
-      if (!lr.next()) {
-        more = false;
-        break;
-      }
-      if (!pk.add_line(b, lr.line.data(), lr.line.size())) {
-        more = false;
-        break;
-      }
+  size_t kChunk = 256u << 20;  // input bytes per batch (PW_CHUNK_BYTES: tests force many batches)
+  if (const char* e = getenv("PW_CHUNK_BYTES"))
+    if (atoll(e) > 0) kChunk = (size_t)atoll(e);
+  auto pack_next = [&](Batch& B) -> bool {
+    B.clear();
+    if (!rd.next(B, kChunk)) return false;
+    pk.pack(B);
+    return true;
+  };
+  int cur = 0;
+  bool have = pack_next(bb[0]);
+  while (have) {
+    Batch& B = bb[cur];
+    const bool more = !B.fatal;
+    std::future<bool> nxt;
+    if (more) {
+      const int o = cur ^ 1;
+      nxt = std::async(std::launch::async, [&, o] { return pack_next(bb[o]); });
     }
-    if (!dev.run(b, skip_codan, text_h, res_h, pages_h)) return 2;
-    const int rc = emit(b, text_h.data(), res_h.data(), pages_h.data(), out.f);
+    const int rc = dev.run(B, skip_codan, text_h, res_h, pages_h) ? emit(B, text_h.data(), res_h.data(), pages_h.data(), out.f)
+                                                                  : 2;
     if (rc >= 0) {
+      if (more) nxt.wait();
       fflush(out.f);
       return rc;
     }
+    have = more && nxt.get();
+    cur ^= 1;
   }
   fflush(out.f);
   return 0;
@@ -981,14 +1418,21 @@ struct pw_batch {
   Packer pk;
   bool skip_codan = false;
   uint64_t alg_in = 0;
+  // per-genome tables (target sequence names in order of first appearance), built on demand
+  bool g_ready = false;
+  std::vector<uint32_t> gid;
+  std::vector<int32_t> taln;
+  std::string gnames;
+  uint32_t ngen = 0;
 };
 
-extern "C" pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uint32_t flags, char* errbuf,
-                                         size_t errlen) {
+extern "C" pw_batch* pw_batch_from_files_shard(const char* fasta, const char* paf, uint32_t flags, uint32_t shard,
+                                               uint32_t nshards, char* errbuf, size_t errlen) {
   auto fail = [&](const std::string& m) -> pw_batch* {
     if (errbuf && errlen) snprintf(errbuf, errlen, "%s", m.c_str());
     return nullptr;
   };
+  if (nshards == 0 || shard >= nshards) return fail("bad shard");
   pw_batch* bt = new pw_batch();
   std::string err;
   if (!bt->q.load(fasta, err)) {
@@ -1003,20 +1447,32 @@ extern "C" pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uin
   if (!skip && !fc && fsize > 120000) skip = true;
   bt->skip_codan = skip;
   bt->pk.qdb = &bt->q;
+  bt->pk.nt = host_threads();
   bt->pk.opt.fullgenome = full;
   bt->pk.opt.skip_codan = skip;
   bt->pk.opt.single_query_gene = (bt->q.ids.size() == 1 && !full);
-  FILE* f = fopen(paf, "r");
+  bt->pk.opt.shard = shard;
+  bt->pk.opt.nshards = nshards;
+  FILE* f = fopen(paf, "rb");
   if (!f) {
     delete bt;
     return fail(strf("cannot open %s", paf));
   }
-  LineReader lr(f);
-  while (lr.next())
-    if (!bt->pk.add_line(bt->b, lr.line.data(), lr.line.size())) break;
+  ChunkReader rd(f);
+  const auto t0 = std::chrono::steady_clock::now();
+  if (rd.next(bt->b, SIZE_MAX / 4)) {  // the whole file is one batch
+    if (getenv("PW_PROFILE_HOST"))
+      fprintf(stderr, "[read] %.3f s\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    bt->pk.pack(bt->b);
+  }
   fclose(f);
   bt->alg_in = alg_bytes(bt->b, bt->q, skip);
   return bt;
+}
+
+extern "C" pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uint32_t flags, char* errbuf,
+                                         size_t errlen) {
+  return pw_batch_from_files_shard(fasta, paf, flags, 0, 1, errbuf, errlen);
 }
 
 extern "C" int pw_batch_view_get(const pw_batch* bt, pw_batch_view* v) {
@@ -1085,6 +1541,115 @@ extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host
     if (st >= 0) break;
   }
   if (fclose(f) != 0 && ret == PW_OK) ret = PW_E_IO;
+  return ret;
+}
+
+extern "C" uint32_t pw_batch_genomes(pw_batch* bt, uint64_t* names_bytes) {
+  if (!bt) return 0;
+  if (!bt->g_ready) {
+    const Batch& b = bt->b;
+    std::unordered_map<std::string_view, uint32_t> m;
+    bt->gid.resize(b.recs.size());
+    bt->taln.resize(b.recs.size());
+    for (size_t i = 0; i < b.recs.size(); i++) {
+      const RecHost& r = b.recs[i];
+      const std::string_view nm(b.buf.data() + r.line_off + r.tname_off, r.tname_len);
+      auto it = m.find(nm);
+      uint32_t g;
+      if (it == m.end()) {
+        g = (uint32_t)m.size();
+        m.emplace(nm, g);
+        bt->gnames.append(nm.data(), nm.size());
+        bt->gnames.push_back('\0');
+      } else {
+        g = it->second;
+      }
+      bt->gid[i] = g;
+      bt->taln[i] = r.t_aln;
+    }
+    bt->ngen = (uint32_t)m.size();
+    bt->g_ready = true;
+  }
+  if (names_bytes) *names_bytes = bt->gnames.size();
+  return bt->ngen;
+}
+
+extern "C" int pw_batch_genomes_get(const pw_batch* bt, uint32_t* genome_of, int32_t* t_aln, char* names) {
+  if (!bt || !bt->g_ready) return PW_E_ARG;
+  if (genome_of && !bt->gid.empty()) memcpy(genome_of, bt->gid.data(), bt->gid.size() * 4);
+  if (t_aln && !bt->taln.empty()) memcpy(t_aln, bt->taln.data(), bt->taln.size() * 4);
+  if (names && !bt->gnames.empty()) memcpy(names, bt->gnames.data(), bt->gnames.size());
+  return PW_OK;
+}
+
+// k-way merge of PWI1 item streams (each sorted by global input line) up to the first item
+// with a status >= 0.
+extern "C" int pw_items_merge(const char* const* paths, uint32_t n, const char* out_path, const char* err_path) {
+  struct Src {
+    FILE* f = nullptr;
+    bool ok = false;
+    uint64_t line = 0;
+    int32_t st = -1;
+    uint32_t no = 0, ne = 0;
+    bool next() {
+      unsigned char h[20];
+      ok = fread(h, 1, 20, f) == 20;
+      if (ok) {
+        memcpy(&line, h, 8);
+        memcpy(&st, h + 8, 4);
+        memcpy(&no, h + 12, 4);
+        memcpy(&ne, h + 16, 4);
+      }
+      return ok;
+    }
+  };
+  std::vector<Src> src(n);
+  int ret = 0;
+  FILE* out = out_path ? fopen(out_path, "wb") : stdout;
+  FILE* err = err_path ? fopen(err_path, "wb") : stderr;
+  if (!out || !err) ret = PW_E_IO;
+  for (uint32_t i = 0; i < n && ret == 0; i++) {
+    src[i].f = fopen(paths[i], "rb");
+    char mg[4];
+    if (!src[i].f || fread(mg, 1, 4, src[i].f) != 4 || memcmp(mg, "PWI1", 4) != 0) ret = PW_E_IO;
+    else src[i].next();
+  }
+  std::vector<char> buf(1 << 20);
+  auto copy = [&](FILE* from, FILE* to, uint64_t bytes) {
+    while (bytes > 0) {
+      const size_t k = (size_t)std::min<uint64_t>(bytes, buf.size());
+      if (fread(buf.data(), 1, k, from) != k) return false;
+      fwrite(buf.data(), 1, k, to);
+      bytes -= k;
+    }
+    return true;
+  };
+  while (ret == 0) {
+    int best = -1;
+    for (uint32_t i = 0; i < n; i++)
+      if (src[i].ok && (best < 0 || src[i].line < src[(size_t)best].line)) best = (int)i;
+    if (best < 0) break;
+    Src& s = src[(size_t)best];
+    if (!copy(s.f, out, s.no)) {
+      ret = PW_E_IO;
+      break;
+    }
+    fflush(out);
+    if (!copy(s.f, err, s.ne)) {
+      ret = PW_E_IO;
+      break;
+    }
+    if (s.st >= 0) {
+      ret = s.st;
+      break;
+    }
+    s.next();
+  }
+  for (auto& s : src)
+    if (s.f) fclose(s.f);
+  if (out && out != stdout) fclose(out);
+  else if (out) fflush(out);
+  if (err && err != stderr) fclose(err);
   return ret;
 }
 

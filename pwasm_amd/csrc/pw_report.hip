@@ -1887,7 +1887,36 @@ __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, co
   }
 }
 
+// ------------------------------------------------------------------ per-genome tables
+// One row per target sequence: alignments, event lines, aligned target bases (the tables the
+// multi-GPU driver all-gathers).  A thread per record, atomics into the rows.
+__global__ __launch_bounds__(256) void genome_table_kernel(const pw_aln_result* res, const uint32_t* gof,
+                                                           const int32_t* taln, uint32_t n, pw_genome_row* rows,
+                                                           uint32_t ng) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t g = gof[i];
+  if (g >= ng) return;
+  const int32_t tb = taln[i];
+  atomicAdd(&rows[g].records, 1u);
+  atomicAdd(&rows[g].events, res[i].n_events);
+  atomicAdd((unsigned long long*)&rows[g].t_bases, (unsigned long long)(tb > 0 ? tb : 0));
+}
+
 }  // namespace pw
+
+extern "C" int pw_genome_table(const pw_aln_result* results, const uint32_t* genome_of, const int32_t* t_aln,
+                               uint32_t n_alns, pw_genome_row* rows, uint32_t n_genomes, void* stream) {
+  if (n_genomes && !rows) return PW_E_ARG;
+  if (n_alns && (!results || !genome_of || !t_aln)) return PW_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n_genomes && hipMemsetAsync(rows, 0, (size_t)n_genomes * sizeof(pw_genome_row), st) != hipSuccess)
+    return PW_E_HIP;
+  if (n_alns)
+    hipLaunchKernelGGL(pw::genome_table_kernel, dim3((n_alns + 255) / 256), dim3(256), 0, st, results, genome_of,
+                       t_aln, n_alns, rows, n_genomes);
+  return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+}
 
 extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_alns) {
   return pw::work_layout(nullptr, n_events_max, n_alns, nullptr);
