@@ -39,7 +39,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--config", type=int, default=None,
+                    help="2 (default at N=1: BASELINE configs[1]); 3 (default at N>1: the 10M-record set sharded "
+                         "by target genome, configs[2]); 5 (GapAssem, configs[4])")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -48,6 +50,9 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.config is None:
+        args.config = 2 if world == 1 else 3
     if args.traffic_json is None:  # the newest committed profile of the same command (profiles/run_prof.sh)
         args.traffic_json = latest_profile(args.config)
 
@@ -60,31 +65,57 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    if world > 1:  # PW_DIST_BACKEND=gloo: rehearsal with several ranks on one GPU (RCCL refuses that)
+        dist.init_process_group(backend=os.environ.get("PW_DIST_BACKEND",
+                                                       "nccl" if torch.cuda.is_available() else "gloo"))
+    local = local % max(torch.cuda.device_count(), 1)
     dev_name = f"cuda:{local}"
     torch.cuda.set_device(local)
     if args.config == 5:
         return bench_gapassem(args, world, rank, dev_name)
 
-    # ---- data: this rank's shard (synthetic, seeded; generated outside the timed region)
+    # ---- data (synthetic, seeded; generated outside the timed region).  cfg3 is ONE 10M-record
+    # set: rank r generates exactly the lines of its target-genome shard (crc32(target) % N == r,
+    # the rule of pw_batch_from_files_shard / pwasm_amd.mgpu) — strong scaling.  Other configs
+    # at N > 1: one independent batch per rank (weak scaling).
+    sharded = args.config == 3
     tmp = tempfile.mkdtemp(prefix=f"pwbench{rank}_")
     fa, paf = os.path.join(tmp, "q.fa"), os.path.join(tmp, "a.paf")
-    seed = 2 + 1000 * rank if args.config == 2 else args.config + 1000 * rank
+    seed = 3 if sharded else (2 + 1000 * rank if args.config == 2 else args.config + 1000 * rank)
     t0 = time.time()
-    subprocess.run([str(REPO / "synth/build/pwsynth"), "paf", "--config", str(args.config), "--scale",
-                    str(args.scale), "--seed", str(seed), "--fa", fa, "--paf", paf], check=True,
-                   stderr=subprocess.DEVNULL)
+    cmd = [str(REPO / "synth/build/pwsynth"), "paf", "--config", str(args.config), "--scale", str(args.scale),
+           "--seed", str(seed), "--fa", fa, "--paf", paf]
+    if sharded:
+        cmd += ["--threads", str(host_threads())] + (["--shard", f"{rank}/{world}"] if world > 1 else [])
+    subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
+    t_gen = time.time() - t0
     flags = pw.FLAG_G | pw.FLAG_C if args.config in (1, 2, 3) else 0
     batch = pw.HostBatch(fa, paf, flags)
     v = batch.view
     dev = pw.stage_batch(batch, dev_name)
     torch.cuda.synchronize()
     log(f"[rank {rank}] staged {v.n_alns} records, {v.n_ops} ops, {v.n_lits} literal bytes "
-        f"({time.time() - t0:.1f}s host prep)")
+        f"({t_gen:.1f}s generate, {time.time() - t0 - t_gen:.1f}s pack + stage)")
 
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
+    gtab = None
+    if world > 1:
+        # per-genome coverage / event tables (pw_genome_table) all-gathered every step (RCCL):
+        # padded to the largest rank's row count, measured once here
+        from pwasm_amd import mgpu
+        rows, _, gt = mgpu.genome_rows(batch, dev, sp)
+        if dist.get_backend() == "gloo":
+            nb = torch.tensor([rows.numel()], dtype=torch.int64)
+            nbs = [torch.empty_like(nb) for _ in range(world)]
+            dist.all_gather(nbs, nb)
+        else:
+            nb = torch.tensor([rows.numel()], dtype=torch.int64, device=dev_name)
+            nbs = [torch.empty_like(nb) for _ in range(world)]
+            dist.all_gather(nbs, nb)
+        pad = max(int(x.item()) for x in nbs)
+        gtab = (mgpu, rows, gt, torch.zeros(max(pad, 16), dtype=torch.uint8, device=dev_name),
+                torch.empty(world * max(pad, 16), dtype=torch.uint8, device=dev_name))
 
     def step(ev=None):
         if not v.skip_codan:
@@ -98,6 +129,15 @@ def main():
         assert rc == 0
         if ev is not None:
             ev[1].record(stream)
+        if gtab is not None:
+            mg, rows, gt, padded, gathered = gtab
+            mg.launch_genome_table(dev, rows, gt, sp)
+            padded[: rows.numel()].copy_(rows)
+            if dist.get_backend() == "gloo":  # (rehearsal only: host copies)
+                h = [torch.empty(padded.numel(), dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(h, padded.cpu())
+            else:
+                dist.all_gather_into_tensor(gathered, padded)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -124,14 +164,16 @@ def main():
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
 
     tot_events = n_events
+    tot_records = int(v.n_alns)
     max_el = t_el
     if world > 1:
         t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         max_el = float(t.item())
-        e = torch.tensor([n_events], dtype=torch.float64, device=dev_name)
+        e = torch.tensor([n_events, int(v.n_alns)], dtype=torch.float64, device=dev_name)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        tot_events = int(e.item())
+        tot_events = int(e[0].item())
+        tot_records = int(e[1].item())
 
     if rank == 0:
         report = {}
@@ -152,7 +194,7 @@ def main():
         traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
         flags_cli = ["-G", "-C"] if flags else []
         parity, cpu, e2e = None, None, None
-        if not args.no_parity:
+        if not args.no_parity and world == 1 and v.n_alns <= 200000:
             # the benchmarked batch itself, copied back once (outside the timed region) and
             # diffed byte for byte against the oracle on the same input
             got = os.path.join(tmp, "hip.txt")
@@ -188,14 +230,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": max_el * 1000.0 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (pwsynth, seeded minimap2-style PAF with cs/cg tags)",
-            "config": {"workload": f"cfg{args.config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
-                                   f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU",
+            "config": {"workload": (f"cfg3: {tot_records} PAF records (gene panel of {v.n_queries} CDS x assemblies, "
+                                    f"-G -C) sharded by target genome over {world} GPU(s), {tot_events} events"
+                                    if sharded else
+                                    f"cfg{args.config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
+                                    f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU"),
                        "records_per_gpu": int(v.n_alns), "events_per_gpu": n_events, "scale": args.scale,
-                       "parallelism": "independent per-rank batches" if world > 1 else "single GPU"},
+                       "parallelism": (f"shard-by-target x{world} + RCCL all-gather of per-genome tables"
+                                       if sharded and world > 1 else
+                                       ("independent per-rank batches" if world > 1 else "single GPU"))},
             "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -338,6 +385,13 @@ def bench_gapassem(args, world, rank, dev_name):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_threads():
+    for k in ("PW_THREADS", "OMP_NUM_THREADS"):
+        if os.environ.get(k, "").isdigit() and int(os.environ[k]) > 0:
+            return int(os.environ[k])
+    return max(1, min(len(os.sched_getaffinity(0)), 16))
 
 
 def latest_profile(config):

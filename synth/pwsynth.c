@@ -2,6 +2,8 @@
  * pwsynth.c — deterministic synthetic inputs for tests and bench.py (tooling, not product).
  *
  *   pwsynth paf    --config K [--scale F] [--seed S] --fa out.fa --paf out.paf [knobs]
+ *                  (cfg3: [--threads T] [--shard r/N] — per-record random streams, so a shard
+ *                  or a multi-threaded run writes exactly the lines of the full file it owns)
  *   pwsynth layout --config 5 [--scale F] [--seed S] --out layout.pwl [knobs]
  *
  * PAF records are minimap2-style (`-c --cs`): 12 columns + NM/ms/AS/nn/tp/cm/s1/s2/de/rl/cg/cs
@@ -17,12 +19,14 @@
  * opens or closes an alignment with an indel).  Knobs add the edge cases the tests need.
  */
 #include <math.h>
+#include <pthread.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-static uint64_t g_rng;
+static __thread uint64_t g_rng; /* per thread: cfg3 records are generated in parallel */
 static uint64_t rnd64(void) { /* splitmix64 */
   uint64_t z = (g_rng += 0x9E3779B97F4A7C15ull);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -87,6 +91,7 @@ typedef struct {
   int ncds, len_min, len_max, recs_per_cds, contig_min, contig_max;
   double err, rev, partial, p_sub, p_del, p_ins, hp_boost, p_subrun, p_longindel, p_inframe;
   int margin, motif_plant, long_mode;
+  int threads, shard, nshards; /* cfg3: worker threads; --shard r/N keeps the target-genome shard r */
   double p_dup, p_self, p_comment, p_softclip;
   const char* fa;
   const char* paf;
@@ -310,6 +315,108 @@ static void simulate(const opts_t* o, const char* Q, int qs, int qe, aln_out* a)
   if (clast) sb_printf(&a->cg, "%d%c", crun, clast);
 }
 
+/* CRC-32 (IEEE, = zlib.crc32): a record's shard is crc32(target name) % N, the rule of
+ * pwasm_amd/shard.py and pw_batch_from_files_shard. */
+static uint32_t crc32_ieee(const char* p, size_t n) {
+  static uint32_t tab[256];
+  static int init = 0;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[i] = c;
+    }
+    init = 1;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = tab[(c ^ (uint8_t)p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+typedef struct {
+  const opts_t* o;
+  char** cds;
+  char** rcs;
+  const int* clen;
+  int recs;
+} paf_ctx;
+
+/* One PAF record (query i, target r) appended to `out`. */
+static void gen_record(const paf_ctx* c, int i, int r, aln_out* a, sbuf* line, sbuf* out) {
+  const opts_t* o = c->o;
+  int L = c->clen[i];
+  int rev = rndu() < o->rev;
+  int qs = 0, qe = L;
+  if (rndu() < o->partial && L > 120) {
+    qs = rndi(0, L / 4);
+    qe = L - rndi(0, L / 4);
+    if (qe - qs < 60) {
+      qs = 0;
+      qe = L;
+    }
+  }
+  /* aligned strand coordinates: cs walks rc from offset = L - qend */
+  const char* Q = rev ? c->rcs[i] : c->cds[i];
+  int as = rev ? L - qe : qs, ae = rev ? L - qs : qe;
+  simulate(o, Q, as, ae, a);
+  int tlen = rndi(o->contig_min, o->contig_max);
+  if (tlen < a->tlen_aln + 10) tlen = a->tlen_aln + 10;
+  int ts = rndi(0, tlen - a->tlen_aln);
+  int te = ts + a->tlen_aln;
+  char tname[64];
+  if (o->config == 0 && rndu() < o->p_self) snprintf(tname, sizeof tname, "cds%d", i);
+  else snprintf(tname, sizeof tname, "asm%d_ctg%d", r, i % 7);
+  line->len = 0;
+  if (o->config == 0 && rndu() < o->p_comment) sb_printf(line, "# comment line %d\n", r);
+  int as_score = 2 * a->nmatch - 4 * a->nm;
+  sb_printf(line, "cds%d\t%d\t%d\t%d\t%c\t%s\t%d\t%d\t%d\t%d\t%d\t60\t", i, L, qs, qe, rev ? '-' : '+', tname,
+            tlen, ts, te, a->nmatch, a->alnlen);
+  sb_printf(line, "NM:i:%d\tms:i:%d\tAS:i:%d\tnn:i:0\ttp:A:P\tcm:i:%d\ts1:i:%d\ts2:i:0\tde:f:%.4f\trl:i:0\tcg:Z:",
+            a->nm, as_score, as_score, a->nmatch / 10, a->nmatch, (double)a->nm / (a->alnlen ? a->alnlen : 1));
+  sb_putn(line, a->cg.buf, a->cg.len);
+  sb_putn(line, "\tcs:Z:", 6);
+  sb_putn(line, a->cs.buf, a->cs.len);
+  sb_putc(line, '\n');
+  sb_putn(out, line->buf, line->len);
+  if (o->config == 0 && rndu() < o->p_dup) sb_putn(out, line->buf, line->len); /* duplicate q~t pair */
+}
+
+/* cfg3: record k = i * recs + r draws from its own stream (seed, k), so any subset of the
+ * records (a shard) or any split over threads generates the same bytes. */
+typedef struct {
+  const paf_ctx* c;
+  long long k0, k1;
+  sbuf out;
+  long long n;
+} blk_job;
+
+static void* gen_block(void* arg) {
+  blk_job* j = (blk_job*)arg;
+  const paf_ctx* c = j->c;
+  const opts_t* o = c->o;
+  aln_out a;
+  memset(&a, 0, sizeof a);
+  sbuf line = {0};
+  j->out.len = 0;
+  j->n = 0;
+  for (long long k = j->k0; k < j->k1; k++) {
+    const int i = (int)(k / c->recs), r = (int)(k % c->recs);
+    if (o->nshards > 1) {
+      char tname[64];
+      int tn = snprintf(tname, sizeof tname, "asm%d_ctg%d", r, i % 7);
+      if (crc32_ieee(tname, (size_t)tn) % (uint32_t)o->nshards != (uint32_t)o->shard) continue;
+    }
+    g_rng = (o->seed * 0x2545F4914F6CDD1Dull + 12345) ^ ((uint64_t)k * 0xD1B54A32D192ED03ull);
+    rnd64();
+    gen_record(c, i, r, &a, &line, &j->out);
+    j->n++;
+  }
+  free(line.buf);
+  free(a.cs.buf);
+  free(a.cg.buf);
+  return NULL;
+}
+
 static int cmd_paf(opts_t* o) {
   int ncds = o->ncds;
   int recs = (int)llround(o->recs_per_cds * o->scale);
@@ -328,6 +435,7 @@ static int cmd_paf(opts_t* o) {
     return 2;
   }
   char** cds = (char**)calloc((size_t)ncds, sizeof(char*));
+  char** rcs = (char**)calloc((size_t)ncds, sizeof(char*));
   int* clen = (int*)calloc((size_t)ncds, sizeof(int));
   for (int i = 0; i < ncds; i++) {
     int L = rndi(o->len_min / 3, o->len_max / 3) * 3;
@@ -339,56 +447,53 @@ static int cmd_paf(opts_t* o) {
     for (int k = 0; k < L; k += 70) fprintf(ff, "%.*s\n", (L - k) < 70 ? (L - k) : 70, cds[i] + k);
   }
   fclose(ff);
-  aln_out a;
-  memset(&a, 0, sizeof a);
-  sbuf line = {0};
-  char* rc = NULL;
-  int rc_cap = 0;
+  paf_ctx c = {o, cds, rcs, clen, recs};
   long long nrec = 0;
-  for (int i = 0; i < ncds; i++) {
-    int L = clen[i];
-    if (L + 1 > rc_cap) {
-      rc_cap = L + 1;
-      rc = (char*)realloc(rc, (size_t)rc_cap);
+  if (o->config == 3) {
+    for (int i = 0; i < ncds; i++) {  /* reverse complements are generated lazily below */
+      rcs[i] = (char*)malloc((size_t)clen[i] + 1);
+      for (int k = 0; k < clen[i]; k++) rcs[i][k] = comp(cds[i][clen[i] - 1 - k]);
+      rcs[i][clen[i]] = 0;
     }
-    for (int k = 0; k < L; k++) rc[k] = comp(cds[i][L - 1 - k]);
-    rc[L] = 0;
-    for (int r = 0; r < recs; r++) {
-      int rev = rndu() < o->rev;
-      int qs = 0, qe = L;
-      if (rndu() < o->partial && L > 120) {
-        qs = rndi(0, L / 4);
-        qe = L - rndi(0, L / 4);
-        if (qe - qs < 60) {
-          qs = 0;
-          qe = L;
-        }
+    const long long total = (long long)ncds * recs;
+    int T = o->threads > 0 ? o->threads : 16;
+    const long long B = 4096;
+    blk_job* jobs = (blk_job*)calloc((size_t)T, sizeof(blk_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+    for (long long k0 = 0; k0 < total; k0 += B * T) {
+      int nj = 0;
+      for (int t = 0; t < T && k0 + B * t < total; t++, nj++) {
+        jobs[t].c = &c;
+        jobs[t].k0 = k0 + B * t;
+        jobs[t].k1 = jobs[t].k0 + B < total ? jobs[t].k0 + B : total;
+        pthread_create(&th[t], NULL, gen_block, &jobs[t]);
       }
-      /* aligned strand coordinates: cs walks rc from offset = L - qend */
-      const char* Q = rev ? rc : cds[i];
-      int as = rev ? L - qe : qs, ae = rev ? L - qs : qe;
-      simulate(o, Q, as, ae, &a);
-      int tlen = rndi(o->contig_min, o->contig_max);
-      if (tlen < a.tlen_aln + 10) tlen = a.tlen_aln + 10;
-      int ts = rndi(0, tlen - a.tlen_aln);
-      int te = ts + a.tlen_aln;
-      char tname[64];
-      if (o->config == 0 && rndu() < o->p_self) snprintf(tname, sizeof tname, "cds%d", i);
-      else snprintf(tname, sizeof tname, "asm%d_ctg%d", r, i % 7);
-      line.len = 0;
-      if (o->config == 0 && rndu() < o->p_comment) sb_printf(&line, "# comment line %d\n", r);
-      int as_score = 2 * a.nmatch - 4 * a.nm;
-      sb_printf(&line, "cds%d\t%d\t%d\t%d\t%c\t%s\t%d\t%d\t%d\t%d\t%d\t60\t", i, L, qs, qe, rev ? '-' : '+', tname,
-                tlen, ts, te, a.nmatch, a.alnlen);
-      sb_printf(&line, "NM:i:%d\tms:i:%d\tAS:i:%d\tnn:i:0\ttp:A:P\tcm:i:%d\ts1:i:%d\ts2:i:0\tde:f:%.4f\trl:i:0\tcg:Z:",
-                a.nm, as_score, as_score, a.nmatch / 10, a.nmatch, (double)a.nm / (a.alnlen ? a.alnlen : 1));
-      sb_putn(&line, a.cg.buf, a.cg.len);
-      sb_putn(&line, "\tcs:Z:", 6);
-      sb_putn(&line, a.cs.buf, a.cs.len);
-      sb_putc(&line, '\n');
-      fwrite(line.buf, 1, line.len, fp);
-      nrec++;
-      if (o->config == 0 && rndu() < o->p_dup) fwrite(line.buf, 1, line.len, fp); /* duplicate q~t pair */
+      for (int t = 0; t < nj; t++) {
+        pthread_join(th[t], NULL);
+        fwrite(jobs[t].out.buf, 1, jobs[t].out.len, fp);
+        nrec += jobs[t].n;
+      }
+    }
+    for (int t = 0; t < T; t++) free(jobs[t].out.buf);
+    free(jobs);
+    free(th);
+  } else {
+    aln_out a;
+    memset(&a, 0, sizeof a);
+    sbuf line = {0}, out = {0};
+    for (int i = 0; i < ncds; i++) {
+      int L = clen[i];
+      rcs[i] = (char*)malloc((size_t)L + 1);
+      for (int k = 0; k < L; k++) rcs[i][k] = comp(cds[i][L - 1 - k]);
+      rcs[i][L] = 0;
+      for (int r = 0; r < recs; r++) {
+        out.len = 0;
+        gen_record(&c, i, r, &a, &line, &out);
+        fwrite(out.buf, 1, out.len, fp);
+        nrec++;
+      }
+      free(rcs[i]);
+      rcs[i] = NULL;
     }
   }
   fclose(fp);
@@ -522,12 +627,23 @@ int main(int argc, char** argv) {
     else if (!strcmp(k, "--ref-len")) o.ref_len = atoi(v);
     else if (!strcmp(k, "--row-min")) o.row_min = atoi(v);
     else if (!strcmp(k, "--row-max")) o.row_max = atoi(v);
+    else if (!strcmp(k, "--threads")) o.threads = atoi(v);
+    else if (!strcmp(k, "--shard")) {
+      if (sscanf(v, "%d/%d", &o.shard, &o.nshards) != 2 || o.nshards < 1 || o.shard < 0 || o.shard >= o.nshards) {
+        fprintf(stderr, "pwsynth: --shard r/N\n");
+        return 2;
+      }
+    }
     else {
       fprintf(stderr, "pwsynth: unknown option %s\n", k);
       return 2;
     }
   }
   if (!seed_set) o.seed = (uint64_t)(o.config > 0 ? o.config : 7);
+  if (o.nshards > 1 && o.config != 3) {
+    fprintf(stderr, "pwsynth: --shard is for --config 3 (per-record streams)\n");
+    return 2;
+  }
   g_rng = o.seed * 0x2545F4914F6CDD1Dull + 12345;
   if (!strcmp(argv[1], "paf")) {
     if (!o.fa || !o.paf) {

@@ -1,0 +1,105 @@
+"""GPU: the multi-GPU pafreport driver (pwasm_amd/mgpu.py) with 2 and 3 ranks, each packing its
+target-genome shard and running the HIP pass (all ranks on cuda:0 here, collectives over gloo —
+RCCL refuses two ranks on one GPU; on a node every rank has its own GPU and the backend is
+"nccl").  The merged report, stderr and exit code must equal the single-process oracle run; the
+node-wide per-genome table must equal one computed from the PAF and the oracle's report."""
+import collections
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ORACLE, run, synth_paf
+from test_gpu_parity import _inject
+from test_shard import _with_duplicates_and_comments
+
+pytestmark = pytest.mark.gpu
+
+
+def _rank(rank, world, port, argv, errf, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PW_DIST_BACKEND="gloo")
+    if rank == 0:
+        fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+        os.dup2(fd, 2)
+    from pwasm_amd import mgpu
+    import torch.distributed as dist
+    rc = mgpu.main(argv)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    q.put((rank, rc))
+
+
+def run_mgpu(world, argv, tmp_path):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    errf = str(tmp_path / "mg.err")
+    ps = [ctx.Process(target=_rank, args=(r, world, port, argv, errf, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    rcs = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(set(rcs.values())) == 1
+    return rcs[0], open(errf, "rb").read()
+
+
+def _genome_table_from(paf, report):
+    recs = [ln.split("\t") for ln in open(paf).read().splitlines() if ln and not ln.startswith("#")]
+    blocks = report.decode().split(">")[1:]
+    tab = collections.OrderedDict()
+    # records in report order are the PAF's kept records (dedupe / self alignments removed):
+    # match them by their header's target label
+    it = iter(recs)
+    for blk in blocks:
+        hdr = blk.split("\n", 1)[0]
+        tl = hdr.split(" ")[0].split("--")[-1]
+        while True:
+            f = next(it)
+            if f"{f[5]}:{f[7]}-{f[8]}{f[4]}" == tl:
+                break
+        r = tab.setdefault(f[5], [0, 0, 0])
+        r[0] += 1
+        r[1] += blk.count("\n") - 1
+        r[2] += int(f[8]) - int(f[7])
+    return tab
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_mgpu_matches_single_process(built, tmp_path, world):
+    fa, paf = synth_paf(tmp_path, 0, seed=17)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 2)
+    out = tmp_path / "r.txt"
+    tab = tmp_path / "g.tsv"
+    rc, err = run_mgpu(world, ["-r", fa, dup, "-o", str(out), "--genome-table", str(tab)], tmp_path)
+    orc, oout, oerr = run([ORACLE, "-r", fa, dup])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr)
+    want = _genome_table_from(dup, oout)
+    got = {}
+    for ln in tab.read_text().splitlines()[1:]:
+        t, a, e, b = ln.split("\t")
+        got[t] = [int(a), int(e), int(b)]
+    assert got == dict(want)
+
+
+def test_mgpu_fatal_midway(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 0, seed=41)
+    bad = _inject(paf, tmp_path, "mismatch", seed=5)
+    out = tmp_path / "r.txt"
+    rc, err = run_mgpu(2, ["-r", fa, bad, "-o", str(out)], tmp_path)
+    orc, oout, oerr = run([ORACLE, "-r", fa, bad])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr) and orc == 1
+
+
+def test_mgpu_cfg3_shards_gene_mode(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 3, scale=0.002)
+    out = tmp_path / "r.txt"
+    rc, err = run_mgpu(2, ["-G", "-C", "-r", fa, paf, "-o", str(out)], tmp_path)
+    orc, oout, oerr = run([ORACLE, "-G", "-C", "-r", fa, paf])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr) and orc == 0

@@ -171,3 +171,22 @@ def test_modseq_mismatch_reverse_u(built, tmp_path):
     rc, out, err = run([ORACLE, "-r", "q.fa", "a.paf"], cwd=str(tmp_path))
     assert rc == 1 and b"modseq" in err
     same(["-r", "q.fa", "a.paf"], cwd=str(tmp_path))
+
+
+# ---------------------------------------------------------------- pipelined CLI batches
+@pytest.mark.parametrize("chunk,kind", [(3000, None), (20000, None), (5000, "mismatch"), (7000, "crlf")])
+def test_cli_many_batches(built, tmp_path, chunk, kind, monkeypatch):
+    """The CLI reads the PAF in chunks (PW_CHUNK_BYTES), packs chunk k+1 while the GPU runs
+    chunk k, and the q~t dedupe state carries across chunks: same bytes as one pass."""
+    from test_gpu_parity import _inject
+    from test_shard import _with_duplicates_and_comments
+    fa, paf = synth_paf(tmp_path, 0, seed=23)
+    paf = _with_duplicates_and_comments(paf, tmp_path, 3)
+    if kind == "mismatch":
+        paf = _inject(paf, tmp_path, "mismatch", seed=9)
+    elif kind == "crlf":
+        p = tmp_path / "crlf.paf"
+        p.write_bytes(open(paf, "rb").read().replace(b"\n", b"\r\n"))
+        paf = str(p)
+    monkeypatch.setenv("PW_CHUNK_BYTES", str(chunk))
+    same(["-r", fa, paf])
