@@ -66,7 +66,7 @@ extern "C" int pw_gapassem_run(const char* layout_path, const char* out_path, ui
     w.clp5 = h[2];
     w.clp3 = h[3];
     w.revcompl = h[4];
-    w.base = seq.size();
+    w.base = (seq.size() + 7) / 8 * 8;  // rows start 8-base aligned: the count kernels' vector loads
     seq.resize(w.base + (size_t)w.seqlen);
     ofs.resize(w.base + (size_t)w.seqlen);
     if (fread(seq.data() + w.base, 1, (size_t)w.seqlen, f) != (size_t)w.seqlen ||

@@ -45,23 +45,25 @@
 #include <stdint.h>
 
 #include "pwasm_amd.h"
+#include "pw_wave.h"
 
 namespace pw {
 
 constexpr int kChunk = 256;   // bases per checkpoint chunk
 constexpr int kTileW = 2048;  // columns per workgroup
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int bin_of(uint8_t c) {
-  if (c >= 'a' && c <= 'z') c -= 32;
-  switch (c) {
-    case 'A': return 0;
-    case 'C': return 1;
-    case 'G': return 2;
-    case 'T': return 3;
-    case '-':
-    case '*': return 5;
-    default: return 4;
-  }
+// GAlnColumn::addNuc / addGap bin (GapAssem.h:295-337): toupper(c) A,C,G,T -> 0..3, '-' / '*' ->
+// 5 (gap), anything else -> 4 (N).  Branch-free: a switch compiles to a divergent compare tree.
+__device__ __forceinline__ int bin_of(uint32_t c) {
+  const uint32_t u = c & 0xDFu;  // clears bit 5 only: u == 'A' iff c is 'A' or 'a' (same for C, G, T)
+  int b = (c == '-' || c == '*') ? 5 : 4;
+  b = u == 'A' ? 0 : b;
+  b = u == 'C' ? 1 : b;
+  b = u == 'G' ? 2 : b;
+  b = u == 'T' ? 3 : b;
+  return b;
 }
 
 // K0: the row of every slot (slot_row), one workgroup per row, coalesced
@@ -70,63 +72,142 @@ __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* s
     for (int64_t k = A.slot_base[r] + threadIdx.x; k < A.slot_base[r + 1]; k += 256) slot_row[k] = (int32_t)r;
 }
 
-// per row: number of chunks = ceil(len / 256); chunk index space = prefix over rows
-__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const int32_t* slot_row) {
-  const int64_t* chunk_base = A.slot_base;
-  const uint64_t n_chunks = A.n_slots;
-  const int lane = threadIdx.x & 63;
-  const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  for (uint64_t c = wid; c < n_chunks; c += (uint64_t)gridDim.x * 4) {
-    const uint32_t r = (uint32_t)slot_row[c];
-    const int64_t k = (int64_t)c - chunk_base[r];
-    const int len = A.row_len[r];
-    const int64_t i0 = k * kChunk;
-    int s = 0;
+// K1: per 256-base chunk of a row, sum of (1 + max(ofs, 0)).  A wavefront takes 8 consecutive
+// slots at a time, 8 lanes per slot, 32 bases per lane (four 16-byte loads when the row starts
+// 8-base aligned); the next group's loads are issued before this group is reduced.
+__device__ __forceinline__ int adv_sum8(v4i q) {  // 8 int16 gaps packed in 16 bytes
+  int s = 8;
 #pragma unroll
-    for (int j = 0; j < kChunk / 64; j++) {
-      const int64_t i = i0 + j * 64 + lane;
-      if (i < len) {
-        const int g = A.ofs[A.row_off[r] + i];
-        s += 1 + (g > 0 ? g : 0);
-      }
+  for (int w = 0; w < 4; w++) {
+    const int lo = (int16_t)(q[w] & 0xFFFF), hi = (int16_t)((uint32_t)q[w] >> 16);
+    s += (lo > 0 ? lo : 0) + (hi > 0 ? hi : 0);
+  }
+  return s;
+}
+struct SumPre {
+  v4i q[4];
+  int len, i0;
+  uint32_t r;
+  bool vec;
+};
+__device__ __forceinline__ void sums_load(const pw_msa_args& A, const int32_t* slot_row, uint64_t g, int lane, SumPre& p) {
+  const uint64_t c = g * 8 + (uint64_t)(lane >> 3);
+  p.len = 0;
+  p.vec = false;
+  if (c >= A.n_slots) return;
+  p.r = (uint32_t)slot_row[c];
+  const int64_t k = (int64_t)c - A.slot_base[p.r];
+  p.len = A.row_len[p.r];
+  p.i0 = (int)(k * kChunk) + 32 * (lane & 7);
+  const uint64_t roff = A.row_off[p.r];
+  p.vec = (roff & 7) == 0 && p.i0 + 32 <= p.len;
+  if (p.vec) {
+    const v4i* src = reinterpret_cast<const v4i*>(A.ofs + roff + p.i0);
+#pragma unroll
+    for (int w = 0; w < 4; w++) p.q[w] = src[w];
+  } else {
+    int s = 0;  // (row tail / unaligned row: element loads, folded into q[0].x)
+    for (int i = p.i0; i < p.i0 + 32 && i < p.len; i++) {
+      const int gg = A.ofs[roff + i];
+      s += 1 + (gg > 0 ? gg : 0);
     }
+    p.q[0] = (v4i){s, 0, 0, 0};
+  }
+}
+__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const int32_t* slot_row) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t ng = (A.n_slots + 7) / 8;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  SumPre cur;
+  if (g < ng) sums_load(A, slot_row, g, lane, cur);
+  for (; g < ng; g += nw) {
+    SumPre nxt;
+    if (g + nw < ng) sums_load(A, slot_row, g + nw, lane, nxt);
+    int s = 0;
+    if (cur.vec) {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-    if (lane == 0) chunk_sum[c] = s;
+      for (int w = 0; w < 4; w++) s += adv_sum8(cur.q[w]);
+    } else if (cur.len > 0) {
+      s = cur.q[0].x;
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    const uint64_t c = g * 8 + (uint64_t)(lane >> 3);
+    if ((lane & 7) == 0 && c < A.n_slots) chunk_sum[c] = s;
+    cur = nxt;
   }
 }
 
-// one 64-thread workgroup per row: chunk checkpoints (column where chunk k's first gap run
-// starts), row extent, bounds check (MSAColumns::operator[], GapAssem.h:366-370)
-__global__ __launch_bounds__(64) void row_prefix(const pw_msa_args A, const int32_t* chunk_sum, int32_t* ckpt) {
+// K2: one 1024-thread workgroup per row: chunk checkpoints (column where chunk k's first gap run
+// starts) = col0 + exclusive scan of the chunk sums, row extent, bounds check
+// (MSAColumns::operator[], GapAssem.h:366-370).  Thread t owns a contiguous run of chunks.
+__global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const int32_t* chunk_sum, int32_t* ckpt) {
+  __shared__ int wsum[16];
   const int64_t* chunk_base = A.slot_base;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
     const int64_t b = chunk_base[r], e = chunk_base[r + 1];
-    int carry = A.col0[r];
-    for (int64_t k0 = b; k0 < e; k0 += 64) {
-      const int64_t k = k0 + lane;
-      const int v = (k < e) ? chunk_sum[k] : 0;
-      int incl = v;
+    const int64_t n = e - b, per = (n + 1023) / 1024;
+    const int64_t k0 = b + (int64_t)t * per, k1 = k0 + per < e ? k0 + per : e;
+    int mine = 0;
+    for (int64_t k = k0; k < k1; k++) mine += chunk_sum[k];
+    int incl = mine;
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        int t = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += t;
-      }
-      if (k < e) ckpt[k] = carry + incl - v;
-      carry += __shfl(incl, 63, 64);
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += v;
     }
-    if (lane == 0) {  // the row's last slot (chunk sum 0) now holds its end column + 1
-      const int last = carry - 1;
-      if (A.row_len[r] > 0 && (A.col0[r] < 0 || last >= A.n_cols)) {
-        atomicMin(&A.minmax[2], (int)r);  // first offending row; host reports the column
-      }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int base = A.col0[r];
+    for (int w = 0; w < wv; w++) base += wsum[w];
+    int run = base + incl - mine;
+    for (int64_t k = k0; k < k1; k++) {
+      ckpt[k] = run;
+      run += chunk_sum[k];
     }
+    if (t == 1023) {  // the row's last slot (chunk sum 0) now holds its end column + 1
+      const int last = run - 1;
+      if (A.row_len[r] > 0 && (A.col0[r] < 0 || last >= A.n_cols)) atomicMin(&A.minmax[2], (int)r);
+    }
+    __syncthreads();
   }
 }
 
-// counts for one column tile: 16 waves, each walks the chunks of its rows that overlap the
-// tile; the next chunk's bases / gaps are loaded while the current one is scanned
+// K3: counts for one column tile.  16 waves share the rows overlapping the tile; a wave walks its
+// row's 256-base chunks from the one holding the tile's first column: each lane takes 4
+// consecutive bases (one 4-byte + one 8-byte load when the row starts 4-base aligned; the next
+// chunk is loaded while this one is counted), a single wave scan of the lanes' column advances
+// gives every base its column (the closed form of toMSA, GapAssem.cpp:568-590), and the bases are
+// added to the LDS counters in four rounds in which lane l adds its base (round + l/8) % 4:
+// lanes 8 apart then hit columns 32 apart + 1, i.e. different banks.  Gap runs (ofs > 0, ~1 % of
+// bases) take a ballot-guarded per-lane loop.
+struct Quad {
+  uint32_t s4;  // 4 bases
+  v2u g4;       // 4 int16 gaps
+};
+__device__ __forceinline__ int16_t gap_of(const Quad& q, int j) {
+  return (int16_t)((j < 2 ? q.g4.x : q.g4.y) >> (16 * (j & 1)));
+}
+__device__ __forceinline__ void quad_load(const pw_msa_args& A, uint64_t roff, bool vec, int64_t i, int len, Quad& q) {
+  if (vec && i + 3 < len) {
+    q.s4 = *reinterpret_cast<const uint32_t*>(A.seq + roff + i);
+    q.g4 = *reinterpret_cast<const v2u*>(A.ofs + roff + i);
+  } else {
+    q.s4 = 0;
+    q.g4 = (v2u){0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (i + j < len) {
+        q.s4 |= (uint32_t)A.seq[roff + i + j] << (8 * j);
+        const uint32_t g = (uint16_t)A.ofs[roff + i + j];
+        if (j < 2) q.g4.x |= g << (16 * j);
+        else q.g4.y |= g << (16 * (j - 2));
+      }
+  }
+}
 constexpr int kTileWaves = 16;
 __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args A, const int32_t* ckpt) {
   const int64_t* chunk_base = A.slot_base;
@@ -137,6 +218,7 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
   for (int i = tid; i < 6 * kTileW; i += 64 * kTileWaves) (&cnt[0][0])[i] = 0;
   __syncthreads();
   int my_min = INT_MAX, my_max = -1;
+  const int rot = lane >> 3;
   for (uint32_t r = wv; r < A.n_rows; r += kTileWaves) {
     const int64_t b = chunk_base[r], e = chunk_base[r + 1] - 1;  // [b, e) chunks, e = end slot
     if (b == e) continue;
@@ -153,56 +235,53 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
       while (k + 1 < e && ckpt[k + 1] <= c0) k++;
     }
     const uint64_t roff = A.row_off[r];
+    const bool vec = (roff & 3) == 0;
     int col = ckpt[k];
-    int16_t g_nx[kChunk / 64];
-    uint8_t s_nx[kChunk / 64];
-    auto load = [&](int64_t kk) {
-      const int64_t ib = (kk - b) * kChunk;
-#pragma unroll
-      for (int j = 0; j < kChunk / 64; j++) {
-        const int64_t i = ib + j * 64 + lane;
-        g_nx[j] = i < len ? A.ofs[roff + i] : (int16_t)0;
-        s_nx[j] = i < len ? A.seq[roff + i] : (uint8_t)0;
-      }
-    };
-    load(k);
+    Quad nx;
+    quad_load(A, roff, vec, (k - b) * kChunk + 4 * lane, len, nx);
     for (; k < e && col < c1; k++) {
-      int16_t gg[kChunk / 64];
-      uint8_t ss[kChunk / 64];
+      const Quad q = nx;
+      const int64_t i0 = (k - b) * kChunk + 4 * lane;  // this lane's first base
+      if (k + 1 < e) quad_load(A, roff, vec, i0 + kChunk, len, nx);
+      int adv[4], gp[4];
+      int tot = 0;
 #pragma unroll
-      for (int j = 0; j < kChunk / 64; j++) {
-        gg[j] = g_nx[j];
-        ss[j] = s_nx[j];
+      for (int j = 0; j < 4; j++) {
+        const int g = gap_of(q, j);
+        gp[j] = g > 0 ? g : 0;
+        adv[j] = (i0 + j < len) ? 1 + gp[j] : 0;
+        tot += adv[j];
       }
-      if (k + 1 < e) load(k + 1);
-      const int64_t ib = (k - b) * kChunk;
+      const int incl = wave_scan_incl(tot);
+      int bcol[4];
+      bool take[4];
+      int run = col + incl - tot;
+      bool gaps = false;
 #pragma unroll
-      for (int j = 0; j < kChunk / 64; j++) {
-        const int64_t i = ib + j * 64 + lane;
-        const bool ok = i < len;
-        const int g0 = gg[j];
-        const int g = g0 > 0 ? g0 : 0;
-        const uint8_t ch = ss[j];
-        const int adv = ok ? 1 + g : 0;
-        int incl = adv;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          int t = __shfl_up(incl, d, 64);
-          if (lane >= d) incl += t;
-        }
-        const int bcol = col + incl - 1;  // this base's column
-        const int gstart = bcol - g;      // its gap run starts here
-        if (ok) {
-          const bool clipped = (i < cl) || (i >= len - cr);
-          if (!clipped) {
-            for (int c = gstart > c0 ? gstart : c0; c < bcol && c < c1; c++) atomicAdd(&cnt[5][c - c0], 1);
-            if (bcol >= c0 && bcol < c1) atomicAdd(&cnt[bin_of(ch)][bcol - c0], 1);
-            if (i == cl) my_min = min(my_min, gstart);
-            if (i == len - cr - 1) my_max = max(my_max, bcol);
-          }
-        }
-        col += __shfl(incl, 63, 64);
+      for (int j = 0; j < 4; j++) {
+        run += adv[j];
+        bcol[j] = run - 1;  // this base's column (its gap run starts at bcol - gp)
+        const int64_t i = i0 + j;
+        take[j] = i < len && i >= cl && i < len - cr;
+        if (take[j] && i == cl) my_min = min(my_min, bcol[j] - gp[j]);
+        if (take[j] && i == len - cr - 1) my_max = max(my_max, bcol[j]);
+        gaps = gaps || (take[j] && gp[j] > 0 && bcol[j] > c0 && bcol[j] - gp[j] < c1);
       }
+#pragma unroll
+      for (int kk = 0; kk < 4; kk++) {
+        const int j = (kk + rot) & 3;
+        const int bc = j == 0 ? bcol[0] : (j == 1 ? bcol[1] : (j == 2 ? bcol[2] : bcol[3]));
+        const bool tk = j == 0 ? take[0] : (j == 1 ? take[1] : (j == 2 ? take[2] : take[3]));
+        const uint32_t ch = (q.s4 >> (8 * j)) & 0xFFu;
+        if (tk && bc >= c0 && bc < c1) atomicAdd(&cnt[bin_of(ch)][bc - c0], 1);
+      }
+      if (__ballot(gaps)) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (take[j] && gp[j] > 0)
+            for (int c = max(bcol[j] - gp[j], c0); c < bcol[j] && c < c1; c++) atomicAdd(&cnt[5][c - c0], 1);
+      }
+      col += wave_last(incl);
     }
   }
   // fold mincol / maxcol
@@ -422,10 +501,10 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   static const int32_t init[4] = {INT_MAX, -1, INT_MAX, INT_MAX};
   if (hipMemcpyAsync(a->minmax, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return PW_E_HIP;
   hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row);
-  const uint64_t nb1 = (a->n_slots + 3) / 4;
-  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 65536 ? nb1 : 65536)), dim3(256), 0, s, *a,
+  const uint64_t nb1 = ((a->n_slots + 7) / 8 + 3) / 4;  // 8 slots per wave, 4 waves per workgroup
+  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 4096 ? nb1 : 4096)), dim3(256), 0, s, *a,
                      chunk_sum, slot_row);
-  hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, chunk_sum, ckpt);
+  hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(1024), 0, s, *a, chunk_sum, ckpt);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kTileW - 1) / pw::kTileW);
   hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kTileWaves), 0, s, *a, ckpt);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;

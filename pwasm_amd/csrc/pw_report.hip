@@ -38,6 +38,7 @@
 
 #include "pw_tables.h"
 #include "pwasm_amd.h"
+#include "pw_wave.h"
 
 namespace pw {
 
@@ -104,14 +105,7 @@ struct SmallTables {
 };
 
 // ------------------------------------------------------------------ wave primitives
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    uint32_t t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int) { return wave_scan_incl(v); }
 __device__ __forceinline__ uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, kWave); }
 // LDS written by some lanes of a wavefront and read by others of the SAME wavefront (the
 // waves of a workgroup are independent): LDS operations of one wave execute in order, so only
@@ -1103,9 +1097,9 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       qs[k] = qc + (int)(qtot + qi_ - qa);
       ts[k] = tc + (int)(ttot + ti_ - ta);
       ls[k] = lc + ltot + li_ - la;
-      qtot += bcast(qi_, 63);
-      ttot += bcast(ti_, 63);
-      ltot += bcast(li_, 63);
+      qtot += wave_last(qi_);
+      ttot += wave_last(ti_);
+      ltot += wave_last(li_);
       w->opw[kOpHalo + idx] = wd[k];
     }
     if (lane < 2) {  // halo: the op words just before / after the segment (tctx_fast's neighbours)
@@ -1462,7 +1456,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     const uint32_t fn_cur = h.fn;
     h = load_hot(W, c + nw, lane);  // the next chunk's records load behind this one's output
     const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
-    const uint32_t B = bcast(incl, kWave - 1);
+    const uint32_t B = wave_last(incl);
     const uint32_t my_off = incl - (uint32_t)linelen;
     // the page: in place, or an arena allocation when the lines do not fit
     uint64_t P = c * (uint64_t)PW_PAGE_BYTES;
@@ -1613,7 +1607,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
     const uint32_t f4 = (fi < nf32 ? f32[fi] : 0u) & 0x01010101u;
     const uint32_t cnt = (uint32_t)__popc(f4);
     const uint32_t incl = wave_incl_scan(cnt, lane);
-    const uint32_t total = bcast(incl, kWave - 1);
+    const uint32_t total = wave_last(incl);
     if (total == 0) continue;
     uint32_t o = incl - cnt;
 #pragma unroll

@@ -105,9 +105,16 @@ class HipEngine:
         if nr == 0:
             raise ValueError("gapassem: a shard without rows")
         lens = np.array([int(lay.seqlen[r]) for r in rows], dtype=np.int32)
-        row_off = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))])[:nr].astype(np.uint64)
-        seq = np.concatenate([lay.seq[r] for r in rows])
-        ofs = np.concatenate([lay.ofs[r] for r in rows])
+        # rows start 8-base aligned (the count kernels' vector loads); the gaps between rows are zero
+        padded = (lens.astype(np.uint64) + 7) // 8 * 8
+        row_off = np.concatenate([[0], np.cumsum(padded)])[:nr].astype(np.uint64)
+        total = int(row_off[-1] + padded[-1]) if nr else 0
+        seq = np.zeros(max(total, 1), dtype=np.uint8)
+        ofs = np.zeros(max(total, 1), dtype=np.int16)
+        for k, r in enumerate(rows):
+            o = int(row_off[k])
+            seq[o:o + int(lens[k])] = lay.seq[r]
+            ofs[o:o + int(lens[k])] = lay.ofs[r]
         cl = np.array([lay.clips(r)[0] for r in rows], dtype=np.int32)
         cr = np.array([lay.clips(r)[1] for r in rows], dtype=np.int32)
         col0 = np.array([int(lay.offset[r]) - lay.minoffset for r in rows], dtype=np.int32)
