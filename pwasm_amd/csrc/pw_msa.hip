@@ -68,6 +68,8 @@ __device__ __forceinline__ int bin_of(uint32_t c) {
 
 // K0: the row of every slot (slot_row), one workgroup per row, coalesced
 __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row) {
+  if (blockIdx.x == 0 && threadIdx.x < 4)  // minmax sentinels (no host copy on the stream)
+    A.minmax[threadIdx.x] = threadIdx.x == 1 ? -1 : INT_MAX;
   for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x)
     for (int64_t k = A.slot_base[r] + threadIdx.x; k < A.slot_base[r + 1]; k += 256) slot_row[k] = (int32_t)r;
 }
@@ -181,9 +183,9 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
 // consecutive bases (one 4-byte + one 8-byte load when the row starts 4-base aligned; the next
 // chunk is loaded while this one is counted), a single wave scan of the lanes' column advances
 // gives every base its column (the closed form of toMSA, GapAssem.cpp:568-590), and the bases are
-// added to the LDS counters in four rounds in which lane l adds its base (round + l/8) % 4:
-// lanes 8 apart then hit columns 32 apart + 1, i.e. different banks.  Gap runs (ofs > 0, ~1 % of
-// bases) take a ballot-guarded per-lane loop.
+// added to the LDS counters (bin from a 256-entry LDS table).  Gap runs (ofs > 0, ~1 % of bases)
+// take a ballot-guarded per-lane loop; mincol / maxcol are only evaluated in the chunks holding
+// the row's first / last unclipped base.
 struct Quad {
   uint32_t s4;  // 4 bases
   v2u g4;       // 4 int16 gaps
@@ -191,7 +193,7 @@ struct Quad {
 __device__ __forceinline__ int16_t gap_of(const Quad& q, int j) {
   return (int16_t)((j < 2 ? q.g4.x : q.g4.y) >> (16 * (j & 1)));
 }
-__device__ __forceinline__ void quad_load(const pw_msa_args& A, uint64_t roff, bool vec, int64_t i, int len, Quad& q) {
+__device__ __forceinline__ void quad_load(const pw_msa_args& A, uint64_t roff, bool vec, int i, int len, Quad& q) {
   if (vec && i + 3 < len) {
     q.s4 = *reinterpret_cast<const uint32_t*>(A.seq + roff + i);
     q.g4 = *reinterpret_cast<const v2u*>(A.ofs + roff + i);
@@ -211,21 +213,24 @@ __device__ __forceinline__ void quad_load(const pw_msa_args& A, uint64_t roff, b
 constexpr int kTileWaves = 16;
 __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args A, const int32_t* ckpt) {
   const int64_t* chunk_base = A.slot_base;
-  __shared__ int32_t cnt[6][kTileW];
+  __shared__ int32_t cnt[6 * kTileW];
+  __shared__ uint8_t bin_lut[256];  // GAlnColumn::addNuc/addGap bin of every byte, x kTileW
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * kTileW;
   const int c1 = min(c0 + kTileW, A.n_cols);
-  for (int i = tid; i < 6 * kTileW; i += 64 * kTileWaves) (&cnt[0][0])[i] = 0;
+  const uint32_t tw = (uint32_t)(c1 - c0);
+  for (int i = tid; i < 6 * kTileW; i += 64 * kTileWaves) cnt[i] = 0;
+  if (tid < 256) bin_lut[tid] = (uint8_t)bin_of((uint32_t)tid);
   __syncthreads();
   int my_min = INT_MAX, my_max = -1;
-  const int rot = lane >> 3;
   for (uint32_t r = wv; r < A.n_rows; r += kTileWaves) {
     const int64_t b = chunk_base[r], e = chunk_base[r + 1] - 1;  // [b, e) chunks, e = end slot
     if (b == e) continue;
     const int rs = ckpt[b], re = ckpt[e];  // row columns [rs, re)
     if (re <= c0 || rs >= c1) continue;
     const int len = A.row_len[r];
-    const int cl = A.clip_l[r], cr = A.clip_r[r];
+    const int lo = A.clip_l[r], hi = len - A.clip_r[r];  // bases [lo, hi) are counted (unclipped)
+    const uint32_t span = hi > lo ? (uint32_t)(hi - lo) : 0u;
     // first chunk whose columns reach c0 (last k with ckpt[k] <= c0): interpolate, then step
     int64_t k = b;
     if (c0 > rs) {
@@ -237,11 +242,11 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
     const uint64_t roff = A.row_off[r];
     const bool vec = (roff & 3) == 0;
     int col = ckpt[k];
+    int i0 = (int)(k - b) * kChunk + 4 * lane;  // this lane's first base of the chunk
     Quad nx;
-    quad_load(A, roff, vec, (k - b) * kChunk + 4 * lane, len, nx);
-    for (; k < e && col < c1; k++) {
+    quad_load(A, roff, vec, i0, len, nx);
+    for (; k < e && col < c1; k++, i0 += kChunk) {
       const Quad q = nx;
-      const int64_t i0 = (k - b) * kChunk + 4 * lane;  // this lane's first base
       if (k + 1 < e) quad_load(A, roff, vec, i0 + kChunk, len, nx);
       int adv[4], gp[4];
       int tot = 0;
@@ -253,33 +258,33 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
         tot += adv[j];
       }
       const int incl = wave_scan_incl(tot);
+      int run = col + incl - tot;
       int bcol[4];
       bool take[4];
-      int run = col + incl - tot;
       bool gaps = false;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         run += adv[j];
-        bcol[j] = run - 1;  // this base's column (its gap run starts at bcol - gp)
-        const int64_t i = i0 + j;
-        take[j] = i < len && i >= cl && i < len - cr;
-        if (take[j] && i == cl) my_min = min(my_min, bcol[j] - gp[j]);
-        if (take[j] && i == len - cr - 1) my_max = max(my_max, bcol[j]);
-        gaps = gaps || (take[j] && gp[j] > 0 && bcol[j] > c0 && bcol[j] - gp[j] < c1);
+        bcol[j] = run - 1;  // this base's column; its gap run is [bcol - gp, bcol)
+        take[j] = (uint32_t)(i0 + j - lo) < span;
+        gaps = gaps || (take[j] && gp[j] > 0);
+        const uint32_t o = (uint32_t)(bcol[j] - c0);
+        if (take[j] && o < tw) atomicAdd(&cnt[bin_lut[(q.s4 >> (8 * j)) & 0xFFu] * kTileW + o], 1);
       }
+      // mincol / maxcol: only the chunks holding the first / last unclipped base
+      const int cb = (int)(k - b) * kChunk;
+      if ((uint32_t)(lo - cb) < (uint32_t)kChunk || (uint32_t)(hi - 1 - cb) < (uint32_t)kChunk) {
 #pragma unroll
-      for (int kk = 0; kk < 4; kk++) {
-        const int j = (kk + rot) & 3;
-        const int bc = j == 0 ? bcol[0] : (j == 1 ? bcol[1] : (j == 2 ? bcol[2] : bcol[3]));
-        const bool tk = j == 0 ? take[0] : (j == 1 ? take[1] : (j == 2 ? take[2] : take[3]));
-        const uint32_t ch = (q.s4 >> (8 * j)) & 0xFFu;
-        if (tk && bc >= c0 && bc < c1) atomicAdd(&cnt[bin_of(ch)][bc - c0], 1);
+        for (int j = 0; j < 4; j++) {
+          if (take[j] && i0 + j == lo) my_min = min(my_min, bcol[j] - gp[j]);
+          if (take[j] && i0 + j == hi - 1) my_max = max(my_max, bcol[j]);
+        }
       }
       if (__ballot(gaps)) {
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (take[j] && gp[j] > 0)
-            for (int c = max(bcol[j] - gp[j], c0); c < bcol[j] && c < c1; c++) atomicAdd(&cnt[5][c - c0], 1);
+            for (int c = max(bcol[j] - gp[j], c0); c < bcol[j] && c < c1; c++) atomicAdd(&cnt[5 * kTileW + c - c0], 1);
       }
       col += wave_last(incl);
     }
@@ -297,7 +302,7 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
   __syncthreads();
   // the tile's counters, coalesced: column-major in LDS -> [col][6] rows in memory
   int32_t* dst = A.counts + (int64_t)c0 * 6;
-  for (int i = tid; i < (c1 - c0) * 6; i += 64 * kTileWaves) dst[i] = cnt[i % 6][i / 6];
+  for (int i = tid; i < (c1 - c0) * 6; i += 64 * kTileWaves) dst[i] = cnt[(i % 6) * kTileW + i / 6];
 }
 
 // bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage
@@ -498,8 +503,6 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
   int32_t* slot_row = a->scratch + 2 * a->n_slots;
-  static const int32_t init[4] = {INT_MAX, -1, INT_MAX, INT_MAX};
-  if (hipMemcpyAsync(a->minmax, init, sizeof init, hipMemcpyHostToDevice, s) != hipSuccess) return PW_E_HIP;
   hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row);
   const uint64_t nb1 = ((a->n_slots + 7) / 8 + 3) / 4;  // 8 slots per wave, 4 waves per workgroup
   hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 4096 ? nb1 : 4096)), dim3(256), 0, s, *a,
