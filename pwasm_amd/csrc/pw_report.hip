@@ -56,8 +56,9 @@ constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
 constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
 constexpr int kQWin = 48;       // render_kernel: forward-query window per lane (bytes)
 constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dword reads at most 2-way)
-constexpr int kLine = 96;       // render_kernel: per-lane report-line buffer (bytes)
-constexpr int kLStride = 100;   // ... its LDS stride (25 dwords: per-lane byte stores conflict-free)
+constexpr int kLine = 88;       // render_kernel: report lines up to this long are built in LDS (99.5 % at cfg2)
+constexpr int kLSlack = 44;     // ... + slack: a field block (<= 40 bytes) never needs a bounds check
+constexpr int kLStride = kLine + kLSlack;  // 132 bytes = 33 dwords: per-lane byte stores conflict-free
 constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
@@ -143,17 +144,22 @@ struct Rec {
 
 // Query byte x of the forward query, 0 outside [0, L) (the NUL / missing bytes).  The LDS
 // window holds zeros where it extends past the query, so a window hit needs no bounds check.
+// (outside the window: rare, kept out of line so the hot paths stay small)
+__device__ __noinline__ uint8_t rc_global(const uint8_t* R, int L, int x) {
+  return (unsigned)x < (unsigned)L ? R[x] : (uint8_t)0;
+}
 __device__ __forceinline__ uint8_t Rc(const Rec& r, int x) {
   const unsigned o = (unsigned)(x - r.qlo);
   if (o < (unsigned)r.qn) return r.qw[o];
-  return (unsigned)x < (unsigned)r.L ? r.R[x] : (uint8_t)0;
+  return rc_global(r.R, r.L, x);
 }
+__device__ __noinline__ uint8_t lit_global(const uint8_t* lits, uint32_t i) { return lits[i]; }
 __device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
   const uint32_t o = i - r.ls0;
   if (o < r.ln) return (uint8_t)((o < 4 ? r.lit0 : r.lit1) >> (8 * (o & 3)));
   const uint32_t ow = i - r.l_lo;
   if (ow < r.l_n) return r.lw[ow];
-  return r.lits[i];
+  return lit_global(r.lits, i);
 }
 __device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
   const unsigned o = (unsigned)((int)j - r.op_lo);
@@ -215,12 +221,10 @@ struct EvIn {
   uint32_t typ;
   int n, qp, tloc;
   uint32_t ls;
-  int tmode;          // 0 fast (ll / rl), 1 pre-rendered (tx), 2 op walk (j, wd, qs, ts)
+  int tmode;          // 0 fast (ll / rl), 1 pre-rendered by tctx_kernel (tx)
   int ll, rl;
-  const LDS uint8_t* tx;  // length byte + field (tmode 1): an LDS copy of the tx record
+  uint32_t tx[6];     // length byte + field (tmode 1): the tx record's first 24 bytes
   int ns_pre;         // next_stop entry the indel scan needs, loaded ahead (kNsNone: not loaded)
-  uint32_t j, wd;
-  int qs, ts;
 };
 constexpr int kNsNone = INT_MIN;
 
@@ -287,30 +291,34 @@ __device__ __forceinline__ uint64_t lds8(const LDS uint8_t* qw, int off) {
 // character is stored anyway and then overwritten, and runs of characters fold into the
 // immediate offsets of the byte stores.  GlobalSink writes straight to global memory
 // (fixup_kernel lines).
+// Line bytes are stored one ds_write_b8 each through a volatile pointer: left alone, the compiler
+// merges runs of byte stores at fixed offsets into ds_write_b64/b96/b128 at byte-aligned
+// addresses, which the LDS replays at 64 cycles per wave-instruction (SQ_LDS_UNALIGNED_STALL).
+__device__ __forceinline__ void st8(LDS uint8_t* p, uint8_t c) { *(volatile LDS uint8_t*)p = c; }
 struct RawSink {
   LDS uint8_t* buf;
   int pos;
   __device__ __forceinline__ void put(uint8_t c) {
-    buf[pos] = c;
+    st8(buf + pos, c);
     pos++;
   }
   __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
-    buf[pos] = c;
+    st8(buf + pos, c);
     pos += pred ? 1 : 0;
   }
-  __device__ __forceinline__ void put_at(int i, uint8_t c) { buf[i] = c; }
+  __device__ __forceinline__ void put_at(int i, uint8_t c) { st8(buf + i, c); }
   // bytes 1.. of w, n of them (n <= 4 * N - 1): all stored at fixed offsets, then pos += n
   template <int N>
   __device__ __forceinline__ void put_span(const uint32_t (&w)[N], int n) {
 #pragma unroll
-    for (int q = 0; q < 4 * N - 1; q++) buf[pos + q] = (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3)));
+    for (int q = 0; q < 4 * N - 1; q++) st8(buf + pos + q, (uint8_t)(w[(q + 1) >> 2] >> (8 * ((q + 1) & 3))));
     pos += n;
   }
   // the first n bytes of w (all 4N stored at fixed offsets; the block reserved them)
   template <int N>
   __device__ __forceinline__ void put_bytes(const uint32_t (&w)[N], int n) {
 #pragma unroll
-    for (int q = 0; q < 4 * N; q++) buf[pos + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+    for (int q = 0; q < 4 * N; q++) st8(buf + pos + q, (uint8_t)(w[q >> 2] >> (8 * (q & 3))));
     pos += n;
   }
   template <class F>
@@ -361,7 +369,26 @@ struct LdsSink {
     }
   }
 };
-typedef LdsSink<kLine> LineSink;
+// ClampSink: render_kernel's line buffer (kLine bytes + kLSlack).  Every field goes through a
+// block of at most 40 bytes written with a RawSink (no per-character checks): a block starting
+// at pos <= kLine ends inside the slack; once pos passes kLine the line is long (fixup_kernel
+// rewrites it) and the block is folded back onto the slack.
+struct ClampSink {
+  LDS uint8_t* line;
+  int pos;
+  template <class F>
+  __device__ __forceinline__ void block(int, F&& f) {
+    const int p0 = pos < kLine ? pos : kLine;
+    RawSink u{line + (p0 - pos), pos};
+    f(u);
+    pos = u.pos;
+  }
+  __device__ __forceinline__ void put(uint8_t c) {
+    st8(line + (pos < kLine ? pos : kLine), c);
+    pos++;
+  }
+};
+typedef ClampSink LineSink;
 struct GlobalSink {
   uint8_t* p;
   int pos;
@@ -431,26 +458,30 @@ __device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, 
   }
 }
 
-// "%d" of a non-negative int
+// "%d" of a non-negative int, digit by digit (numbers >= 10^8: rare, out of line)
 template <class S>
-__device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
-  if (v >= 100000u) {
-    for (uint32_t P = 1000000000u; P >= 100000u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
-  }
-#pragma unroll
-  for (uint32_t P = 10000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
+__device__ __noinline__ void wr_dig(S& k, uint32_t v) {
+  for (uint32_t P = 1000000000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   k.put((uint8_t)('0' + v % 10u));
 }
-// "%d" through the digit-pair table for v < 10000 (two LDS reads, 4 bytes stored at fixed
-// offsets; needs 4 bytes of room); the division ladder otherwise
+// "%d" through the digit-pair table for v < 10^8 (up to four LDS reads, the digits stored at
+// fixed offsets; needs 8 bytes of room)
 template <class S>
 __device__ __forceinline__ void wr_num(S& k, const LDS SmallTables* t, uint32_t v) {
+  const LDS uint16_t* d2 = reinterpret_cast<const LDS uint16_t*>(t->dig2);
   if (v < 10000u) {
     const uint32_t hi = v / 100u, lo = v - 100u * hi;
-    const uint32_t p = (uint32_t)*reinterpret_cast<const LDS uint16_t*>(t->dig2 + 2 * hi) |
-                       (uint32_t)*reinterpret_cast<const LDS uint16_t*>(t->dig2 + 2 * lo) << 16;
+    const uint32_t p = (uint32_t)d2[hi] | (uint32_t)d2[lo] << 16;
     const int nd = 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u);
     const uint32_t w[1] = {p >> (8 * (4 - nd))};
+    k.put_bytes(w, nd);
+  } else if (v < 100000000u) {
+    const uint32_t h = v / 10000u, l = v - 10000u * h;
+    const uint32_t hh = h / 100u, hl = h - 100u * hh, lh = l / 100u, ll = l - 100u * lh;
+    const uint64_t p = (uint64_t)d2[hh] | (uint64_t)d2[hl] << 16 | (uint64_t)d2[lh] << 32 | (uint64_t)d2[ll] << 48;
+    const int nd = 5 + (h >= 10u) + (h >= 100u) + (h >= 1000u);
+    const uint64_t q = p >> (8 * (8 - nd));
+    const uint32_t w[2] = {(uint32_t)q, (uint32_t)(q >> 32)};
     k.put_bytes(w, nd);
   } else {
     wr_dig(k, v);
@@ -835,18 +866,12 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
     o.put('\t');
   });
   // ---- target context (setTContext :120-128, revCompl :631, abbreviation :918-927)
-  if (in.tmode == 2) {
-    emit_tctx_walk(k, r, typ, e.n, in.j, in.wd, in.qs, in.ts, in.ls);
-  } else {
+  {
     k.block(10 + kMaxEv + 4, [&](auto& o) {
       if (in.tmode == 0) {
         emit_tctx_fast(o, r, typ, e.n, in.qp, in.ls, in.ll, in.rl);
       } else {
-        uint32_t tw[6];
-        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(in.tx);
-#pragma unroll
-        for (int q = 0; q < 6; q++) tw[q] = t32[q];
-        o.put_span(tw, (int)(tw[0] & 0xFFu));
+        o.put_span(in.tx, (int)(in.tx[0] & 0xFFu));
       }
     });
   }
@@ -924,7 +949,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
         }
         if (caa != cmaa) {
           const uint32_t ap = (uint32_t)(ao + e.rloc / 3);
-          k.block(18 + (cmaa == '.' ? 31 : 0), [&](auto& o) {
+          k.block(18, [&](auto& o) {
             if (any) wr_lit(o, ", ");
             wr_lit(o, "AA");
             wr_num(o, r.tab, ap);
@@ -932,11 +957,12 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
             o.put(caa);
             o.put(':');
             o.put(cmaa);
-            if (cmaa == '.') {
+          });
+          if (cmaa == '.')
+            k.block(31, [&](auto& o) {
               wr_lit(o, "|premature stop at AA");
               wr_num(o, r.tab, ap);
-            }
-          });
+            });
           any = true;
         }
       }
@@ -1292,7 +1318,6 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
-  uint8_t txw[kWave * kTxL];        // per-lane copy of the event's tx record (tmode 1)
   uint32_t ostart[kWave + 1];       // line starts in the page
   uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
 };
@@ -1340,7 +1365,6 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
   LDS RenderWave* w = (LDS RenderWave*)&rw[wv];
   LDS uint8_t* my_line = w->line + lane * kLStride;
   LDS uint8_t* my_qw = w->qw + lane * kQStride;
-  LDS uint8_t* my_tx = w->txw + lane * kTxL;
   const bool skip = A.skip_codan != 0;
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
 
@@ -1419,12 +1443,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       in.rl = (int)((h.fn >> 20) & 7u);
       // loads issued ahead of the line (their latency overlaps the query-window staging): the
       // pre-rendered target context and the next-stop entry the indel stop scan ends on
-      in.tx = my_tx;
-      if (use_tx) {
-        LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(my_tx);
-        d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
-        d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
-      }
+      in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
       in.ns_pre = kNsNone;
       if (typ != PW_OP_SUB && r.NS && !skip) {
         const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
@@ -1432,11 +1451,8 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         const int k0 = rl + dl + (15 - a - x);
         if (a + x <= 15 && (r.L - rt) + x - dl > 17 && k0 >= 0 && k0 < r.L) in.ns_pre = r.NS[k0];
       }
-      in.j = in.wd = 0;
-      in.qs = in.ts = 0;
       LineSink k;
-      k.buf = my_line;
-      k.junk = my_line + kLine;  // (the stride's spare bytes)
+      k.line = my_line;
       k.pos = 0;
       int rel = 0;
       const int merr = emit_event(k, r, in, skip, rel);
@@ -1515,8 +1531,9 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       if (lane == 0) w->ostart[kWave] = B;
       if (linelen > 0) {
         const uint32_t c1 = (my_off + (uint32_t)linelen + 15) >> 4;
-        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) w->cmap[ci] = (uint8_t)lane;
-        if (my_off == 0) w->cmap[0] = (uint8_t)lane;
+        // (byte stores: a vectorised fill would be unaligned ds_write_b128)
+        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) st8(&w->cmap[ci], (uint8_t)lane);
+        if (my_off == 0) st8(&w->cmap[0], (uint8_t)lane);
       }
       wave_sync();
       // gather: each lane assembles 16 output bytes from (at most a few) line buffers with
@@ -1701,7 +1718,6 @@ constexpr int kFxLit = 32;
 struct FixLane {
   uint8_t qw[kQWin];
   uint8_t lw[kFxLit];
-  uint8_t tx[kTxL];
 };
 __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
@@ -1752,12 +1768,11 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
       ne = event_len(r, cd.j, r.ops[cd.j]);
     }
     // windows: tx record, 48 query bytes from 8 before the event, 32 literal bytes from ls
+    v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
     if (use_tx) {
       const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * f.s);
-      const v4u t0 = tp4[0], t1 = tp4[1];
-      LDS uint32_t* d32 = reinterpret_cast<LDS uint32_t*>(me->tx);
-      d32[0] = t0.x, d32[1] = t0.y, d32[2] = t0.z, d32[3] = t0.w;
-      d32[4] = t1.x, d32[5] = t1.y, d32[6] = t1.z, d32[7] = t1.w;
+      t0 = tp4[0];
+      t1 = tp4[1];
     }
     const int rl = event_rloc(r.L, rev, typ, h.qp, ne);
     int x0 = rl - 8;
@@ -1785,10 +1800,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     in.tmode = use_tx ? 1 : 0;
     in.ll = (int)((h.fn >> 23) & 7u);
     in.rl = (int)((h.fn >> 20) & 7u);
-    in.tx = me->tx;
+    in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
     in.ns_pre = kNsNone;
-    in.j = in.wd = 0;
-    in.qs = in.ts = 0;
     GlobalSink g;
     g.p = A.text + f.dst;
     g.pos = 0;
