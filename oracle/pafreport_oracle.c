@@ -424,10 +424,201 @@ static void td_free(tdiff_vec* v) {
 static const char* CIGAR_ERROR = "Error parsing cigar string from line: %s (cigar position: %s)\n";
 static const char* CS_ERROR = "Error parsing cs string from line: %s (cs position: %s)\n";
 
+/* ------------------------------------------------------------------ -w: GapAssem layout
+ * Literal restatement of the progressive MSA construction pafreport -w performs
+ * (pafreport.cpp:382-421, 447-450): GASeq::setGap/addGap (GapAssem.cpp:104-120),
+ * GSeqAlign(s1,s2) (:605-641), addAlign (:645-690), addSeq (:694-716), injectGap (:720-753),
+ * finalize/prepSeq (:1006-1012, 89-101) and writeMSA/printMFasta (:1039-1046, 482-520).
+ * O(rows x L) per injected gap, exactly as the reference. */
+typedef struct {
+  int pos, len;
+} gapdata; /* GapData, pafreport.cpp:48-52 */
+typedef struct {
+  gapdata* d;
+  int n, cap;
+} gapvec;
+static void gv_add(gapvec* v, int pos, int len) {
+  if (v->n == v->cap) {
+    v->cap = v->cap ? 2 * v->cap : 16;
+    v->d = (gapdata*)realloc(v->d, sizeof(gapdata) * (size_t)v->cap);
+  }
+  v->d[v->n].pos = pos;
+  v->d[v->n].len = len;
+  v->n++;
+}
+
+struct gsalign;
+typedef struct {
+  char* id;
+  char* seq; /* NULL: not loaded (an instance of the query in one alignment) */
+  int len;   /* loaded sequence length (0 when not loaded) */
+  int seqlen;
+  short* ofs;
+  int numgaps, offset;
+  char revcompl, prepped;
+  struct gsalign* msa;
+} gaseq;
+typedef struct gsalign {
+  gaseq** rows;
+  int n, cap, length, minoffset;
+} gsalign;
+
+static gaseq* ga_new(const char* id, const char* seq, int slen, int offset) {
+  gaseq* g = (gaseq*)calloc(1, sizeof(gaseq));
+  g->id = strdup(id);
+  if (seq) {
+    g->seq = (char*)malloc((size_t)slen + 1);
+    memcpy(g->seq, seq, (size_t)slen);
+    g->seq[slen] = 0;
+    g->len = slen;
+  }
+  g->seqlen = slen;
+  g->ofs = (short*)calloc((size_t)(slen > 0 ? slen : 1), sizeof(short));
+  g->offset = offset;
+  return g;
+}
+static void ga_free(gaseq* g) {
+  free(g->id);
+  free(g->seq);
+  free(g->ofs);
+  free(g);
+}
+static void ga_setgap(gaseq* g, int pos, short gaplen) { /* GASeq::setGap :104-111 */
+  if (pos < 0 || pos >= g->seqlen) gerror("Error: invalid gap position (%d) given for sequence %s\n", pos + 1, g->id);
+  g->numgaps -= g->ofs[pos];
+  g->ofs[pos] = gaplen;
+  g->numgaps += gaplen;
+}
+static void ga_addgap(gaseq* g, int pos, short gapadd) { /* GASeq::addGap :114-120 */
+  if (pos < 0 || pos >= g->seqlen) gerror("Error: invalid gap position (%d) given for sequence %s\n", pos + 1, g->id);
+  g->numgaps += gapadd;
+  g->ofs[pos] += gapadd;
+}
+static int ga_endoffset(const gaseq* g) { return g->offset + g->seqlen + g->numgaps; }
+static void msa_add(gsalign* m, gaseq* s) {
+  if (m->n == m->cap) {
+    m->cap = m->cap ? 2 * m->cap : 8;
+    m->rows = (gaseq**)realloc(m->rows, sizeof(gaseq*) * (size_t)m->cap);
+  }
+  m->rows[m->n++] = s;
+}
+static gsalign* msa_new2(gaseq* s1, gaseq* s2) { /* GSeqAlign(s1, s2) :605-641 */
+  gsalign* m = (gsalign*)calloc(1, sizeof(gsalign));
+  s1->msa = m;
+  s2->msa = m;
+  msa_add(m, s1);
+  msa_add(m, s2);
+  m->minoffset = s1->offset < s2->offset ? s1->offset : s2->offset;
+  int e1 = ga_endoffset(s1), e2 = ga_endoffset(s2);
+  m->length = (e1 > e2 ? e1 : e2) - m->minoffset;
+  return m;
+}
+static void msa_inject_gap(gsalign* m, gaseq* seq, int pos, int xgap) { /* injectGap :720-753 */
+  int alpos = seq->offset + pos;
+  for (int i = 0; i <= pos; i++) alpos += seq->ofs[i];
+  for (int i = 0; i < m->n; i++) {
+    gaseq* s = m->rows[i];
+    int spos = 0;
+    if (s == seq) {
+      spos = pos;
+    } else {
+      int salpos = s->offset;
+      if (salpos >= alpos) {
+        s->offset += xgap;
+        continue;
+      }
+      while (spos < s->seqlen) {
+        salpos += 1 + s->ofs[spos];
+        if (salpos > alpos) break;
+        spos++;
+      }
+      if (spos >= s->seqlen) continue;
+    }
+    ga_addgap(s, spos, (short)xgap);
+  }
+  m->length += xgap;
+}
+static void msa_add_seq(gsalign* m, gaseq* s, int soffs) { /* addSeq :694-716 (ng_ofs unused here) */
+  s->offset = soffs;
+  s->msa = m;
+  msa_add(m, s);
+  if (soffs < m->minoffset) {
+    m->length += m->minoffset - soffs;
+    m->minoffset = soffs;
+  }
+  if (ga_endoffset(s) - m->minoffset > m->length) m->length = ga_endoffset(s) - m->minoffset;
+}
+/* addAlign :645-690 (both instances of the query are forward here: no revComplement) */
+static void msa_add_align(gsalign* m, gaseq* seq, gsalign* om, gaseq* oseq) {
+  if (seq->seqlen != oseq->seqlen)
+    gerror("GSeqAlign Error: invalid merge %s(len %d) vs %s(len %d)\n", seq->id, seq->seqlen, oseq->id, oseq->seqlen);
+  for (int i = 0; i < seq->seqlen; i++) {
+    int d = seq->ofs[i] - oseq->ofs[i];
+    if (d > 0) msa_inject_gap(om, oseq, i, d);
+    else if (d < 0) msa_inject_gap(m, seq, i, -d);
+  }
+  for (int i = 0; i < om->n; i++) {
+    gaseq* s = om->rows[i];
+    if (s == oseq) continue;
+    msa_add_seq(m, s, seq->offset + s->offset - oseq->offset);
+  }
+  ga_free(oseq);
+  free(om->rows);
+  free(om);
+}
+/* writeMSA :1039-1046 -> finalize -> prepSeq (revcompl) -> printMFasta :482-520 */
+static void msa_write(gsalign* m, FILE* f) {
+  for (int i = 0; i < m->n; i++) {
+    gaseq* s = m->rows[i];
+    if (s->len == 0) gerror("Error: sequence for %s not loaded!\n", s->id);
+    if (!s->prepped) {
+      if (s->revcompl == 1) {
+        gstr g;
+        g.s = s->seq;
+        g.len = s->len;
+        rev_compl(&g);
+      }
+      s->prepped = 1;
+    }
+  }
+  for (int i = 0; i < m->n; i++) {
+    gaseq* s = m->rows[i];
+    const int llen = 60;
+    fprintf(f, ">%s\n", s->id);
+    int printed = 0;
+    for (int k = 0; k < s->offset; k++) {
+      fputc('-', f);
+      if (++printed == llen) {
+        fputc('\n', f);
+        printed = 0;
+      }
+    }
+    for (int k = 0; k < s->seqlen; k++) {
+      if (s->ofs[k] < 0) continue;
+      for (int j = 0; j < s->ofs[k]; j++) {
+        fputc('-', f);
+        if (++printed == llen) {
+          fputc('\n', f);
+          printed = 0;
+        }
+      }
+      char c = s->seq[k];
+      printed++;
+      if (printed == llen) {
+        fprintf(f, "%c\n", c);
+        printed = 0;
+      } else {
+        fputc(c, f);
+      }
+    }
+    if (printed < llen) fputc('\n', f);
+  }
+}
+
 /* Decode: PAFAlignment::PAFAlignment, pafreport.cpp:477-719.
  * rs/rlen = the aligned-strand query (forward, or reverse complement for '-'). */
 static void paf_decode(char** t, int tnum, const aln_info* al, const char* rs, int rlen, gstr* tseq,
-                       const char* line, tdiff_vec* tdiffs, int* edist, int* alnscore) {
+                       const char* line, tdiff_vec* tdiffs, int* edist, int* alnscore, gapvec* rgaps, gapvec* tgaps) {
   int reverse = al->reverse;
   int offset = al->r_alnstart; /* :486-490 */
   if (reverse) offset = al->r_len - al->r_alnend;
@@ -598,7 +789,8 @@ static void paf_decode(char** t, int tnum, const aln_info* al, const char* rs, i
       tdiffs->d[j] = s;
     }
   }
-  /* CIGAR :645-718 (gap lists are only consumed by -w) */
+  /* CIGAR :645-718 (gap lists rgaps / tgaps are only consumed by -w) */
+  rgaps->n = tgaps->n = 0;
   p = cigar;
   qpos = 0;
   tpos = 0;
@@ -621,11 +813,13 @@ static void paf_decode(char** t, int tnum, const aln_info* al, const char* rs, i
         qpos += cl;
         gmessage("Warning: soft clipping shouldn't be found in this application!\n%s\n", line);
         break;
-      case 'I':
+      case 'I': /* gap in the target :685-691 */
+        gv_add(tgaps, reverse ? eff_t_len - tpos : tpos, cl);
         qpos += cl;
         break;
-      case 'D':
-      case 'N':
+      case 'D': /* gap in the query :692-700 */
+      case 'N': /* :701-711 */
+        gv_add(rgaps, reverse ? al->r_len - (offset + qpos) : offset + qpos, cl);
         tpos += cl;
         break;
       default:
@@ -1014,13 +1208,18 @@ int main(int argc, char* argv[]) {
   if (!fullgenome && !gene_cds && fsize > 120000) fullgenome = 1;
   g_skip_codan = (fullgenome || force_noncoding);
   if (!g_skip_codan && !force_coding && fsize > 120000) g_skip_codan = 1;
-  if (args.set['w'] && args.val['w'][0]) {
+  FILE* fmsa = NULL;
+  if (args.set['w'] && args.val['w'][0]) { /* :263-273 */
     if (fullgenome) {
       gmessage("%s Error: can only generate MSA for -G mode!\n", USAGE);
       exit(1);
     }
-    gerror("Error: -w (MSA output) is not supported by this oracle\n");
+    fmsa = fopen(args.val['w'], "w");
+    if (!fmsa) gerror("Cannot open file %s for writing!\n", args.val['w']);
   }
+  gapvec rgaps = {0}, tgaps = {0};
+  gaseq* ga_ref = NULL; /* GASeq of the current query (:341-351); NULL until it is first used */
+  gsalign* ref_msa = NULL; /* refMSA */
   strmap alnpairs = {0};
   gstr lbuf, lstr, tseq, qtpair, tlabel, rlabel;
   gs_init(&lbuf);
@@ -1076,6 +1275,7 @@ int main(int argc, char* argv[]) {
       }
     }
     if (refseq == NULL || strcmp(refseq->id, al.r_id) != 0) { /* :338-354 */
+      ga_ref = NULL; /* a new GASeq for the query: its msa starts empty (rseqs is never filled) */
       fa_rec* r = fasta_fetch(&qfasta, al.r_id);
       if (!r) gerror("Error: could not retrieve sequence for %s !\n", al.r_id);
       refseq = r;
@@ -1091,7 +1291,7 @@ int main(int argc, char* argv[]) {
     const char* r_seq = al.reverse ? refseq_rc : refseq->seq;
     tdiff_vec tdiffs = {0};
     int edist, alnscore;
-    paf_decode(t, numt, &al, r_seq, refseq->len, &tseq, lstr.s, &tdiffs, &edist, &alnscore);
+    paf_decode(t, numt, &al, r_seq, refseq->len, &tseq, lstr.s, &tdiffs, &edist, &alnscore, &rgaps, &tgaps);
     gs_set(&tlabel, al.t_id);
     gs_set(&rlabel, al.r_id);
     if (fullgenome) {
@@ -1108,6 +1308,26 @@ int main(int argc, char* argv[]) {
     if (qfasta.n == 1 && !fullgenome) gs_clear(&rlabel);
     print_diff_info(freport, rlabel.s, tlabel.s, &al, alnscore, edist, &tdiffs, refseq->seq, refseq->len);
     td_free(&tdiffs);
+    if (fmsa) { /* :382-421 */
+      gaseq* taseq = ga_new(tlabel.s, tseq.s, tseq.len, al.r_alnstart);
+      taseq->revcompl = (char)al.reverse;
+      if (ga_ref == NULL) ga_ref = ga_new(refseq->id, refseq->seq, refseq->len, 0);
+      gaseq* rseq = ga_ref;
+      const int first = ga_ref->msa == NULL;
+      if (!first) rseq = ga_new(refseq->id, NULL, al.r_len, 0);
+      for (int g = 0; g < rgaps.n; g++) ga_setgap(rseq, rgaps.d[g].pos, (short)rgaps.d[g].len);
+      for (int g = 0; g < tgaps.n; g++) ga_setgap(taseq, tgaps.d[g].pos, (short)tgaps.d[g].len);
+      gsalign* newmsa = msa_new2(rseq, taseq);
+      if (first) ref_msa = newmsa;
+      else {
+        msa_add_align(ga_ref->msa, ga_ref, newmsa, rseq);
+        ref_msa = ga_ref->msa;
+      }
+    }
+  }
+  if (fmsa) { /* :447-450 (no alignment at all: the reference dereferences NULL; here: empty file, D10) */
+    if (ref_msa) msa_write(ref_msa, fmsa);
+    fclose(fmsa);
   }
   if (g_items) {
     fclose(g_items);

@@ -1352,9 +1352,69 @@ __device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
   return h;
 }
 
+// What a lane needs from global memory before its line can be rendered besides the Hot record:
+// the forward-query window, the tx record, the next-stop entry and, for a record's first / last
+// line, the record index.  Issued for chunk c + NW while chunk c writes its page (the Hot record
+// of c + NW was loaded one chunk earlier), so the latency hides behind a whole output phase.
+struct RenderPre {
+  v4u q[kQWin / 16];  // 48 forward-query bytes from the 16-byte aligned qlo
+  v4u t0, t1;         // tx record (pre-rendered target context)
+  int qlo;            // forward position of q[0]
+  int n;              // evtbases length (resolved when the Hot field saturates)
+  int ns;             // next-stop entry the indel scan ends on (kNsNone: not needed)
+  uint32_t ai;        // record of a first / last line
+};
+__device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& W, const Hot& h, uint64_t s, bool skip,
+                                           RenderPre& p) {
+  p.ns = kNsNone;
+  p.ai = 0;
+  p.n = 0;
+  p.qlo = 0;
+  if (h.fn == kNoEv) return;
+  const uint32_t typ = h.fn >> 30;
+  const bool rev = (h.fn >> 29) & 1u;
+  int n = (int)(h.fn & kNBig);
+  if (!((h.fn >> 28) & 1u)) {
+    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+    p.t0 = tp4[0];
+    p.t1 = tp4[1];
+  }
+  if (h.fn & (3u << 26)) p.ai = W.cold[s].ai;
+  const uint8_t* R = A.qseq + ((uint64_t)h.qb << 4);
+  if ((uint32_t)n == kNBig) {  // saturated length: from the op stream (rare; dependent loads)
+    const Cold cd = W.cold[s];
+    const pw_aln_desc d = A.desc[cd.ai];
+    Rec r;
+    r.ops = A.ops + d.op_begin;
+    r.n_ops = d.n_ops;
+    r.op_n = 0;
+    r.op_lo = 0;
+    r.opw = nullptr;
+    n = event_len(r, cd.j, r.ops[cd.j]);
+  }
+  p.n = n;
+  // 48 forward-query bytes from 8 before the event (16-byte aligned; covers [rloc - 8, rloc + 25],
+  // the reads of all but long deletions)
+  const int rl = event_rloc(h.L, rev, typ, h.qp, n);
+  int x0 = rl - 8;
+  if (x0 < 0) x0 = 0;
+  const uintptr_t a0 = (uintptr_t)(R + x0) & ~(uintptr_t)15;  // >= qseq (16-byte aligned)
+#pragma unroll
+  for (int q = 0; q < kQWin / 16; q++) p.q[q] = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+  p.qlo = (int)((intptr_t)a0 - (intptr_t)R);
+  if (typ != PW_OP_SUB && A.next_stop && !skip) {
+    const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
+    const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
+    const int k0 = rl + dl + (15 - a - x);
+    if (a + x <= 15 && (h.L - rt) + x - dl > 17 && k0 >= 0 && k0 < h.L)
+      p.ns = A.next_stop[((uint64_t)h.qb << 4) + (uint64_t)k0];
+  }
+}
+
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
 // inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
-// chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).
+// chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).  Hot records are loaded
+// two chunks ahead, the rest of a lane's inputs one chunk ahead (render_pre).
 __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];
@@ -1370,6 +1430,9 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
 
   uint64_t c = (uint64_t)blockIdx.x * kWaves + wv;
   Hot h = load_hot(W, c, lane);
+  Hot hn = load_hot(W, c + nw, lane);
+  RenderPre pre;
+  render_pre(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
   for (; c < W.n_chunks; c += nw) {
     const uint64_t s = c * kWave + (uint64_t)lane;
     const bool act = h.fn != kNoEv;
@@ -1377,16 +1440,8 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     if (act) {
       const uint32_t typ = h.fn >> 30;
       const bool rev = (h.fn >> 29) & 1u;
-      int n = (int)(h.fn & kNBig);
-      // the pre-rendered target context (tctx_kernel) is loaded first: its latency overlaps the
-      // query-window loads below
+      const int n = pre.n;
       const bool use_tx = !((h.fn >> 28) & 1u);
-      v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
-      if (use_tx) {
-        const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
-        t0 = tp4[0];
-        t1 = tp4[1];
-      }
       Rec r;
       r.lits = A.lits;
       r.R = A.qseq + ((uint64_t)h.qb << 4);
@@ -1407,30 +1462,15 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       r.acgt = (h.fn & kFnAcgt) != 0;
       r.offset = 0;
       r.T = 0;
-      r.qn = 0;
-      if ((uint32_t)n == kNBig) {  // saturated length: from the op stream
-        const Cold cd = W.cold[s];
-        const pw_aln_desc d = A.desc[cd.ai];
-        r.ops = A.ops + d.op_begin;
-        r.n_ops = d.n_ops;
-        n = event_len(r, cd.j, r.ops[cd.j]);
-      }
       r.ops = nullptr;
       r.n_ops = 0;
-      // per-lane window: 48 forward-query bytes from 8 before the event (16-byte aligned; covers
-      // [rloc - 8, rloc + 25], the reads of all but long deletions)
-      const int rl = event_rloc(r.L, rev, typ, h.qp, n);
-      int x0 = rl - 8;
-      if (x0 < 0) x0 = 0;
-      const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;  // >= qseq (16-byte aligned)
 #pragma unroll
       for (int q = 0; q < kQWin / 16; q++) {
-        const v4u v = *reinterpret_cast<const v4u*>(a0 + 16 * q);
-        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){v.x, v.y};
-        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){v.z, v.w};
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};
       }
       r.qw = my_qw;
-      r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+      r.qlo = pre.qlo;
       r.qn = kQWin;
       EvIn in;
       in.typ = typ;
@@ -1441,16 +1481,9 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       in.tmode = use_tx ? 1 : 0;
       in.ll = (int)((h.fn >> 23) & 7u);
       in.rl = (int)((h.fn >> 20) & 7u);
-      // loads issued ahead of the line (their latency overlaps the query-window staging): the
-      // pre-rendered target context and the next-stop entry the indel stop scan ends on
-      in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
-      in.ns_pre = kNsNone;
-      if (typ != PW_OP_SUB && r.NS && !skip) {
-        const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
-        const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
-        const int k0 = rl + dl + (15 - a - x);
-        if (a + x <= 15 && (r.L - rt) + x - dl > 17 && k0 >= 0 && k0 < r.L) in.ns_pre = r.NS[k0];
-      }
+      in.tx[0] = pre.t0.x, in.tx[1] = pre.t0.y, in.tx[2] = pre.t0.z, in.tx[3] = pre.t0.w, in.tx[4] = pre.t1.x,
+      in.tx[5] = pre.t1.y;
+      in.ns_pre = pre.ns;
       LineSink k;
       k.line = my_line;
       k.pos = 0;
@@ -1470,7 +1503,11 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       }
     }
     const uint32_t fn_cur = h.fn;
-    h = load_hot(W, c + nw, lane);  // the next chunk's records load behind this one's output
+    const uint32_t ai_cur = pre.ai;
+    // the next chunk's inputs load behind this one's output
+    h = hn;
+    hn = load_hot(W, c + 2 * nw, lane);
+    render_pre(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);
     const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
     const uint32_t B = wave_last(incl);
     const uint32_t my_off = incl - (uint32_t)linelen;
@@ -1496,7 +1533,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     }
     const uint64_t g0 = P + my_off;
     if (act && (fn_cur & (3u << 26))) {  // first / last line of a record
-      const uint32_t ai = W.cold[s].ai;
+      const uint32_t ai = ai_cur;
       if ((fn_cur >> 27) & 1u) {
         A.results[ai].text_off = g0;
         A.results[ai].page_first = (uint32_t)c;
