@@ -244,7 +244,8 @@ typedef struct pw_batch_view {
   uint64_t alg_bytes_in; /* algorithmic input bytes of one pass */
   uint32_t skip_codan;
 } pw_batch_view;
-/* flags: bit0 = -G, bit1 = -F, bit2 = -C, bit3 = -N (same defaults as the CLI) */
+/* flags: bit0 = -G, bit1 = -F, bit2 = -C, bit3 = -N (same defaults as the CLI), bit4 = -w (keep the
+ * gap lists and the last query run for pw_batch_write_msa) */
 pw_batch* pw_batch_from_files(const char* fasta, const char* paf, uint32_t flags, char* errbuf, size_t errlen);
 int pw_batch_view_get(const pw_batch* b, pw_batch_view* out);
 /* Render the report (headers + event text) for results of a finished batch into `path`
@@ -259,6 +260,11 @@ int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_
 int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                          const pw_page* pages_host, const char* path);
 void pw_batch_free(pw_batch* b);
+/* `pafreport -w`: the multi-FASTA MSA of the batch's last query run (refMSA->writeMSA,
+ * pafreport.cpp:382-421, 447-450; GapAssem.cpp:645-753, 1006-1046) from its gap lists — the
+ * query's gap profile is the elementwise max of the alignments' query gaps and target-only
+ * bases are left-packed in it.  Needs flags bit4. */
+int pw_batch_write_msa(const pw_batch* b, const char* path);
 
 /* ---------------------------------------------------------------- multi-GPU
  * Shard by target genome: rank `shard` of `nshards` packs only the PAF lines whose target name

@@ -27,7 +27,7 @@ PW_REC_OK, PW_REC_MISMATCH, PW_REC_MODSEQ = 0, 1, 2
 DEV_PAD = 256  # readable bytes required past the end of the device query / literal arrays
 
 # pafreport mode flags for pw_batch_from_files (same meaning as -G/-F/-C/-N)
-FLAG_G, FLAG_F, FLAG_C, FLAG_N = 1, 2, 4, 8
+FLAG_G, FLAG_F, FLAG_C, FLAG_N, FLAG_W = 1, 2, 4, 8, 16
 
 
 class AlnDesc(ctypes.Structure):
@@ -124,6 +124,7 @@ _SIGS = {
     "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_char_p]),
     "pw_batch_free": (None, [ctypes.c_void_p]),
+    "pw_batch_write_msa": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "pw_version": (ctypes.c_char_p, []),
     "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
     "pw_batch_from_files_shard": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
@@ -218,6 +219,10 @@ class HostBatch:
     def write_items_from(self, dev: dict, path: str) -> int:
         return self.write_items(dev["text"].cpu().numpy(), dev["results"].cpu().numpy(), dev["pages"].cpu().numpy(),
                                 path)
+
+    def write_msa(self, path: str) -> int:
+        """-w: the MSA of the last query run as multi-FASTA (needs FLAG_W)."""
+        return lib().pw_batch_write_msa(self._h, str(path).encode())
 
     def genomes(self):
         """-> (genome index per record [n_alns] uint32, aligned target bases [n_alns] int32,

@@ -24,6 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "pw_msa_layout.h"
 #include "pwasm_amd.h"
 
 namespace {
@@ -385,6 +386,7 @@ struct Options {
   bool fullgenome = false, skip_codan = false, verbose = false;
   bool single_query_gene = false;  // rlabel "" (pafreport.cpp:378-379)
   uint32_t shard = 0, nshards = 1;  // multi-GPU: only lines whose target hashes to `shard`
+  bool msa = false;                 // -w: gap lists, setGap checks and the query run are kept
 };
 
 struct RecHost {                // (trivial: lives in PodVec; pack_line sets every field)
@@ -398,6 +400,11 @@ struct RecHost {                // (trivial: lives in PodVec; pack_line sets eve
   int32_t qlen;
   uint32_t tname_off, tname_len;  // target name (per-genome tables of the multi-GPU driver)
   int32_t t_aln;                // aligned target bases (t_alnend - t_alnstart)
+  // -w (Options::msa): the alignment's gap lists in Batch::gaps (rgaps then tgaps), its tlabel
+  // in the header pool after the header, and the setGap error it ends with
+  int32_t w_msg;
+  int32_t r_alnstart, t_len;
+  uint32_t gap_off, n_rg, n_tg, lab_len;
 };
 
 // Ordered log of what a batch prints: messages, records, a terminating fatal.
@@ -426,9 +433,11 @@ struct Batch {
   PodVec<pw_aln_desc> desc;
   PodVec<uint32_t> ops;
   PodVec<uint8_t> lits;
+  PodVec<int32_t> gaps;  // -w: (pos, len) pairs
   uint64_t text_total = 0, n_events_max = 0;
   bool fatal = false;
   void clear_out() {
+    gaps.clear();
     hdr.clear();
     msgs.clear();
     log.clear();
@@ -467,7 +476,7 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
       break;
     }
   std::vector<uint64_t> o_desc(np + 1), o_ops(np + 1), o_lits(np + 1), o_hdr(np + 1), o_msg(np + 1), o_log(np + 1),
-      o_ev(np + 1), o_txt(np + 1);
+      o_ev(np + 1), o_txt(np + 1), o_gap(np + 1);
   for (size_t i = 0; i < np; i++) {
     const Batch& p = parts[i];
     o_desc[i + 1] = o_desc[i] + p.desc.size();
@@ -478,10 +487,13 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
     o_log[i + 1] = o_log[i] + p.log.size();
     o_ev[i + 1] = o_ev[i] + p.n_events_max;
     o_txt[i + 1] = o_txt[i] + p.text_total;
+    o_gap[i + 1] = o_gap[i] + p.gaps.size();
   }
   const size_t d0 = b.desc.size(), op0 = b.ops.size(), l0 = b.lits.size(), h0 = b.hdr.size(), m0 = b.msgs.size(),
                g0 = b.log.size();
   const uint64_t e0 = b.n_events_max;
+  const size_t gp0 = b.gaps.size();
+  b.gaps.resize(gp0 + o_gap[np]);
   b.desc.resize(d0 + o_desc[np]);
   b.recs.resize(d0 + o_desc[np]);
   b.ops.resize(op0 + o_ops[np]);
@@ -509,10 +521,13 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
         if (r.pre_msg >= 0) r.pre_msg += dm;
         if (r.cs_msg >= 0) r.cs_msg += dm;
         if (r.post_msg >= 0) r.post_msg += dm;
+        if (r.w_msg >= 0) r.w_msg += dm;
+        r.gap_off += (uint32_t)(gp0 + o_gap[i]);
         b.recs[d0 + o_desc[i] + k] = r;
       }
       if (!p.ops.empty()) memcpy(&b.ops[op0 + o_ops[i]], p.ops.data(), p.ops.size() * 4);
       if (!p.lits.empty()) memcpy(&b.lits[l0 + o_lits[i]], p.lits.data(), p.lits.size());
+      if (!p.gaps.empty()) memcpy(&b.gaps[gp0 + o_gap[i]], p.gaps.data(), p.gaps.size() * 4);
       if (!p.hdr.empty()) memcpy(&b.hdr[h0 + o_hdr[i]], p.hdr.data(), p.hdr.size());
       for (size_t k = 0; k < p.msgs.size(); k++) b.msgs[m0 + o_msg[i] + k] = std::move(p.msgs[k]);
       for (size_t k = 0; k < p.log.size(); k++) {
@@ -691,13 +706,55 @@ struct Packer {
     });
     const double t_3 = prof ? now() : 0;
     append_parts(b, parts, nt);
+    if (opt.msa) track_run(b);
     if (prof)
       fprintf(stderr, "[pack] %zu lines, %d threads: classify %.3f dedupe %.3f pack %.3f append %.3f s\n", nl, nt,
               t_1 - t_0, t_2 - t_1, t_3 - t_2, now() - t_3);
   }
 
+  // -w: the alignments of the current query run, in input order (a record of another query
+  // starts a new run: pafreport fetches a fresh refseq GASeq at every query switch, :338-351)
+  pw::MsaRun run;
+  void track_run(const Batch& b) {
+    for (size_t k = 0; k < b.recs.size(); k++) {
+      const RecHost& rh = b.recs[k];
+      const pw_aln_desc& d = b.desc[k];
+      if (rh.pre_msg >= 0 || rh.cs_msg >= 0 || rh.post_msg >= 0 || rh.w_msg >= 0) return;  // the run stops here
+      const int qi = (int)(d.ref & PW_REF_QMASK);
+      if (run.qi != qi) {
+        run.clear();
+        run.qi = qi;
+      }
+      pw::MsaRec m;
+      m.offset = d.offset;
+      m.r_alnstart = rh.r_alnstart;
+      m.t_len = rh.t_len;
+      m.reverse = (d.ref & PW_REF_REVERSE) ? 1 : 0;
+      m.op_begin = (uint32_t)run.ops.size();
+      m.n_ops = d.n_ops;
+      uint32_t nl = 0;
+      for (uint32_t j = 0; j < d.n_ops; j++) {
+        const uint32_t w = b.ops[d.op_begin + j];
+        run.ops.push_back(w);
+        nl += (w >> 30) == PW_OP_SUB ? 2u : ((w >> 30) == PW_OP_INS ? (w & 0x3FFFFFFFu) : 0u);
+      }
+      m.lit_begin = (uint32_t)run.lits.size();
+      m.n_lits = nl;
+      run.lits.insert(run.lits.end(), b.lits.data() + d.lit_begin, b.lits.data() + d.lit_begin + nl);
+      m.gap_off = (uint32_t)run.gaps.size();
+      m.n_rg = rh.n_rg;
+      m.n_tg = rh.n_tg;
+      run.gaps.insert(run.gaps.end(), b.gaps.data() + rh.gap_off, b.gaps.data() + rh.gap_off + 2 * (rh.n_rg + rh.n_tg));
+      m.lab_off = (uint32_t)run.labels.size();
+      m.lab_len = rh.lab_len;
+      run.labels.append(b.hdr.data() + rh.hdr_off + rh.hdr_len, rh.lab_len);
+      run.recs.push_back(m);
+    }
+  }
+
   // One input line (pafreport.cpp:304-382).
   void pack_line(Batch& b, const char* base, const LineRef& lr, const LineInfo& li, std::vector<uint32_t>& fs) {
+    thread_local std::vector<std::pair<int, int>> rgl, tgl;  // -w gap lists of this record
     const char* s = base + lr.off;  // the untouched, NUL-terminated line (lstr)
     const uint32_t n = lr.len;
     if (li.kind == kLineSkip) return;
@@ -755,8 +812,12 @@ struct Packer {
     }
     // ---- record
     RecHost rh;
-    rh.pre_msg = rh.cs_msg = rh.post_msg = -1;
+    rh.pre_msg = rh.cs_msg = rh.post_msg = rh.w_msg = -1;
     rh.n_softclip = 0;
+    rh.r_alnstart = r_alnstart;
+    rh.t_len = 0;
+    rh.gap_off = (uint32_t)b.gaps.size();
+    rh.n_rg = rh.n_tg = rh.lab_len = 0;
     rh.line_off = lr.off;
     rh.qlen = L;
     rh.tname_off = (uint32_t)(t_id - s);
@@ -834,6 +895,8 @@ struct Packer {
         const char* p = cigar;
         int qpos = 0, tpos = 0;
         std::string err;
+        rgl.clear();
+        tgl.clear();
         while (p < cigar_end) {
           int cl = 0;
           if (!parse_int(p, cigar_end, cl)) {
@@ -859,9 +922,15 @@ struct Packer {
               qpos += cl;
               rh.n_softclip++;
               break;
-            case 'I': qpos += cl; break;
-            case 'D':
-            case 'N': tpos += cl; break;
+            case 'I':  // gap in the target (pafreport.cpp:685-691)
+              if (opt.msa) tgl.push_back({reverse ? eff_t_len - tpos : tpos, cl});
+              qpos += cl;
+              break;
+            case 'D':  // gap in the query (:692-711)
+            case 'N':
+              if (opt.msa) rgl.push_back({reverse ? r_len - (offset + qpos) : offset + qpos, cl});
+              tpos += cl;
+              break;
             default:
               err = strf("Error: unhandled cigar_op %c (len %d) in %s\n", cop, cl, s);
               bad = true;
@@ -877,7 +946,36 @@ struct Packer {
             err = strf("Error: ref alignment length mismatch (%d vs %d-%d) at line:%s\n", qpos, r_alnend,
                        r_alnstart, s);
         }
-        if (!err.empty()) rh.post_msg = (int32_t)b.add_msg(std::move(err));
+        if (!err.empty()) {
+          rh.post_msg = (int32_t)b.add_msg(std::move(err));
+        } else if (opt.msa) {
+          // -w: rseq->setGap / taseq->setGap after the report block (pafreport.cpp:394-404)
+          rh.t_len = tot.t_total;
+          for (auto& g : rgl) {
+            b.gaps.push_back(g.first);
+            b.gaps.push_back(g.second);
+          }
+          for (auto& g : tgl) {
+            b.gaps.push_back(g.first);
+            b.gaps.push_back(g.second);
+          }
+          rh.n_rg = (uint32_t)rgl.size();
+          rh.n_tg = (uint32_t)tgl.size();
+          for (auto& g : rgl)
+            if (g.first < 0 || g.first >= r_len) {
+              rh.w_msg = (int32_t)b.add_msg(strf("Error: invalid gap position (%d) given for sequence %.*s\n",
+                                                 g.first + 1, r_idn, r_id));
+              break;
+            }
+          if (rh.w_msg < 0)
+            for (auto& g : tgl)
+              if (g.first < 0 || g.first >= tot.t_total) {
+                rh.w_msg = (int32_t)b.add_msg(strf("Error: invalid gap position (%d) given for sequence %.*s:%d-%d%c\n",
+                                                   g.first + 1, t_idn, t_id, t_alnstart, t_alnend,
+                                                   reverse ? '-' : '+'));
+                break;
+              }
+        }
       }
     }
     // header (printDiffInfo, pafreport.cpp:886-892; labels :366-379)
@@ -907,6 +1005,13 @@ struct Packer {
       b.hdr.append(h.data(), h.size());
     }
     rh.hdr_len = (uint32_t)(b.hdr.size() - rh.hdr_off);
+    if (opt.msa) {  // the taseq name (tlabel) right after the header
+      char lb[300];
+      const int ln = snprintf(lb, sizeof lb, "%.*s:%d-%d%c", t_idn > 256 ? 256 : t_idn, t_id, t_alnstart, t_alnend,
+                              reverse ? '-' : '+');
+      b.hdr.append(lb, (size_t)ln);
+      rh.lab_len = (uint32_t)ln;
+    }
     b.desc.push_back(d);
     b.recs.push_back(rh);
     b.log.push_back({1, (uint32_t)b.recs.size() - 1, b.cur_line});
@@ -1184,7 +1289,12 @@ int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_a
     post = strf("Error: modseq[%d] not matching di.evtsub[%d] !\n", r.err_a, r.err_b);
   }
   write_lines(text, pages, r, nlines, out);
-  if (nlines == r.n_events) return -1;
+  if (nlines == r.n_events) {
+    if (rh.w_msg < 0) return -1;
+    fflush(out);  // -w: rseq / taseq setGap failed after the report block (pafreport.cpp:394-404)
+    fputs(b.msgs[rh.w_msg].c_str(), err);
+    return 1;
+  }
   fflush(out);
   fputs(post.c_str(), err);
   return 1;
@@ -1354,13 +1464,17 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   if (!fullgenome && !gene && fsize > 120000) fullgenome = true;
   bool skip_codan = fullgenome || force_noncoding;
   if (!skip_codan && !force_coding && fsize > 120000) skip_codan = true;
-  if (args.set['w'] && args.val['w'][0]) {
+  FileCloser fmsa;
+  if (args.set['w'] && args.val['w'][0]) {  // pafreport.cpp:263-273
     if (fullgenome) {
       fprintf(stderr, "%s Error: can only generate MSA for -G mode!\n", USAGE);
       return 1;
     }
-    fprintf(stderr, "Error: -w (MSA output) is not supported by this build yet\n");
-    return 1;
+    fmsa.f = fopen(args.val['w'], "w");
+    if (!fmsa.f) {
+      fprintf(stderr, "Cannot open file %s for writing!\n", args.val['w']);
+      return 1;
+    }
   }
   Device dev;
   if (!dev.init(qdb, skip_codan)) return 2;
@@ -1371,6 +1485,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   pk.opt.skip_codan = skip_codan;
   pk.opt.verbose = verbose;
   pk.opt.single_query_gene = (qdb.ids.size() == 1 && !fullgenome);
+  pk.opt.msa = fmsa.f != nullptr;
   // Pipeline: while the GPU runs batch k and its report is written, batch k + 1 is read and
   // packed (by pk.nt threads); nothing past a fatal batch is packed.
   ChunkReader rd(in.f);
@@ -1408,6 +1523,12 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     cur ^= 1;
   }
   fflush(out.f);
+  if (fmsa.f && pk.run.qi >= 0) {  // refMSA->writeMSA(fmsa), pafreport.cpp:447-450
+    const int qi = pk.run.qi;
+    const int rc = pw::write_run_msa(fmsa.f, qdb.ids[(size_t)qi].c_str(), qdb.seq.data() + qdb.off[(size_t)qi],
+                                 qdb.len[(size_t)qi], pk.run);
+    if (rc != 0) return rc;
+  }
   return 0;
 }
 
@@ -1453,6 +1574,7 @@ extern "C" pw_batch* pw_batch_from_files_shard(const char* fasta, const char* pa
   bt->pk.opt.single_query_gene = (bt->q.ids.size() == 1 && !full);
   bt->pk.opt.shard = shard;
   bt->pk.opt.nshards = nshards;
+  bt->pk.opt.msa = (flags & 16u) != 0 && !full;
   FILE* f = fopen(paf, "rb");
   if (!f) {
     delete bt;
@@ -1542,6 +1664,19 @@ extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host
   }
   if (fclose(f) != 0 && ret == PW_OK) ret = PW_E_IO;
   return ret;
+}
+
+extern "C" int pw_batch_write_msa(const pw_batch* bt, const char* path) {
+  if (!bt || !path || !bt->pk.opt.msa) return PW_E_ARG;
+  FILE* f = fopen(path, "w");
+  if (!f) return PW_E_IO;
+  int rc = 0;
+  const pw::MsaRun& run = bt->pk.run;
+  if (run.qi >= 0)
+    rc = pw::write_run_msa(f, bt->q.ids[(size_t)run.qi].c_str(), bt->q.seq.data() + bt->q.off[(size_t)run.qi],
+                           bt->q.len[(size_t)run.qi], run);
+  if (fclose(f) != 0 && rc == 0) rc = PW_E_IO;
+  return rc;
 }
 
 extern "C" uint32_t pw_batch_genomes(pw_batch* bt, uint64_t* names_bytes) {

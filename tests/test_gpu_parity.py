@@ -361,3 +361,67 @@ def test_reads_past_query_end(built, tmp_path):
     fa, paf = query_end_case(tmp_path)
     out = same(["-G", "-C", "-r", fa, paf])
     assert out.count(b">") == 4 and b"(X)" in out
+
+
+# ---------------------------------------------------------------- -w (MSA of the last query run)
+def same_w(args, tmp_path, msa_ok=True):
+    """CLI and oracle with `-w`: stdout, stderr, exit code and the MSA file bytes."""
+    mo, mp = tmp_path / "oracle.mfa", tmp_path / "hip.mfa"
+    ro, oo, eo = run([ORACLE, "-w", mo, *args])
+    rp, op, ep = run([CLI, "-w", mp, *args])
+    assert (rp, op, ep) == (ro, oo, eo), (rp, ro, ep[-2000:], eo[-2000:])
+    if msa_ok:
+        assert mp.read_bytes() == mo.read_bytes()
+    return ro, mo.read_bytes()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_w_edge_mix(built, tmp_path, seed):
+    fa, paf = synth_paf(tmp_path, 0, seed=seed)
+    rc, msa = same_w(["-r", fa, paf], tmp_path)
+    assert rc == 0 and msa.count(b">") >= 2
+
+
+def test_w_cfg2_subsample(built, tmp_path):
+    fa, paf = synth_paf(tmp_path, 2, seed=5, scale=0.05)
+    rc, _ = same_w(["-G", "-C", "-r", fa, paf], tmp_path)
+    assert rc == 0
+
+
+@pytest.mark.parametrize("seed,rev", [(7, 0.5), (8, 1.0)])
+def test_w_long_run(built, tmp_path, seed, rev):
+    fa, paf = str(tmp_path / "r.fa"), str(tmp_path / "r.paf")
+    rc, _, err = run([SYNTH, "paf", "--config", 0, "--seed", seed, "--ncds", 2, "--recs", 300, "--rev", rev,
+                      "--fa", fa, "--paf", paf])
+    assert rc == 0, err
+    rc, msa = same_w(["-r", fa, paf], tmp_path)
+    assert rc == 0 and msa.count(b">") > 100
+
+
+def _w_error_paf(tmp_path, kind):
+    fa, paf = query_end_case(tmp_path)
+    rec = {  # a gap at the sequence end: GASeq::setGap refuses it (GapAssem.cpp:212-233)
+        "ref_end_fwd": ["qa", 32, 0, 32, "+", "t5", 100, 10, 43, 30, 33, 60, "cg:Z:32M1D", "cs:Z::32-a"],
+        "ref_start_rev": ["qa", 32, 0, 32, "-", "t6", 100, 10, 43, 30, 33, 60, "cg:Z:1D32M", "cs:Z:-a:32"],
+        "target_end": ["qa", 32, 0, 32, "+", "t7", 100, 10, 40, 30, 32, 60, "cg:Z:30M2I", "cs:Z::30+cg"],
+    }[kind]
+    rec = rec[:12] + ["NM:i:1", "AS:i:9"] + rec[12:]
+    p = tmp_path / f"{kind}.paf"
+    p.write_text(open(paf).read() + "\t".join(map(str, rec)) + "\n")
+    return fa, str(p)
+
+
+@pytest.mark.parametrize("kind", ["ref_end_fwd", "ref_start_rev", "target_end"])
+def test_w_invalid_gap_position(built, tmp_path, kind):
+    fa, paf = _w_error_paf(tmp_path, kind)
+    rc, msa = same_w(["-r", fa, paf], tmp_path)
+    assert rc == 1 and msa == b""
+
+
+def test_w_refused_in_genome_mode_and_bad_path(built, tmp_path):
+    fa, paf = query_end_case(tmp_path)
+    rc, _ = same_w(["-F", "-r", fa, paf], tmp_path, msa_ok=False)
+    assert rc == 1
+    ro, oo, eo = run([ORACLE, "-w", tmp_path / "no" / "x.mfa", "-r", fa, paf])
+    rp, op, ep = run([CLI, "-w", tmp_path / "no" / "x.mfa", "-r", fa, paf])
+    assert (rp, op, ep) == (ro, oo, eo) and ro == 1
