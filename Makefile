@@ -9,7 +9,7 @@ SRC_DIR  := pwasm_amd/csrc
 OBJ_DIR  := pwasm_amd/build
 LIB      := pwasm_amd/lib/libpwasm_amd.so
 CLI      := pwasm_amd/bin/pafreport
-OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o
+OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o $(OBJ_DIR)/pw_ga_api.o
 GA_CLI   := pwasm_amd/bin/gapassem_consensus
 
 all: $(LIB) $(CLI) $(GA_CLI) oracle synth
@@ -20,7 +20,7 @@ $(OBJ_DIR):
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pw_tables.h include/pwasm_amd.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp include/pwasm_amd.h $(SRC_DIR)/pw_msa_layout.h | $(OBJ_DIR)
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp include/pwasm_amd.h include/pwasm_gapassem.hpp $(SRC_DIR)/pw_msa_layout.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
 $(LIB): $(OBJS)

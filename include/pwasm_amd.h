@@ -195,9 +195,40 @@ typedef struct pw_msa_refine_args {
   int32_t* offset_out;        /* [n_rows] GASeq::offset after refineMSA */
   int64_t* numgaps_out;       /* [n_rows] in: GASeq::numgaps; out: after refineMSA */
   uint32_t remove_gaps;
+  uint32_t keep_clip_gaps;    /* 1: stop after the removeColumn edits (offset', ofs', numgaps');
+                                 the caller runs refineClipping / removeClipGaps per row on the
+                                 host (pw_ga_row_finish) */
 } pw_msa_refine_args;
 uint64_t pw_msa_refine_tiles(int32_t n_cols);
 int pw_msa_refine(const pw_msa_args* args, const pw_msa_refine_args* refine, void* stream);
+
+/* Host per-row steps of GSeqAlign::refineMSA after the consensus (the GapAssem C++ API,
+ * pwasm_gapassem.hpp, and the multi-GPU driver call these on the rows they own).
+ * pw_ga_row_remove_columns: removeColumn(alpos) (GapAssem.cpp:755-779 -> GASeq::removeBase
+ *   :122-131) for the non-decreasing layout positions alpos[0..n) of the removed consensus-gap
+ *   columns (the k-th at column c_k: alpos = c_k - k + minoffset), in one pass over the row —
+ *   exact for any gap values, including deleted bases (ofs < 0) where the closed form of
+ *   pw_msa_refine does not apply.
+ * pw_ga_row_finish: refineClipping (X-drop, :182-349), removeClipGaps (:522-549) when
+ *   PW_GA_REMOVE_GAPS, and the second refineClipping(skipDels) when gaps were removed
+ *   (:1163-1181).  cpos_base = minoffset + mincol.  Returns 0, or 1 after a GError the
+ *   reference exits on; msgbuf receives what the reference prints for the row (its warnings,
+ *   then the GError message), NUL-terminated and cut at msglen. */
+typedef struct pw_ga_row {
+  const uint8_t* seq; /* [seqlen] bases as stored */
+  int16_t* ofs;       /* [seqlen] gap before each base (negative = deleted base), edited */
+  int32_t seqlen;
+  int32_t offset;     /* in / out */
+  int32_t numgaps;    /* in / out */
+  int32_t clp5, clp3; /* in / out */
+  int32_t revcompl;
+  const char* id;     /* for messages */
+} pw_ga_row;
+#define PW_GA_REMOVE_GAPS 1u /* MSAColumns::removeConsGaps */
+#define PW_GA_REFINE_CLIP 2u /* MSAColumns::refineClipping */
+int pw_ga_row_remove_columns(pw_ga_row* row, const int32_t* alpos, uint64_t n);
+int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int32_t cpos_base, uint32_t flags,
+                     char* msgbuf, size_t msglen);
 
 /* ---------------------------------------------------------------- host pre-pass + CLI */
 
@@ -222,9 +253,14 @@ int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size
 
 /* GSeqAlign::refineMSA consensus of a packed layout file (PWL1, tests/pwl_format.md) on the HIP
  * path, written as a PWC1 result; flags bit0 = MSAColumns::removeConsGaps, bit1 = disable
- * MSAColumns::refineClipping.  Returns the reference's exit code (0, 1 bad index, 5 zero
- * coverage) or 2 for I/O / device errors. */
+ * MSAColumns::refineClipping.  Returns the reference's exit code (0, 1 bad index / GError, 5 zero
+ * coverage) or 2 for I/O / device errors.  Result rows: {offset, numgaps, clp5, clp3, ofs[]}. */
 int pw_gapassem_run(const char* layout_path, const char* out_path, uint32_t flags);
+/* pw_gapassem_run through the GapAssem C++ API (pwasm_gapassem.hpp), then, for each non-NULL
+ * path, GSeqAlign::writeACE / writeInfo (contig "contig1") and writeMSA (GapAssem.cpp:1200-1367,
+ * 1039-1046).  Clipped rows are refined (refineClipping) unless flags bit1. */
+int pw_gapassem_run_ex(const char* layout_path, const char* out_path, uint32_t flags, const char* ace_path,
+                       const char* info_path, const char* msa_path);
 
 /* The `pafreport` CLI (pafreport.cpp:175-460) on the HIP path; returns the process exit code
  * the reference would produce (it prints exactly what the reference prints). */

@@ -95,7 +95,14 @@ class MsaArgs(ctypes.Structure):
 class MsaRefineArgs(ctypes.Structure):
     _fields_ = [("gap_prefix", ctypes.c_void_p), ("tile_gaps", ctypes.c_void_p), ("cons_out", ctypes.c_void_p),
                 ("cons_len", ctypes.c_void_p), ("row_offset", ctypes.c_void_p), ("ofs_out", ctypes.c_void_p),
-                ("offset_out", ctypes.c_void_p), ("numgaps_out", ctypes.c_void_p), ("remove_gaps", ctypes.c_uint32)]
+                ("offset_out", ctypes.c_void_p), ("numgaps_out", ctypes.c_void_p), ("remove_gaps", ctypes.c_uint32),
+                ("keep_clip_gaps", ctypes.c_uint32)]
+
+
+class GaRow(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_void_p), ("ofs", ctypes.c_void_p), ("seqlen", ctypes.c_int32),
+                ("offset", ctypes.c_int32), ("numgaps", ctypes.c_int32), ("clp5", ctypes.c_int32),
+                ("clp3", ctypes.c_int32), ("revcompl", ctypes.c_int32), ("id", ctypes.c_char_p)]
 
 
 # every function declared in include/pwasm_amd.h (tests check the export table against it)
@@ -109,6 +116,9 @@ _SIGS = {
     "pw_msa_call": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_refine_tiles": (ctypes.c_uint64, [ctypes.c_int32]),
     "pw_msa_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
+    "pw_ga_row_remove_columns": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_uint64]),
+    "pw_ga_row_finish": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
     "pw_pack_cs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),
                                   ctypes.POINTER(ctypes.c_int32)]),
@@ -127,6 +137,8 @@ _SIGS = {
     "pw_batch_write_msa": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p]),
     "pw_version": (ctypes.c_char_p, []),
     "pw_gapassem_run": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]),
+    "pw_gapassem_run_ex": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                          ctypes.c_char_p, ctypes.c_char_p]),
     "pw_batch_from_files_shard": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
                                                     ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
     "pw_items_merge": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32, ctypes.c_char_p,

@@ -39,7 +39,7 @@
 //                      string ('-' -> '*', or gap columns dropped)
 //   K8 row_edit:       ofs' of every base (chunked like K3)
 //   K9 row_finish:     offset', numgaps', then removeClipGaps on ofs' (i <= clipL and
-//                      i >= seqlen - clipR)
+//                      i >= seqlen - clipR) unless keep_clip_gaps (refineClipping first, host)
 #include <hip/hip_runtime.h>
 #include <limits.h>
 #include <stdint.h>
@@ -456,13 +456,13 @@ __global__ __launch_bounds__(64) void row_finish(const pw_msa_args A, pw_msa_ref
   for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
     const int len = A.row_len[r];
     const uint64_t roff = A.row_off[r];
-    const int cl = A.clip_l[r], cr = A.clip_r[r];
+    const int cl = R.keep_clip_gaps ? -1 : A.clip_l[r], cr = R.keep_clip_gaps ? 0 : A.clip_r[r];
     long long dl = 0, dr = 0;
     for (int i = lane; i < len && i <= cl; i += 64) {
       dl += R.ofs_out[roff + i];
       R.ofs_out[roff + i] = 0;
     }
-    const int r0 = (len - cr > cl + 1) ? len - cr : cl + 1;
+    const int r0 = (len - cr > cl + 1) ? len - cr : cl + 1;  // (keep_clip_gaps: r0 = len, nothing)
     for (int i = r0 + lane; i < len; i += 64) {
       dr += R.ofs_out[roff + i];
       R.ofs_out[roff + i] = 0;

@@ -25,6 +25,7 @@
 #include <memory>
 
 #include "pw_tables.h"
+#include "pwasm_gapassem.hpp"
 
 namespace pw {
 namespace {
@@ -134,105 +135,35 @@ bool closed_form_ok(const MsaRun& run) {
 }
 
 // ---------------------------------------------------------------- literal replay (fallback)
-struct LSeq {
-  std::string id, seq;
-  int seqlen = 0, offset = 0;
-  bool revcompl = false;
-  std::vector<short> ofs;
-};
-struct LMsa {
-  std::vector<LSeq*> rows;
-  int length = 0, minoffset = 0;
-};
-int end_offset(const LSeq* s) {
-  int ng = 0;
-  for (short g : s->ofs) ng += g;
-  return s->offset + s->seqlen + ng;
-}
-void inject_gap(LMsa& m, LSeq* seq, int pos, int xgap) {  // GSeqAlign::injectGap :720-753
-  int alpos = seq->offset + pos;
-  for (int i = 0; i <= pos; i++) alpos += seq->ofs[(size_t)i];
-  for (LSeq* s : m.rows) {
-    int spos = 0;
-    if (s == seq) {
-      spos = pos;
-    } else {
-      int salpos = s->offset;
-      if (salpos >= alpos) {
-        s->offset += xgap;
-        continue;
-      }
-      while (spos < s->seqlen) {
-        salpos += 1 + s->ofs[(size_t)spos];
-        if (salpos > alpos) break;
-        spos++;
-      }
-      if (spos >= s->seqlen) continue;
-    }
-    s->ofs[(size_t)spos] = (short)(s->ofs[(size_t)spos] + xgap);
-  }
-  m.length += xgap;
-}
-
+// pafreport's own construction (pafreport.cpp:382-421) through the GapAssem C++ API: the first
+// alignment's GSeqAlign(refseq, taseq) becomes refMSA, every later one is a GSeqAlign(rseq,
+// taseq) merged into it by addAlign (injectGap both ways, addSeq), then writeMSA.
 int replay(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& run) {
-  std::vector<std::unique_ptr<LSeq>> owned;
-  auto mk = [&](const std::string& id, const std::string& seq, int seqlen, int offset) {
-    owned.emplace_back(new LSeq());
-    LSeq* s = owned.back().get();
-    s->id = id;
-    s->seq = seq;
-    s->seqlen = seqlen;
-    s->offset = offset;
-    s->ofs.assign((size_t)(seqlen > 0 ? seqlen : 0), 0);
-    return s;
-  };
-  LSeq* ref = mk(qid, std::string((const char*)q, (size_t)qlen), qlen, 0);
-  LMsa msa;
+  GASeq* refseq = new GASeq(qid, nullptr, (const char*)q, qlen);  // (upper case already: allupper)
+  refseq->setFlag(GA_FLAG_IS_REF);
+  GSeqAlign* refMSA = nullptr;
   std::string tseq;
   for (size_t a = 0; a < run.recs.size(); a++) {
     const MsaRec& r = run.recs[a];
     build_tseq(q, qlen, run, r, tseq);
-    LSeq* ta = mk(run.labels.substr(r.lab_off, r.lab_len), tseq, (int)tseq.size(), r.r_alnstart);
-    ta->revcompl = r.reverse != 0;
-    LSeq* rs = a == 0 ? ref : mk(qid, std::string(), qlen, 0);
+    const std::string label = run.labels.substr(r.lab_off, r.lab_len);
+    GASeq* taseq = new GASeq(label.c_str(), "", tseq.c_str(), (int)tseq.size(), r.r_alnstart);
+    taseq->revcompl = r.reverse != 0;
+    GASeq* rseq = refseq->msa != nullptr ? new GASeq(qid, 0, qlen) : refseq;
     const int32_t* g = &run.gaps[r.gap_off];
-    for (uint32_t k = 0; k < r.n_rg; k++) rs->ofs[(size_t)g[2 * k]] = (short)g[2 * k + 1];
-    for (uint32_t k = 0; k < r.n_tg; k++) ta->ofs[(size_t)g[2 * (r.n_rg + k)]] = (short)g[2 * (r.n_rg + k) + 1];
-    if (a == 0) {
-      msa.rows = {rs, ta};
-      msa.minoffset = std::min(rs->offset, ta->offset);
-      msa.length = std::max(end_offset(rs), end_offset(ta)) - msa.minoffset;
-      continue;
+    for (uint32_t k = 0; k < r.n_rg; k++) rseq->setGap(g[2 * k], (short)g[2 * k + 1]);
+    for (uint32_t k = 0; k < r.n_tg; k++) taseq->setGap(g[2 * (r.n_rg + k)], (short)g[2 * (r.n_rg + k) + 1]);
+    GSeqAlign* newmsa = new GSeqAlign(rseq, taseq);
+    if (rseq == refseq) {
+      refMSA = newmsa;
+    } else {
+      refseq->msa->addAlign(refseq, newmsa, rseq);
+      refMSA = refseq->msa;
+      delete newmsa;  // its rows now belong to refMSA (addAlign cleared its free flag)
     }
-    LMsa om;  // GSeqAlign(rseq, taseq), merged with addAlign(refseq, newmsa, rseq) :645-690
-    om.rows = {rs, ta};
-    om.minoffset = std::min(rs->offset, ta->offset);
-    om.length = std::max(end_offset(rs), end_offset(ta)) - om.minoffset;
-    for (int i = 0; i < qlen; i++) {
-      const int d = ref->ofs[(size_t)i] - rs->ofs[(size_t)i];
-      if (d > 0) inject_gap(om, rs, i, d);
-      else if (d < 0) inject_gap(msa, ref, i, -d);
-    }
-    ta->offset = ref->offset + ta->offset - rs->offset;  // addSeq :694-716
-    msa.rows.push_back(ta);
-    if (ta->offset < msa.minoffset) {
-      msa.length += msa.minoffset - ta->offset;
-      msa.minoffset = ta->offset;
-    }
-    if (end_offset(ta) - msa.minoffset > msa.length) msa.length = end_offset(ta) - msa.minoffset;
   }
-  Printer pr;
-  const uint8_t* cm = comp().c;
-  std::vector<int32_t> o;
-  for (LSeq* s : msa.rows) {
-    std::string seq = s->seq;
-    if (s->revcompl) {  // finalize -> prepSeq -> reverseComplement (GapAssem.cpp:89-101)
-      std::reverse(seq.begin(), seq.end());
-      for (char& c : seq) c = (char)cm[(uint8_t)c];
-    }
-    o.assign(s->ofs.begin(), s->ofs.end());
-    pr.row(f, s->id, seq.data(), s->seqlen, s->offset, o.data());
-  }
+  if (refMSA) refMSA->writeMSA(f);
+  delete refMSA;  // frees refseq and every taseq
   return 0;
 }
 

@@ -14,8 +14,9 @@ is the multi-GPU driver of the same computation, one process per GPU:
                 a single-GPU count;
   pw_msa_call   bestChar of every column (GapAssem.cpp:1048-1069), identical on every rank;
   pw_msa_refine refineMSA's consensus string and, with removeConsGaps, the closed-form
-                removeColumn/removeBase/removeClipGaps edits of the rank's own rows
-                (GapAssem.cpp:1143-1181).
+                removeColumn/removeBase edits of the rank's own rows (GapAssem.cpp:1143-1162);
+  finish_rows   the per-row tail on the host through the C-ABI: removeColumn replayed for rows
+                with deleted bases, refineClipping, removeClipGaps (GapAssem.cpp:1163-1181).
 Rank 0 writes the PWC1 result (edited rows gathered from their owners).  Messages and exit codes
 are the reference's (trimmed-row warnings :1096-1101, bad index GapAssem.h:366-370 -> 1, zero
 coverage :1121-1131 -> 5), in row order, as the single-GPU driver prints them.
@@ -144,6 +145,7 @@ class HipEngine:
         a.scratch, a.counts, a.consensus, a.minmax = (d[k].data_ptr() for k in ("scr", "counts", "cons", "mm"))
         a.n_slots, a.n_rows, a.n_cols = nslots, nr, ncols
         ra = MsaRefineArgs()
+        ra.keep_clip_gaps = 1  # refineClipping / removeClipGaps per row on the host (finish_rows)
         ra.gap_prefix, ra.tile_gaps, ra.cons_out, ra.cons_len = (d[k].data_ptr() for k in ("gp", "tg", "cout", "clen"))
         ra.row_offset, ra.ofs_out, ra.offset_out, ra.numgaps_out = (d[k].data_ptr()
                                                                     for k in ("roffs", "ofso", "offo", "ngo"))
@@ -216,7 +218,50 @@ def _bad_index_col(lay: Layout, r: int, ncols: int):
     return None
 
 
-def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=None):
+def _i32(v: int) -> int:
+    """int32 wrap-around (the reference's int arithmetic)."""
+    return (v + 2 ** 31) % 2 ** 32 - 2 ** 31
+
+
+def finish_rows(lay: Layout, rows, base: dict, alpos, cons: bytes, mincol: int, remove_gaps: bool,
+                refine_clipping: bool):
+    """refineMSA's per-row tail for `rows` on the host (GapAssem.cpp:1163-1181) through the C-ABI:
+    rows holding deleted bases (ofs < 0) get removeColumn replayed from their input gaps
+    (pw_ga_row_remove_columns), every row then refineClipping / removeClipGaps / refineClipping
+    (pw_ga_row_finish).  base = {row: (offset, numgaps, ofs)} after the GPU's removeColumn edits.
+    -> {row: (messages, failed, offset, numgaps, clp5, clp3, ofs)}."""
+    from pwasm_amd import GaRow, lib
+    L = lib()
+    flags = (1 if remove_gaps else 0) | (2 if refine_clipping else 0)
+    al = np.ascontiguousarray(np.asarray(alpos, dtype=np.int32))
+    cons_a = np.frombuffer(cons, dtype=np.uint8) if cons else np.zeros(1, dtype=np.uint8)
+    cpos_base = _i32(lay.minoffset + mincol)
+    msg = ctypes.create_string_buffer(1 << 16)
+    out = {}
+    for r in rows:
+        neg = remove_gaps and int(lay.ofs[r].min(initial=0)) < 0
+        if neg:
+            off, ng, ofs = int(lay.offset[r]), int(lay.numgaps[r]), lay.ofs[r].astype(np.int16).copy()
+        else:
+            off, ng, ofs = base[r]
+            ofs = np.array(ofs, dtype=np.int16)
+        seq = np.ascontiguousarray(lay.seq[r])
+        row = GaRow()
+        row.seq, row.ofs, row.seqlen = seq.ctypes.data, ofs.ctypes.data, int(lay.seqlen[r])
+        row.offset, row.numgaps = off, ng
+        row.clp5, row.clp3, row.revcompl = int(lay.clp5[r]), int(lay.clp3[r]), int(lay.rev[r])
+        rid = b"row%d" % r
+        row.id = rid
+        if neg and L.pw_ga_row_remove_columns(ctypes.byref(row), al.ctypes.data, al.size) != 0:
+            raise RuntimeError("pw_ga_row_remove_columns")
+        rc = L.pw_ga_row_finish(ctypes.byref(row), cons_a.ctypes.data, len(cons), cpos_base, flags, msg, len(msg))
+        if rc < 0:
+            raise RuntimeError(f"pw_ga_row_finish: {rc}")
+        out[r] = (msg.value.decode(), rc == 1, row.offset, row.numgaps, row.clp5, row.clp3, ofs)
+    return out
+
+
+def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=None, refine_clipping: bool = True):
     """refineMSA's consensus with rows sharded over the ranks of `group` (torch.distributed; a
     single process when it is not initialised).  Returns (exit_code, stderr_text, pwc_bytes) on
     rank 0 — the same bytes as the gapassem_consensus CLI — and (exit_code, "", None) elsewhere."""
@@ -231,13 +276,6 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
     ncols = lay.length
     if ncols <= 0 or ncols > INT_MAX:
         return 1, ("MSAColumns op[]: bad index 0 (size=%d)\n" % ncols) if rank == 0 else "", None
-    neg = any(int(lay.ofs[r].min(initial=0)) < 0 for r in range(lo, hi)) if remove_gaps else False
-    if world > 1 and remove_gaps:
-        flag = [None] * world
-        dist.all_gather_object(flag, neg, group=group)
-        neg = any(flag)
-    if neg:
-        return 2, "removeConsGaps with negative gap values is not supported on the HIP path\n" if rank == 0 else "", None
     engine = engine or HipEngine()
     st = engine.stage(lay, range(lo, hi), ncols)
     counts, mm = engine.count(st)
@@ -263,7 +301,7 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
             col = next(c for c in cols if c is not None)
         err.append("MSAColumns op[]: bad index %d (size=%d)\n" % (col, ncols))
         return 1, "".join(err) if rank == 0 else "", None
-    _, mm = engine.call(st)
+    cons_cols, mm = engine.call(st)
     zero = int(mm[3].item())
     mincol, maxcol = mm_h[0], max(mm_h[1], 0)
     if zero != INT_MAX:
@@ -271,26 +309,40 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
                    % (zero, mincol, hdr.n))
         err.extend("row%u\n" % r for r in range(hdr.n))
         return 5, "".join(err) if rank == 0 else "", None
-    cons_s, own, n_removed = b"", {}, 0
+    own = range(lo, hi)
+    cons_s, base, alpos = b"", {r: (int(lay.offset[r]), int(lay.numgaps[r]), lay.ofs[r]) for r in own}, []
     if mincol != INT_MAX:
-        cons_s, own = engine.refine_host(st, remove_gaps)
-        if remove_gaps:
-            n_removed = (maxcol - mincol + 1) - len(cons_s)
-    if world > 1 and remove_gaps:
+        cons_s, edited = engine.refine_host(st, remove_gaps)
+        base.update(edited)
+        if remove_gaps:  # layout positions of the removed columns, in removal order
+            cc = cons_cols.cpu().numpy() if hasattr(cons_cols, "cpu") else np.asarray(cons_cols)
+            gaps = np.flatnonzero(cc[mincol:maxcol + 1] == ord("-")) + mincol
+            alpos = (gaps - np.arange(gaps.size) + lay.minoffset).astype(np.int32)
+    n_removed = len(alpos)
+    # rows that change: all of them with removeConsGaps (removeClipGaps always moves ofs[0]),
+    # else the clipped ones refineClipping may move
+    fin = finish_rows(lay, [r for r in own if remove_gaps or (refine_clipping and (lay.clp5[r] or lay.clp3[r]))],
+                      base, alpos, cons_s, mincol, remove_gaps, refine_clipping)
+    if world > 1:
         parts = [None] * world
-        dist.all_gather_object(parts, own, group=group)
-        own = {k: v for p in parts for k, v in p.items()}
+        dist.all_gather_object(parts, fin, group=group)
+        fin = {k: v for p in parts for k, v in p.items()}
     if rank != 0:
-        return 0, "", None
-    full = lay if (remove_gaps and own) or world == 1 else Layout(layout_path)
+        return (1 if any(v[1] for v in fin.values()) else 0), "", None
+    for r in range(hdr.n):  # the per-row messages in row order, up to a row that GErrors
+        if r in fin:
+            err.append(fin[r][0])
+            if fin[r][1]:
+                return 1, "".join(err), None
+    full = lay if world == 1 else Layout(layout_path, load=set(r for r in range(hdr.n) if r not in fin))
     counts_h = counts.cpu().numpy().astype("<i4")
     out = [b"PWC1", struct.pack("<6i", ncols, lay.minoffset, -1 if mincol == INT_MAX else mincol, maxcol, len(cons_s),
                                 n_removed), cons_s, counts_h.tobytes(), struct.pack("<I", hdr.n)]
     for r in range(hdr.n):
-        if remove_gaps and r in own:
-            off, ng, ofs = own[r]
+        if r in fin:
+            _, _, off, ng, c5, c3, ofs = fin[r]
         else:
-            off, ng, ofs = int(lay.offset[r]), int(lay.numgaps[r]), full.ofs[r]
-        out.append(struct.pack("<2i", off, ng))
+            off, ng, c5, c3, ofs = int(lay.offset[r]), int(lay.numgaps[r]), int(lay.clp5[r]), int(lay.clp3[r]), full.ofs[r]
+        out.append(struct.pack("<4i", off, ng, c5, c3))
         out.append(np.asarray(ofs, dtype="<i2").tobytes())
     return 0, "".join(err), b"".join(out)

@@ -99,6 +99,7 @@ typedef struct {
   /* layout knobs */
   int rows, ref_len, row_min, row_max;
   double ref_gap, row_gap, n_frac;
+  double clip_frac, del_frac; /* layout: rows with clipped ends; deleted bases (ofs -1) */
 } opts_t;
 
 static void set_config(opts_t* o) {
@@ -504,7 +505,9 @@ static int cmd_paf(opts_t* o) {
 /* ---- GapAssem layout (PWL1, tests/pwl_format.md): row 0 = the reference with insertion
  * blocks (ref_gap per position, 1-5 columns); rows 1.. cover U[row_min,row_max] reference
  * positions, fill part of some insertion blocks with their own bases, delete ~row_gap of their
- * reference bases (a gap column in that row) and carry ~n_frac N bases + 1% mismatches. */
+ * reference bases (a gap column in that row) and carry ~n_frac N bases + 1% mismatches.
+ * --clip P: a row gets clp5 / clp3 in [0, len/8] with probability P; --dels P: a base gets
+ * ofs -1 (deleted) with probability P. */
 static int cmd_layout(opts_t* o) {
   int rows = o->rows;
   int L = (int)llround(o->ref_len * o->scale);
@@ -568,7 +571,15 @@ static int cmd_layout(opts_t* o) {
       ofs[n++] = (short)pending;
       pending = 0;
     }
-    int32_t h[5] = {(int32_t)colof[start], n, 0, 0, (r % 3 == 1) ? 1 : 0};
+    int32_t c5 = 0, c3 = 0;
+    if (r > 0 && o->clip_frac > 0 && rndu() < o->clip_frac) { /* (no draws when the option is off) */
+      c5 = rndi(0, n / 8);
+      c3 = rndi(0, n / 8);
+    }
+    if (r > 0 && o->del_frac > 0)
+      for (int i = 1; i + 1 < n; i++)
+        if (ofs[i] == 0 && rndu() < o->del_frac) ofs[i] = -1;
+    int32_t h[5] = {(int32_t)colof[start], n, c5, c3, (r % 3 == 1) ? 1 : 0};
     fwrite(h, sizeof h, 1, f);
     fwrite(seq, 1, (size_t)n, f);
     fwrite(ofs, sizeof(short), (size_t)n, f);
@@ -627,6 +638,8 @@ int main(int argc, char** argv) {
     else if (!strcmp(k, "--ref-len")) o.ref_len = atoi(v);
     else if (!strcmp(k, "--row-min")) o.row_min = atoi(v);
     else if (!strcmp(k, "--row-max")) o.row_max = atoi(v);
+    else if (!strcmp(k, "--clip")) o.clip_frac = atof(v);
+    else if (!strcmp(k, "--dels")) o.del_frac = atof(v);
     else if (!strcmp(k, "--threads")) o.threads = atoi(v);
     else if (!strcmp(k, "--shard")) {
       if (sscanf(v, "%d/%d", &o.shard, &o.nshards) != 2 || o.nshards < 1 || o.shard < 0 || o.shard >= o.nshards) {

@@ -25,16 +25,29 @@ def read_rows(pwc_raw, lens):
     p += 4
     out = []
     for r in range(n):
-        off, ng = struct.unpack_from("<2i", pwc_raw, p)
-        p += 8
+        off, ng, _c5, _c3 = struct.unpack_from("<4i", pwc_raw, p)
+        p += 16
         ofs = list(struct.unpack_from(f"<{lens[r]}h", pwc_raw, p))
         p += 2 * lens[r]
         out.append((off, ng, ofs))
     return out
 
 
-def model(rows, res):
-    """Closed-form refineMSA row edits from the oracle's consensus columns."""
+def read_clips(pwc_raw, lens):
+    """(clp5, clp3) of every row of a PWC1 result."""
+    p = 4 + 24
+    length, _, _, _, clen, _ = struct.unpack_from("<6i", pwc_raw, 4)
+    p += clen + 24 * length + 4
+    out = []
+    for n in lens:
+        out.append(struct.unpack_from("<2i", pwc_raw, p + 8))
+        p += 16 + 2 * n
+    return out
+
+
+def model(rows, res, clip_gaps=True):
+    """Closed-form refineMSA row edits from the oracle's consensus columns (clip_gaps=False: stop
+    before removeClipGaps, as pw_msa_refine with keep_clip_gaps)."""
     minoff = res["minoff"]
     lo, hi = res["mincol"], res["maxcol"]
     cons_gap = set()
@@ -71,6 +84,9 @@ def model(rows, res):
             new.append(x - dec)
             numgaps -= dec
         cl, cr = (clp3, clp5) if rev else (clp5, clp3)
+        if not clip_gaps:
+            out.append((new_off, numgaps, new))
+            continue
         dl = dr = 0
         for i in range(len(new)):
             if i <= cl:
@@ -83,14 +99,15 @@ def model(rows, res):
     return out
 
 
-def random_layout(rng, nrows, clip):
+def random_layout(rng, nrows, clip, dels=False):
+    """Random rows (offset, seq, ofs, clp5, clp3, rev); dels: some deleted bases (ofs -1)."""
     rows = []
     for r in range(nrows):
         n = rng.randint(5, 40)
         seq = "".join(rng.choice("ACGTACGTN-") for _ in range(n))
-        ofs = [rng.choice([0, 0, 0, 0, 1, 2, 3]) for _ in range(n)]
-        c5 = rng.randint(0, 3) if clip else 0
-        c3 = rng.randint(0, 3) if clip else 0
+        ofs = [rng.choice([0, 0, 0, 0, 1, 2, 3] + ([-1] if dels else [])) for _ in range(n)]
+        c5 = rng.randint(0, 6) if clip else 0
+        c3 = rng.randint(0, 6) if clip else 0
         rows.append((rng.randint(0, 25), seq, ofs, c5, c3, r % 2))
     return rows
 

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from conftest import GA_ORACLE, SYNTH, run
-from test_gapassem_refine import model, random_layout
+from test_gapassem_refine import model, random_layout, read_clips
 from test_oracle_kat import write_pwl
 
 INT_MAX = 2 ** 31 - 1
@@ -83,7 +83,7 @@ class ModelEngine:
             res = dict(minoff=lay.minoffset, mincol=lo, maxcol=hi, length=st["ncols"], counts=counts)
             mine = [(int(lay.offset[r]), bytes(lay.seq[r]).decode(), lay.ofs[r].tolist(), int(lay.clp5[r]),
                      int(lay.clp3[r]), int(lay.rev[r])) for r in st["rows"]]
-            for r, (off, ng, ofs) in zip(st["rows"], model(mine, res)):
+            for r, (off, ng, ofs) in zip(st["rows"], model(mine, res, clip_gaps=False)):
                 rows[r] = (off, ng, np.array(ofs, dtype=np.int16))
         return s, rows
 
@@ -96,13 +96,13 @@ def _free_port():
     return port
 
 
-def _rank(rank, world, port, lay, remove, q):
+def _rank(rank, world, port, lay, remove, q, refine=True):
     import torch.distributed as dist
     from pwasm_amd import gapassem
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = gapassem.consensus(lay, remove_gaps=remove, engine=ModelEngine())
+        res = gapassem.consensus(lay, remove_gaps=remove, engine=ModelEngine(), refine_clipping=refine)
         if rank == 0:
             q.put(res)
         dist.barrier()
@@ -110,12 +110,12 @@ def _rank(rank, world, port, lay, remove, q):
         dist.destroy_process_group()
 
 
-def _sharded(lay, world, remove):
+def _sharded(lay, world, remove, refine=True):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, str(lay), remove, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, str(lay), remove, q, refine)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -125,21 +125,32 @@ def _sharded(lay, world, remove):
     return res
 
 
-def _oracle(lay, tmp_path, remove):
-    extra = ["--no-refine-clipping"] + (["--remove-gaps"] if remove else [])
+def _oracle(lay, tmp_path, remove, refine=True):
+    extra = ([] if refine else ["--no-refine-clipping"]) + (["--remove-gaps"] if remove else [])
     rc, _, err = run([GA_ORACLE, lay, tmp_path / "o.pwc", *extra])
     return rc, err.decode(), (open(tmp_path / "o.pwc", "rb").read() if rc == 0 else None)
 
 
-def test_single_process_model_equals_oracle(built, tmp_path):
+@pytest.mark.parametrize("refine", [False, True])
+def test_single_process_model_equals_oracle(built, tmp_path, refine):
+    """The driver's host per-row tail (pw_ga_row_finish / pw_ga_row_remove_columns through the
+    C-ABI: refineClipping X-drop, removeClipGaps, removeColumn replay for deleted bases) on top of
+    the model engine, against the oracle's literal refineMSA."""
     from pwasm_amd import gapassem
-    for seed in range(6):
-        rows = random_layout(random.Random(900 + seed), 9, clip=seed % 2 == 1)
+    n_clip_moves = 0
+    for seed in range(10):
+        rng = random.Random(900 + seed)
+        rows = random_layout(rng, 9, clip=seed % 2 == 1, dels=seed >= 6)
         lay = tmp_path / f"l{seed}.pwl"
         write_pwl(lay, rows)
         for remove in (False, True):
-            assert gapassem.consensus(str(lay), remove_gaps=remove, engine=ModelEngine()) == \
-                _oracle(lay, tmp_path, remove)
+            want = _oracle(lay, tmp_path, remove, refine)
+            assert gapassem.consensus(str(lay), remove_gaps=remove, engine=ModelEngine(), refine_clipping=refine) == want
+            if want[0] == 0 and refine:
+                got = read_clips(want[2], [len(r[1]) for r in rows])
+                n_clip_moves += sum(c != (r[3], r[4]) for c, r in zip(got, rows))
+    if refine:
+        assert n_clip_moves > 0  # refineClipping moved some clip boundary
 
 
 @pytest.mark.parametrize("world,remove", [(2, True), (2, False), (3, True)])

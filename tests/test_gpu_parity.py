@@ -160,13 +160,21 @@ def test_batch_api_on_torch_stream(built, tmp_path):
 
 
 # ---------------------------------------------------------------- GapAssem consensus
-def ga_same(layout, tmp_path, extra=()):
-    ro, _, eo = run([GA_ORACLE, layout, tmp_path / "o.pwc", *extra])
-    rp, _, ep = run([GA_CLI, layout, tmp_path / "p.pwc", *extra])
+def ga_same(layout, tmp_path, extra=(), writers=True):
+    """gapassem_consensus (GapAssem C++ API on the GPU) against the oracle: exit code, stderr, the
+    PWC1 result and — with `writers` — the writeACE / writeInfo / writeMSA outputs."""
+    outs = ["--ace", "--info", "--msa"] if writers else []
+    ro, _, eo = run([GA_ORACLE, layout, tmp_path / "o.pwc", *extra,
+                     *[a for o in outs for a in (o, tmp_path / ("o" + o[1:]))]])
+    rp, _, ep = run([GA_CLI, layout, tmp_path / "p.pwc", *extra,
+                     *[a for o in outs for a in (o, tmp_path / ("p" + o[1:]))]])
     assert rp == ro, (rp, ro, ep, eo)
     assert ep == eo
     if ro == 0:
         assert open(tmp_path / "p.pwc", "rb").read() == open(tmp_path / "o.pwc", "rb").read()
+        for o in outs:
+            a, b = (open(tmp_path / (x + o[1:]), "rb").read() for x in "op")
+            assert a == b, o
     return ro
 
 
@@ -191,7 +199,31 @@ def test_gapassem_clipped_rows(built, tmp_path):
         rows.append((rng.randint(0, 30), seq, ofs, rng.randint(0, 4), rng.randint(0, 4), r % 2))
     lay = tmp_path / "c.pwl"
     write_pwl(lay, rows)
-    ga_same(lay, tmp_path, ["--no-refine-clipping"])
+    for extra in (["--no-refine-clipping"], [], ["--remove-gaps"], ["--remove-gaps", "--no-refine-clipping"]):
+        ga_same(lay, tmp_path, extra)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_gapassem_refine_clipping_random(built, tmp_path, seed):
+    """refineClipping (X-drop, GapAssem.cpp:182-349) + removeClipGaps per row, deleted bases
+    (ofs -1: removeColumn replayed on the host) — library defaults, both removeConsGaps modes."""
+    from test_gapassem_refine import random_layout
+    rng = random.Random(700 + seed)
+    rows = random_layout(rng, rng.randint(3, 25), clip=True, dels=seed % 2 == 1)
+    lay = tmp_path / "r.pwl"
+    write_pwl(lay, rows)
+    ga_same(lay, tmp_path)
+    ga_same(lay, tmp_path, ["--remove-gaps"])
+
+
+@pytest.mark.parametrize("scale,clip,dels", [(0.002, 0.5, 0.0), (0.01, 0.3, 0.002), (0.02, 0.5, 0.001)])
+def test_gapassem_clipped_synthetic(built, tmp_path, scale, clip, dels):
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", scale, "--rows", 40, "--clip", clip, "--dels", dels,
+                      "--out", lay])
+    assert rc == 0, err
+    assert ga_same(lay, tmp_path) == 0
+    assert ga_same(lay, tmp_path, ["--remove-gaps"]) == 0
 
 
 @pytest.mark.parametrize("scale", [0.0005, 0.002, 0.01])
@@ -264,16 +296,18 @@ def test_gapassem_remove_gaps_synthetic(built, tmp_path, scale):
     assert read_pwc(tmp_path / "p.pwc")["removed"] > 0
 
 
-def test_gapassem_remove_gaps_negative_refused(built, tmp_path):
+def test_gapassem_remove_gaps_deleted_bases(built, tmp_path):
+    """Deleted bases (ofs < 0, as GASeq::removeBase leaves them) under removeConsGaps: the raw-ofs
+    walk of removeColumn (GapAssem.cpp:766-771) replayed per row on the host (former D8)."""
     lay = tmp_path / "n.pwl"
-    write_pwl(lay, [(0, "ACGT", [0, -1, 0, 0], 0, 0, 0), (0, "ACGT", [0, 0, 0, 0], 0, 0, 0)])
-    rc, _, err = run([GA_CLI, lay, tmp_path / "p.pwc", "--remove-gaps"])
-    assert rc == 2 and b"negative gap" in err
+    write_pwl(lay, [(0, "ACGT", [0, -1, 0, 0], 0, 0, 0), (0, "ACGT", [0, 0, 0, 0], 0, 0, 0),
+                    (1, "CGTA", [0, 1, -1, 0], 0, 0, 1)])
+    assert ga_same(lay, tmp_path, ["--remove-gaps"]) == 0
 
 
 # ---------------------------------------------------------------- multi-GPU GapAssem driver
-def _ga_cli(lay, tmp_path, remove):
-    extra = ["--remove-gaps"] if remove else []
+def _ga_cli(lay, tmp_path, remove, refine=True):
+    extra = (["--remove-gaps"] if remove else []) + ([] if refine else ["--no-refine-clipping"])
     rc, _, err = run([GA_CLI, lay, tmp_path / "c.pwc", *extra])
     return rc, err.decode(), (open(tmp_path / "c.pwc", "rb").read() if rc == 0 else None)
 
@@ -287,6 +321,15 @@ def test_gapassem_driver_single_rank_on_gpu(built, tmp_path, remove):
     got = gapassem.consensus(str(lay), remove_gaps=remove)
     assert got == _ga_cli(lay, tmp_path, remove)
     assert got[0] == 0
+    # clipped rows + deleted bases: the driver's host row tail (pw_ga_row_*) after the GPU edits
+    lay2 = tmp_path / "c.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.005, "--rows", 30, "--clip", 0.5, "--dels", 0.002,
+                      "--out", lay2])
+    assert rc == 0, err
+    for refine in (True, False):
+        got = gapassem.consensus(str(lay2), remove_gaps=remove, refine_clipping=refine)
+        assert got == _ga_cli(lay2, tmp_path, remove, refine)
+        assert got[0] == 0
 
 
 def _ga_rank(rank, world, port, lay, remove, q):
@@ -370,6 +413,9 @@ def same_w(args, tmp_path, msa_ok=True):
     ro, oo, eo = run([ORACLE, "-w", mo, *args])
     rp, op, ep = run([CLI, "-w", mp, *args])
     assert (rp, op, ep) == (ro, oo, eo), (rp, ro, ep[-2000:], eo[-2000:])
+    assert mp.exists() == mo.exists()
+    if not mo.exists():
+        return ro, None
     if msa_ok:
         assert mp.read_bytes() == mo.read_bytes()
     return ro, mo.read_bytes()
