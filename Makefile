@@ -9,7 +9,7 @@ SRC_DIR  := pwasm_amd/csrc
 OBJ_DIR  := pwasm_amd/build
 LIB      := pwasm_amd/lib/libpwasm_amd.so
 CLI      := pwasm_amd/bin/pafreport
-OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o $(OBJ_DIR)/pw_ga_api.o
+OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o $(OBJ_DIR)/pw_ga_api.o $(OBJ_DIR)/pw_msa_comm.o
 GA_CLI   := pwasm_amd/bin/gapassem_consensus
 
 all: $(LIB) $(CLI) $(GA_CLI) oracle synth
@@ -24,7 +24,7 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp include/pwasm_amd.h include/pwasm_gapassem.hpp 
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS) -ldl
 
 $(CLI): $(SRC_DIR)/pafreport_main.cpp $(LIB)
 	$(HIPCC) -O2 -std=c++17 $(INC) -o $@ $< -Lpwasm_amd/lib -lpwasm_amd -Wl,-rpath,'$$ORIGIN/../lib'

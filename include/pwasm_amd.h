@@ -202,6 +202,24 @@ typedef struct pw_msa_refine_args {
 uint64_t pw_msa_refine_tiles(int32_t n_cols);
 int pw_msa_refine(const pw_msa_args* args, const pw_msa_refine_args* refine, void* stream);
 
+/* ---------------------------------------------------------------- GapAssem over RCCL
+ * One process per GPU; the 128-byte id travels over any side channel (torch.distributed in
+ * pwasm_amd/gapassem.py).  librccl is loaded on first use.
+ * pw_msa_counts_allreduce: after every rank's pw_msa_count on its rows (rows row_base.. of the
+ *   layout), sums counts[n_cols][6] and reduces minmax[0] min / [1] max / [2] min (as a global
+ *   row index) on all ranks in place — one grouped RCCL call set on `stream`; follow with
+ *   pw_msa_call.  The merged histograms are bit-identical to a single-GPU count.
+ * pw_msa_counts_reduce_scatter: rank r receives the summed counts of columns
+ *   [r * cols_per_rank, (r + 1) * cols_per_rank) in counts_part; counts holds nranks *
+ *   cols_per_rank columns (zero past n_cols). */
+#define PW_COMM_ID_BYTES 128
+int pw_comm_unique_id(uint8_t* id);
+int pw_comm_init(void** comm, int nranks, const uint8_t* id, int rank);
+int pw_comm_destroy(void* comm);
+int pw_msa_counts_allreduce(const pw_msa_args* args, uint32_t row_base, void* comm, void* stream);
+int pw_msa_counts_reduce_scatter(const int32_t* counts, int32_t* counts_part, uint64_t cols_per_rank, void* comm,
+                                 void* stream);
+
 /* Host per-row steps of GSeqAlign::refineMSA after the consensus (the GapAssem C++ API,
  * pwasm_gapassem.hpp, and the multi-GPU driver call these on the rows they own).
  * pw_ga_row_remove_columns: removeColumn(alpos) (GapAssem.cpp:755-779 -> GASeq::removeBase

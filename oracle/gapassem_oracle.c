@@ -345,7 +345,7 @@ static void write_info(FILE* f, const char* name, row_t* rows, uint32_t n, const
         indel_ofs = 0;
       }
     }
-    pid = (pid * 100.0f) / (float)aligned_len;
+    pid = aligned_len ? (pid * 100.0f) / (float)aligned_len : -__builtin_nanf(""); /* x86 0/0: "-nan" */
     int seql = clpl + 1, seqr = s->seqlen - clpr;
     if (seqr < seql) {
       fprintf(stderr, "WARNING: Bad trimming for %s of gapped len %d (%d, %d)\n", s->id, gapped_len, seql, seqr);

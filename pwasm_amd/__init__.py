@@ -116,6 +116,13 @@ _SIGS = {
     "pw_msa_call": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_refine_tiles": (ctypes.c_uint64, [ctypes.c_int32]),
     "pw_msa_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
+    "pw_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "pw_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
+    "pw_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "pw_msa_counts_allreduce": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_uint32, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
+    "pw_msa_counts_reduce_scatter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
     "pw_ga_row_remove_columns": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_uint64]),
     "pw_ga_row_finish": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),

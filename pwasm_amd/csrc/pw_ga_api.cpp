@@ -1177,7 +1177,9 @@ void GSeqAlign::writeInfo(FILE* f, const char* name) {  // GapAssem.cpp:1264-136
         indel_ofs = 0;
       }
     }
-    pid = (pid * 100.0f) / (float)aligned_len;
+    // 0/0 when no base is aligned: x86's default NaN (sign set, printed "-nan"), as the reference's
+    // division produces it there, whatever this compiler folds the expression into
+    pid = aligned_len ? (pid * 100.0f) / (float)aligned_len : -__builtin_nanf("");
     int seql = clpl + 1, seqr = s->len - clpr;
     if (seqr < seql) {
       fprintf(stderr, "WARNING: Bad trimming for %s of gapped len %d (%d, %d)\n", s->id.c_str(), gapped_len, seql,

@@ -8,8 +8,10 @@ is the multi-GPU driver of the same computation, one process per GPU:
                 694-716) and stages ITS rows (a contiguous, base-balanced block) in HBM;
   pw_msa_count  buildMSA's toMSA/addNuc/addGap scatter of those rows -> partial [n_cols x 6]
                 int32 histograms + mincol/maxcol (GapAssem.cpp:551-591, 1088-1106);
-  collectives   one all-reduce(SUM) of the histograms and one all-reduce(MIN) of
-                (mincol, -maxcol, first bad row) — RCCL over xGMI with the "nccl" backend.
+  collectives   one all-reduce(SUM) of the histograms and MIN/MAX reductions of (mincol,
+                maxcol, first bad row): with the "nccl" backend the C-ABI's
+                pw_msa_counts_allreduce on an RCCL communicator of its own (rccl_comm), grouped
+                on the rank's stream; torch.distributed all-reduces otherwise (gloo rehearsals).
                 Integer sums are order-independent: the merged histograms are bit-identical to
                 a single-GPU count;
   pw_msa_call   bestChar of every column (GapAssem.cpp:1048-1069), identical on every rank;
@@ -27,6 +29,7 @@ gloo without a GPU."""
 from __future__ import annotations
 
 import ctypes
+import os
 import struct
 
 import numpy as np
@@ -161,6 +164,13 @@ class HipEngine:
         self._rc("pw_msa_count", self.lib.pw_msa_count(ctypes.byref(st["args"]), self.stream.cuda_stream))
         return st["d"]["counts"], st["d"]["mm"]
 
+    def merge(self, st, row_base: int, comm):
+        """pw_msa_counts_allreduce over an RCCL communicator (rccl_comm): histograms summed,
+        bounds reduced, the bad row made global — in place on every rank."""
+        self._rc("pw_msa_counts_allreduce", self.lib.pw_msa_counts_allreduce(ctypes.byref(st["args"]), row_base, comm,
+                                                                             self.stream.cuda_stream))
+        return st["d"]["counts"], st["d"]["mm"]
+
     def call(self, st):
         """bestChar per column + first zero-coverage column (minmax[3]) from the merged counts."""
         self._rc("pw_msa_call", self.lib.pw_msa_call(ctypes.byref(st["args"]), self.stream.cuda_stream))
@@ -188,6 +198,31 @@ class HipEngine:
                 o = int(st["row_off"][k])
                 rows[r] = (int(offo[k]), int(ngo[k]), ofso[o:o + int(st["lens"][k])].copy())
         return cons, rows
+
+
+_COMMS = {}
+
+
+def rccl_comm(group=None):
+    """An RCCL communicator over the ranks of `group` for the C-ABI collectives (one per group,
+    kept for the process): rank 0 draws the id, torch.distributed broadcasts it."""
+    import torch.distributed as dist
+    from pwasm_amd import lib
+    key = id(group)
+    if key in _COMMS:
+        return _COMMS[key]
+    L = lib()
+    buf = ctypes.create_string_buffer(128)
+    if dist.get_rank(group) == 0 and L.pw_comm_unique_id(buf) != 0:
+        raise RuntimeError("pw_comm_unique_id")
+    obj = [buf.raw]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    buf = ctypes.create_string_buffer(obj[0], 128)
+    comm = ctypes.c_void_p()
+    if L.pw_comm_init(ctypes.byref(comm), dist.get_world_size(group), buf, dist.get_rank(group)) != 0:
+        raise RuntimeError("pw_comm_init")
+    _COMMS[key] = comm
+    return comm
 
 
 def all_reduce(t, op, group=None):
@@ -280,8 +315,17 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
     st = engine.stage(lay, range(lo, hi), ncols)
     counts, mm = engine.count(st)
     mm_h = [int(x) for x in mm.cpu().tolist()]
-    bad = lo + mm_h[2] if mm_h[2] != INT_MAX else INT_MAX
-    if world > 1:
+    mode = os.environ.get("PW_GA_COMM", "auto")  # auto | rccl (also at world 1) | torch
+    use_rccl = (dist_on and isinstance(engine, HipEngine) and dist.get_backend(group) == "nccl"
+                and (mode == "rccl" or (mode == "auto" and world > 1)))
+    if use_rccl:  # the C-ABI collective (pw_msa_counts_allreduce) on this rank's stream
+        counts, mm = engine.merge(st, lo, rccl_comm(group))
+        mm_h = [int(x) for x in mm.cpu().tolist()]
+        bad = mm_h[2]
+        mm_h[2] = INT_MAX
+    else:
+        bad = lo + mm_h[2] if mm_h[2] != INT_MAX else INT_MAX
+    if world > 1 and not use_rccl:
         red = torch.tensor([mm_h[0], -mm_h[1], bad], dtype=torch.int64, device=counts.device)
         all_reduce(counts, dist.ReduceOp.SUM, group)
         all_reduce(red, dist.ReduceOp.MIN, group)

@@ -300,9 +300,12 @@ def test_gapassem_remove_gaps_deleted_bases(built, tmp_path):
     """Deleted bases (ofs < 0, as GASeq::removeBase leaves them) under removeConsGaps: the raw-ofs
     walk of removeColumn (GapAssem.cpp:766-771) replayed per row on the host (former D8)."""
     lay = tmp_path / "n.pwl"
-    write_pwl(lay, [(0, "ACGT", [0, -1, 0, 0], 0, 0, 0), (0, "ACGT", [0, 0, 0, 0], 0, 0, 0),
-                    (1, "CGTA", [0, 1, -1, 0], 0, 0, 1)])
+    # (toMSA still places a deleted base in a column: rows holding one end before the longest row)
+    write_pwl(lay, [(0, "ACGT", [0, -1, 0, 0], 0, 0, 0), (0, "ACGTAC", [0] * 6, 0, 0, 0),
+                    (1, "CGTA", [0, 1, -1, 0], 0, 0, 1), (0, "AGGTAC", [0, 0, 2, 0, 0, 0], 0, 1, 0),
+                    (0, "ACGTAC", [0, 0, 1, 0, 0, 0], 0, 0, 0)])
     assert ga_same(lay, tmp_path, ["--remove-gaps"]) == 0
+    assert read_pwc(tmp_path / "p.pwc")["removed"] > 0
 
 
 # ---------------------------------------------------------------- multi-GPU GapAssem driver
@@ -471,3 +474,70 @@ def test_w_refused_in_genome_mode_and_bad_path(built, tmp_path):
     ro, oo, eo = run([ORACLE, "-w", tmp_path / "no" / "x.mfa", "-r", fa, paf])
     rp, op, ep = run([CLI, "-w", tmp_path / "no" / "x.mfa", "-r", fa, paf])
     assert (rp, op, ep) == (ro, oo, eo) and ro == 1
+
+
+# ---------------------------------------------------------------- RCCL collectives C-ABI
+def test_msa_counts_allreduce_world1(built, tmp_path):
+    """pw_comm_* + pw_msa_counts_allreduce / reduce_scatter on a one-rank RCCL communicator:
+    the merged histograms equal the shard's own, the bad row comes back global (row_base)."""
+    import ctypes
+    import torch
+    from pwasm_amd import gapassem, lib
+    L = lib()
+    lay_p = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.003, "--rows", 12, "--out", lay_p])
+    assert rc == 0, err
+    lay = gapassem.Layout(str(lay_p))
+    eng = gapassem.HipEngine("cuda:0")
+    st = eng.stage(lay, range(lay.n), lay.length)
+    counts, mm = eng.count(st)
+    ref_counts, ref_mm = counts.clone(), mm.clone()
+    uid = ctypes.create_string_buffer(128)
+    assert L.pw_comm_unique_id(uid) == 0
+    comm = ctypes.c_void_p()
+    assert L.pw_comm_init(ctypes.byref(comm), 1, uid, 0) == 0
+    try:
+        counts, mm = eng.merge(st, 5, comm)
+        torch.cuda.synchronize()
+        assert torch.equal(counts, ref_counts)
+        assert mm[:2].tolist() == ref_mm[:2].tolist() and int(mm[2]) == int(ref_mm[2])  # INT_MAX stays
+        part = torch.empty_like(counts)
+        assert L.pw_msa_counts_reduce_scatter(counts.data_ptr(), part.data_ptr(), lay.length, comm,
+                                              torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(part, ref_counts)
+    finally:
+        assert L.pw_comm_destroy(comm) == 0
+
+
+def _ga_rank_nccl(lay, q):
+    import torch.distributed as dist
+    from pwasm_amd import gapassem
+    os.environ.update(MASTER_ADDR="127.0.0.1", PW_GA_COMM="rccl")
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        q.put(gapassem.consensus(lay, remove_gaps=True))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gapassem_driver_rccl_world1(built, tmp_path):
+    """The driver with the nccl backend merges through pw_msa_counts_allreduce on its own RCCL
+    communicator (PW_GA_COMM=rccl forces that path at world 1): same bytes as the CLI."""
+    import socket
+    import torch.multiprocessing as mp
+    lay = tmp_path / "s.pwl"
+    rc, _, err = run([SYNTH, "layout", "--config", 5, "--scale", 0.003, "--rows", 12, "--out", lay])
+    assert rc == 0, err
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_ga_rank_nccl, args=(str(lay), q))
+    p.start()
+    res = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert res == _ga_cli(lay, tmp_path, True)
