@@ -116,6 +116,12 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Global-address-space views (loads through them are global_load, not flat: a flat load also
+// counts on lgkmcnt, so the next LDS wait would wait for it too)
+#define PW_GLOBAL __attribute__((address_space(1)))
+typedef const PW_GLOBAL uint8_t* GU8;
+typedef PW_GLOBAL const v4u GV4;
+
 // ------------------------------------------------------------------ record context
 struct Rec {
   const uint32_t* ops;      // this record's ops (global)
@@ -389,7 +395,7 @@ struct ClampSink {
 };
 typedef ClampSink LineSink;
 struct GlobalSink {
-  uint8_t* p;
+  PW_GLOBAL uint8_t* p;
   int pos;
   __device__ __forceinline__ void put(uint8_t c) { p[pos++] = c; }
   __device__ __forceinline__ void put_if(bool pred, uint8_t c) {
@@ -1332,22 +1338,37 @@ __device__ __noinline__ uint32_t rec_of_slot(const pw_report_args& A, uint64_t s
   return lo;
 }
 
-__device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
+// Prefetched registers are first touched where they are consumed, one or two chunks later: an
+// empty asm that "rewrites" them there keeps the compiler from folding any use into the block
+// that issued the load.  Every prefetch load is unconditional (a clamped or dummy address when
+// the value is not needed): a load inside a branch costs an s_waitcnt vmcnt(0) at the join,
+// since the count of loads issued after it differs between the paths.
+__device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
+struct HotRaw {
+  v4u a, b;
+};
+__device__ __forceinline__ HotRaw load_hot(const Work& W, uint64_t c, int lane) {
+  const uint64_t cc = c < W.n_chunks ? c : W.n_chunks - 1;  // (W.n_chunks >= 1 when render runs)
+  const v4u* p = reinterpret_cast<const v4u*>(W.hot + cc * kWave + lane);
+  HotRaw r;
+  r.a = p[0];
+  r.b = p[1];
+  return r;
+}
+__device__ __forceinline__ Hot decode_hot(HotRaw r, bool valid) {
+  pin(r.a);
+  pin(r.b);
   Hot h;
-  if (c < W.n_chunks) {
-    const v4u* p = reinterpret_cast<const v4u*>(W.hot + c * kWave + lane);
-    const v4u a = p[0], b = p[1];
-    h.qb = a.x;
-    h.L = (int32_t)a.y;
-    h.qp = (int32_t)a.z;
-    h.tloc = (int32_t)a.w;
-    h.ls = b.x;
-    h.fn = b.y;
-    h.l0 = b.z;
-    h.l1 = b.w;
-  } else {
-    h.fn = kNoEv;
-  }
+  h.qb = r.a.x;
+  h.L = (int32_t)r.a.y;
+  h.qp = (int32_t)r.a.z;
+  h.tloc = (int32_t)r.a.w;
+  h.ls = r.b.x;
+  h.fn = valid ? r.b.y : kNoEv;
+  h.l0 = r.b.z;
+  h.l1 = r.b.w;
   return h;
 }
 
@@ -1357,30 +1378,27 @@ __device__ __forceinline__ Hot load_hot(const Work& W, uint64_t c, int lane) {
 // of c + NW was loaded one chunk earlier), so the latency hides behind a whole output phase.
 struct RenderPre {
   v4u q[kQWin / 16];  // 48 forward-query bytes from the 16-byte aligned qlo
-  v4u t0, t1;         // tx record (pre-rendered target context)
+  v4u t0, t1;         // tx record (pre-rendered target context; garbage unless the slot has one)
+  uint32_t ai;        // record of a first / last line (garbage otherwise)
+  uint32_t ns_raw;    // next-stop entry (used when ns_ok)
   int qlo;            // forward position of q[0]
   int n;              // evtbases length (resolved when the Hot field saturates)
-  int ns;             // next-stop entry the indel scan ends on (kNsNone: not needed)
-  uint32_t ai;        // record of a first / last line
+  bool ns_ok;
 };
 __device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& W, const Hot& h, uint64_t s, bool skip,
                                            RenderPre& p) {
-  p.ns = kNsNone;
-  p.ai = 0;
-  p.n = 0;
-  p.qlo = 0;
-  if (h.fn == kNoEv) return;
+  const bool ev = h.fn != kNoEv;
   const uint32_t typ = h.fn >> 30;
   const bool rev = (h.fn >> 29) & 1u;
   int n = (int)(h.fn & kNBig);
-  if (!((h.fn >> 28) & 1u)) {
-    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+  const uint64_t se = ev ? s : 0;  // (empty slots read slot 0's records: valid memory, unused)
+  {
+    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * se);
     p.t0 = tp4[0];
     p.t1 = tp4[1];
   }
-  if (h.fn & (3u << 26)) p.ai = W.cold[s].ai;
-  const uint8_t* R = A.qseq + ((uint64_t)h.qb << 4);
-  if ((uint32_t)n == kNBig) {  // saturated length: from the op stream (rare; dependent loads)
+  p.ai = W.cold[se].ai;
+  if (ev && (uint32_t)n == kNBig) {  // saturated length: from the op stream (rare; dependent loads)
     const Cold cd = W.cold[s];
     const pw_aln_desc d = A.desc[cd.ai];
     Rec r;
@@ -1394,20 +1412,34 @@ __device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& 
   p.n = n;
   // 48 forward-query bytes from 8 before the event (16-byte aligned; covers [rloc - 8, rloc + 25],
   // the reads of all but long deletions)
-  const int rl = event_rloc(h.L, rev, typ, h.qp, n);
+  const uint8_t* R = ev ? A.qseq + ((uint64_t)h.qb << 4) : A.qseq;
+  const int rl = ev ? event_rloc(h.L, rev, typ, h.qp, n) : 0;
   int x0 = rl - 8;
   if (x0 < 0) x0 = 0;
-  const uintptr_t a0 = (uintptr_t)(R + x0) & ~(uintptr_t)15;  // >= qseq (16-byte aligned)
+  // (R is 16-byte aligned: qseq is, and queries start at 16-byte multiples.  Pointer arithmetic,
+  // not an integer round trip, keeps the loads global_load: flat loads would also count on
+  // lgkmcnt and make every LDS wait of the output phase wait for them.)
+  const int x0a = x0 & ~15;
+  const v4u* a0 = reinterpret_cast<const v4u*>(R + x0a);
 #pragma unroll
-  for (int q = 0; q < kQWin / 16; q++) p.q[q] = *reinterpret_cast<const v4u*>(a0 + 16 * q);
-  p.qlo = (int)((intptr_t)a0 - (intptr_t)R);
-  if (typ != PW_OP_SUB && A.next_stop && !skip) {
-    const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
-    const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
-    const int k0 = rl + dl + (15 - a - x);
-    if (a + x <= 15 && (h.L - rt) + x - dl > 17 && k0 >= 0 && k0 < h.L)
-      p.ns = A.next_stop[((uint64_t)h.qb << 4) + (uint64_t)k0];
-  }
+  for (int q = 0; q < kQWin / 16; q++) p.q[q] = a0[q];
+  p.qlo = x0a;
+  const int aap0 = rl / 3, rt = aap0 > 0 ? 3 * (aap0 - 1) : 0, a = rl - rt;
+  const int x = typ == PW_OP_INS ? n : 0, dl = typ == PW_OP_DEL ? n : 0;
+  const int k0 = rl + dl + (15 - a - x);
+  p.ns_ok = ev && typ != PW_OP_SUB && A.next_stop && !skip && a + x <= 15 && (h.L - rt) + x - dl > 17 && k0 >= 0 &&
+            k0 < h.L;
+  const int32_t* nsp = p.ns_ok ? A.next_stop + ((uint64_t)h.qb << 4) + (uint64_t)k0 : (const int32_t*)A.qseq;
+  p.ns_raw = (uint32_t)*nsp;
+}
+// the prefetched registers, first touched here
+__device__ __forceinline__ void render_pre_ready(RenderPre& p) {
+#pragma unroll
+  for (int q = 0; q < kQWin / 16; q++) pin(p.q[q]);
+  pin(p.t0);
+  pin(p.t1);
+  pin(p.ai);
+  pin(p.ns_raw);
 }
 
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
@@ -1428,13 +1460,15 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
   const uint64_t nw = (uint64_t)gridDim.x * kWaves;
 
   uint64_t c = (uint64_t)blockIdx.x * kWaves + wv;
-  Hot h = load_hot(W, c, lane);
-  Hot hn = load_hot(W, c + nw, lane);
+  if (c >= W.n_chunks) return;
+  Hot h = decode_hot(load_hot(W, c, lane), true);
+  HotRaw hn = load_hot(W, c + nw, lane);
   RenderPre pre;
   render_pre(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
   for (; c < W.n_chunks; c += nw) {
     const uint64_t s = c * kWave + (uint64_t)lane;
     const bool act = h.fn != kNoEv;
+    render_pre_ready(pre);
     int linelen = 0;
     if (act) {
       const uint32_t typ = h.fn >> 30;
@@ -1482,7 +1516,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       in.rl = (int)((h.fn >> 20) & 7u);
       in.tx[0] = pre.t0.x, in.tx[1] = pre.t0.y, in.tx[2] = pre.t0.z, in.tx[3] = pre.t0.w, in.tx[4] = pre.t1.x,
       in.tx[5] = pre.t1.y;
-      in.ns_pre = pre.ns;
+      in.ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
       LineSink k;
       k.line = my_line;
       k.pos = 0;
@@ -1504,7 +1538,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     const uint32_t fn_cur = h.fn;
     const uint32_t ai_cur = pre.ai;
     // the next chunk's inputs load behind this one's output
-    h = hn;
+    h = decode_hot(hn, c + nw < W.n_chunks);
     hn = load_hot(W, c + 2 * nw, lane);
     render_pre(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);
     const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
@@ -1704,10 +1738,11 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
         int x0 = fc - kTcQ / 2;
         if (x0 < 0) x0 = 0;
-        const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;
+        const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
+        const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
         v4u qv[kTcQ / 16];
 #pragma unroll
-        for (int q = 0; q < kTcQ / 16; q++) qv[q] = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+        for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
 #pragma unroll
         for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
 #pragma unroll
@@ -1716,7 +1751,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         r.op_lo = o0;
         r.op_n = (uint32_t)kTcOps;
         r.qw = me->qw;
-        r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+        r.qlo = x0a;
         r.qn = kTcQ;
         const uint32_t wd = opword(r, (uint32_t)j);
         int ne = (int)(h.fn & kNBig);
@@ -1813,12 +1848,12 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     const int rl = event_rloc(r.L, rev, typ, h.qp, ne);
     int x0 = rl - 8;
     if (x0 < 0) x0 = 0;
-    const uintptr_t a0 = (uintptr_t)(r.R + x0) & ~(uintptr_t)15;
+    const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
+    const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
 #pragma unroll
-    for (int q = 0; q < kQWin / 16; q++)
-      *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = *reinterpret_cast<const v4u*>(a0 + 16 * q);
+    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];
     r.qw = me->qw;
-    r.qlo = (int)((intptr_t)a0 - (intptr_t)r.R);
+    r.qlo = x0a;
     r.qn = kQWin;
     const uint32_t l0 = h.ls & ~3u;
     const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
@@ -1839,7 +1874,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
     in.ns_pre = kNsNone;
     GlobalSink g;
-    g.p = A.text + f.dst;
+    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);
     g.pos = 0;
     int rel;
     emit_event(g, r, in, skip, rel);
