@@ -1455,12 +1455,16 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     fprintf(stderr, "Error: invalid FASTA file %s !\n", fa);
     return 1;
   }
+  const bool prof = getenv("PW_PROFILE_HOST") != nullptr;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t_start = prof ? now() : 0;
   QueryDb qdb;
   std::string err;
   if (!qdb.load(fa, err)) {
     fputs(err.c_str(), stderr);
     return 1;
   }
+  const double t_fasta = prof ? now() : 0;
   if (!fullgenome && !gene && fsize > 120000) fullgenome = true;
   bool skip_codan = fullgenome || force_noncoding;
   if (!skip_codan && !force_coding && fsize > 120000) skip_codan = true;
@@ -1478,6 +1482,8 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   }
   Device dev;
   if (!dev.init(qdb, skip_codan)) return 2;
+  const double t_dev = prof ? now() : 0;
+  if (prof) fprintf(stderr, "[cli] fasta %.3f s, device init %.3f s\n", t_fasta - t_start, t_dev - t_fasta);
   Packer pk;
   pk.qdb = &qdb;
   pk.nt = host_threads();
@@ -1512,8 +1518,13 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
       const int o = cur ^ 1;
       nxt = std::async(std::launch::async, [&, o] { return pack_next(bb[o]); });
     }
-    const int rc = dev.run(B, skip_codan, text_h, res_h, pages_h) ? emit(B, text_h.data(), res_h.data(), pages_h.data(), out.f)
-                                                                  : 2;
+    const double t_r0 = prof ? now() : 0;
+    const bool ran = dev.run(B, skip_codan, text_h, res_h, pages_h);
+    const double t_r1 = prof ? now() : 0;
+    const int rc = ran ? emit(B, text_h.data(), res_h.data(), pages_h.data(), out.f) : 2;
+    if (prof)
+      fprintf(stderr, "[cli] batch: gpu run + copies %.3f s (%zu text bytes), emit %.3f s\n", t_r1 - t_r0, text_h.size(),
+              now() - t_r1);
     if (rc >= 0) {
       if (more) nxt.wait();
       fflush(out.f);
@@ -1523,6 +1534,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     cur ^= 1;
   }
   fflush(out.f);
+  if (prof) fprintf(stderr, "[cli] total %.3f s\n", now() - t_start);
   if (fmsa.f && pk.run.qi >= 0) {  // refMSA->writeMSA(fmsa), pafreport.cpp:447-450
     const int qi = pk.run.qi;
     const int rc = pw::write_run_msa(fmsa.f, qdb.ids[(size_t)qi].c_str(), qdb.seq.data() + qdb.off[(size_t)qi],

@@ -1000,8 +1000,8 @@ struct Work {
   Cold* cold;
   uint8_t* tx;
   uint8_t* sflag;
-  Fixup* fix;
-  uint32_t fix_cap;
+  Fixup* fix;         // per slot: the destination of a long line (written only for long lines)
+  uint64_t* lmask;    // per chunk: lanes whose line is longer than the LDS line buffer
   uint64_t n_slots, n_chunks;
   uint64_t arena0;  // first arena byte in text (= n_chunks * PW_PAGE_BYTES)
 };
@@ -1024,7 +1024,9 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
   const uint64_t o_sflag = o;
   o = align_up(o + ns, 256);
   const uint64_t o_fix = o;
-  o = align_up(o + sizeof(Fixup) * (n_slots ? n_slots : 1), 256);
+  o = align_up(o + sizeof(Fixup) * ns, 256);
+  const uint64_t o_lmask = o;
+  o = align_up(o + 8 * (n_chunks ? n_chunks : 1), 256);
   if (w && base) {
     w->ctr = reinterpret_cast<uint32_t*>(base);
     w->arena_used = reinterpret_cast<unsigned long long*>(base + 16);
@@ -1034,7 +1036,7 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->tx = base + o_tx;
     w->sflag = base + o_sflag;
     w->fix = reinterpret_cast<Fixup*>(base + o_fix);
-    w->fix_cap = n_slots > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(n_slots ? n_slots : 1);
+    w->lmask = reinterpret_cast<uint64_t*>(base + o_lmask);
     w->n_slots = n_slots;
     w->n_chunks = n_chunks;
     w->arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
@@ -1042,17 +1044,23 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
   return o;
 }
 
+// (every caller runs 256 threads: each thread issues its three loads before any store, so the
+// staging costs one memory round trip, not three)
 __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid, int nthreads) {
   const uint8_t* s = reinterpret_cast<const uint8_t*>(&c_tables);
   LDS uint8_t* d = reinterpret_cast<LDS uint8_t*>(dst);
-  for (int i = tid; i < 256; i += nthreads) {
-    d[offsetof(SmallTables, comp) + i] = s[offsetof(Tables, comp) + i];
-  }
-  for (int i = tid; i < 64; i += nthreads) d[offsetof(SmallTables, codon64) + i] = s[offsetof(Tables, codon64) + i];
-  for (int i = tid; i < 96; i += nthreads) d[offsetof(SmallTables, status) + i] = s[offsetof(Tables, status) + i];
-  for (int i = tid; i < 100; i += nthreads) {
-    d[offsetof(SmallTables, dig2) + 2 * i] = (uint8_t)('0' + i / 10);
-    d[offsetof(SmallTables, dig2) + 2 * i + 1] = (uint8_t)('0' + i % 10);
+  for (int i0 = 0; i0 < 256; i0 += nthreads) {
+    const int i = i0 + tid;
+    const uint8_t b0 = s[offsetof(Tables, comp) + (i < 256 ? i : 255)];
+    const uint8_t b1 = s[offsetof(Tables, codon64) + (i < 64 ? i : 63)];
+    const uint8_t b2 = s[offsetof(Tables, status) + (i < 96 ? i : 95)];
+    if (i < 256) d[offsetof(SmallTables, comp) + i] = b0;
+    if (i < 64) d[offsetof(SmallTables, codon64) + i] = b1;
+    if (i < 96) d[offsetof(SmallTables, status) + i] = b2;
+    if (i < 100) {
+      d[offsetof(SmallTables, dig2) + 2 * i] = (uint8_t)('0' + i / 10);
+      d[offsetof(SmallTables, dig2) + 2 * i + 1] = (uint8_t)('0' + i % 10);
+    }
   }
 }
 
@@ -1074,17 +1082,28 @@ struct RecPre {
   uint64_t qb, ev_next;
   int L;
   uint32_t w0, w1;
+  bool last;  // ai is the batch's last record (ev_next = n_ev_slots)
 };
+// All loads unconditional (clamped / dummy addresses; see pin()): the values are selected when
+// the record is processed, one record later.
 __device__ __forceinline__ void rec_pre(const pw_report_args& A, uint32_t ai, const pw_aln_desc& d, int lane,
                                         RecPre& p) {
   p.d = d;
   const uint32_t qi = d.ref & PW_REF_QMASK;
   p.qb = A.qoff[qi];
   p.L = A.qlen[qi];
-  p.ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;
+  p.last = ai + 1 >= A.n_alns;
+  p.ev_next = A.desc[p.last ? ai : ai + 1].ev_begin;
   const uint32_t* ops = A.ops + d.op_begin;
-  p.w0 = (uint32_t)lane < d.n_ops ? ops[lane] : 0u;
-  p.w1 = (uint32_t)(lane + 64) < d.n_ops ? ops[lane + 64] : 0u;
+  const uint32_t* dummy = reinterpret_cast<const uint32_t*>(A.desc);
+  p.w0 = *((uint32_t)lane < d.n_ops ? ops + lane : dummy);
+  p.w1 = *((uint32_t)(lane + 64) < d.n_ops ? ops + lane + 64 : dummy);
+}
+__device__ __forceinline__ void rec_pre_ready(const pw_report_args& A, RecPre& p, int lane) {
+  asm volatile("" : "+v"(p.qb), "+v"(p.ev_next), "+v"(p.L), "+v"(p.w0), "+v"(p.w1));
+  if (p.last) p.ev_next = A.n_ev_slots;
+  if ((uint32_t)lane >= p.d.n_ops) p.w0 = 0u;
+  if ((uint32_t)(lane + 64) >= p.d.n_ops) p.w1 = 0u;
 }
 
 __device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
@@ -1299,19 +1318,22 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
   // processed (its descriptor two records ahead), so their latency overlaps the work
   const uint32_t stride = gridDim.x * kWaves;
   uint32_t ai = blockIdx.x * kWaves + wv;
-  RecPre cur;
-  pw_aln_desc dn;
-  if (ai < A.n_alns) rec_pre(A, ai, A.desc[ai], lane, cur);
-  if (ai + stride < A.n_alns) dn = A.desc[ai + stride];
-  for (; ai < A.n_alns; ai += stride) {
-    const uint32_t an = ai + stride;
-    RecPre nxt;
-    pw_aln_desc dnn;
-    if (an < A.n_alns) rec_pre(A, an, dn, lane, nxt);
-    if (an + stride < A.n_alns) dnn = A.desc[an + stride];
-    index_record(A, W, tp, w, ai, lane, cur);
-    cur = nxt;
-    dn = dnn;
+  if (ai < A.n_alns) {
+    // (indices past the batch are clamped to its last record: the loads stay unconditional)
+    const uint32_t nm1 = A.n_alns - 1;
+    RecPre cur;
+    rec_pre(A, ai, A.desc[ai], lane, cur);
+    pw_aln_desc dn = A.desc[ai + stride < A.n_alns ? ai + stride : nm1];
+    for (; ai < A.n_alns; ai += stride) {
+      const uint32_t an = ai + stride;
+      RecPre nxt;
+      rec_pre(A, an < A.n_alns ? an : nm1, dn, lane, nxt);
+      const pw_aln_desc dnn = A.desc[an + stride < A.n_alns ? an + stride : nm1];
+      rec_pre_ready(A, cur, lane);
+      index_record(A, W, tp, w, ai, lane, cur);
+      cur = nxt;
+      dn = dnn;
+    }
   }
   // the padding slots of the last chunk are empty
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
@@ -1557,12 +1579,18 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         if (lane == 0) atomicOr(&W.ctr[2], 1u);
       }
     }
+    // long lines -> fixup_kernel: the chunk's lane mask (every chunk writes it) and the lines'
+    // destinations — plain stores: a returning atomic here cost a round trip per chunk with a
+    // long line
+    const bool need_fix = ok && linelen > kLine;
+    const uint64_t lm = __ballot(need_fix);
     if (lane == 0) {
       pw_page pg;
       pg.off = P;
       pg.len = ok ? B : 0u;
       pg.pad = 0;
       A.pages[c] = pg;
+      W.lmask[c] = lm;
     }
     const uint64_t g0 = P + my_off;
     if (act && (fn_cur & (3u << 26))) {  // first / last line of a record
@@ -1577,22 +1605,12 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       }
     }
     if (ok && B > 0) {
-      // long lines -> fixup list (one wave-aggregated atomic)
-      const bool need = linelen > kLine;
-      const uint64_t nm = __ballot(need);
-      if (nm) {
-        uint32_t fb = 0;
-        if (lane == 0) fb = atomicAdd(&W.ctr[1], (uint32_t)__popcll(nm));
-        fb = bcast(fb, 0);
-        const uint32_t slot = fb + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
-        if (need && slot < W.fix_cap) {
-          Fixup f;
-          f.s = (uint32_t)s;
-          f.pad = 0;
-          f.dst = g0;
-          W.fix[slot] = f;
-        }
-        if (__ballot(need && slot >= W.fix_cap) && lane == 0) atomicOr(&W.ctr[2], 2u);
+      if (need_fix) {  // the line's destination for fixup_kernel
+        Fixup f;
+        f.s = (uint32_t)s;
+        f.pad = 0;
+        f.dst = g0;
+        W.fix[s] = f;
       }
       // chunk map: 16-byte block ci of the page -> line holding its first byte (P is 16-byte
       // aligned: pages are PW_PAGE_BYTES apart, arena allocations 16-byte multiples)
@@ -1689,9 +1707,18 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
   const uint64_t n_groups = (W.n_chunks * kWave + 255) / 256;
   const uint32_t* f32 = reinterpret_cast<const uint32_t*>(W.sflag);
   const uint64_t nf32 = W.n_chunks * kWave / 4;
-  for (uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv; gi < n_groups; gi += (uint64_t)gridDim.x * kWaves) {
+  // the next group's flag words load one group ahead (clamped index, masked when consumed)
+  const uint64_t gstride = (uint64_t)gridDim.x * kWaves;
+  uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv;
+  const uint64_t flast = nf32 ? nf32 - 1 : 0;
+  uint32_t fnext = nf32 ? f32[gi * kWave + lane < nf32 ? gi * kWave + lane : flast] : 0u;
+  for (; gi < n_groups; gi += gstride) {
     const uint64_t fi = gi * kWave + lane;
-    const uint32_t f4 = (fi < nf32 ? f32[fi] : 0u) & 0x01010101u;
+    uint32_t fcur = fnext;
+    asm volatile("" : "+v"(fcur));
+    const uint64_t fin = fi + gstride * kWave;
+    fnext = nf32 ? f32[fin < nf32 ? fin : flast] : 0u;
+    const uint32_t f4 = (fi < nf32 ? fcur : 0u) & 0x01010101u;
     const uint32_t cnt = (uint32_t)__popc(f4);
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = wave_last(incl);
@@ -1732,9 +1759,14 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
         const int j = (int)p0.y;
         int o0 = j - kTcOps / 2;
         if (o0 < 0) o0 = 0;
+        // (indices clamped to the record's last op, values masked after: a guarded load would be
+        // a branch and a vmcnt(0) per word)
         uint32_t ow[kTcOps];
+        const uint32_t olast = r.n_ops ? r.n_ops - 1 : 0u;
 #pragma unroll
-        for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? r.ops[o0 + q] : 0u;
+        for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
+#pragma unroll
+        for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
         const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
         int x0 = fc - kTcQ / 2;
         if (x0 < 0) x0 = 0;
@@ -1793,20 +1825,36 @@ struct FixLane {
 __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) FixLane fl[256];
+  __shared__ uint64_t mk[kWaves][kWave];  // the long-line masks of the wave's 64 chunks
+  __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, 256);
   __syncthreads();
   LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x];
-  const uint32_t n = min(W.ctr[1], W.fix_cap);
   const bool skip = A.skip_codan != 0;
   if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
-  // consecutive lines go to different workgroups, then to different waves: a wave gets one or
-  // two lines, not 64 divergent ones
-  const uint32_t q0 = threadIdx.x / kWave + kWaves * (threadIdx.x % kWave);
-  for (uint32_t q = q0;; q += 256) {
-    const uint32_t i = blockIdx.x + gridDim.x * q;
-    if (i >= n) break;
-    const Fixup f = W.fix[i];
+  // a wave takes 64 chunks at a time and spreads their long lines over its lanes (line j of the
+  // group -> lane j % 64): the chunk of line j is the last one whose prefix is <= j
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint64_t nwt = (uint64_t)gridDim.x * kWaves;
+  for (uint64_t c0 = ((uint64_t)blockIdx.x * kWaves + wv) * kWave; c0 < W.n_chunks; c0 += nwt * kWave) {
+    const uint64_t cl = c0 + (uint64_t)lane;
+    const uint64_t m = cl < W.n_chunks ? W.lmask[cl] : 0ull;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t T = wave_last(incl);
+    if (T == 0) continue;
+    mk[wv][lane] = m;
+    ex[wv][lane] = incl - cnt;
+    wave_sync();
+  for (uint32_t jl = (uint32_t)lane; jl < T; jl += kWave) {
+    int k = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if (k + step < kWave && ex[wv][k + step] <= jl) k += step;
+    uint64_t mm = mk[wv][k];
+    for (uint32_t r = jl - ex[wv][k]; r > 0; r--) mm &= mm - 1;
+    const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];
     const Hot h = W.hot[f.s];
     const uint32_t typ = h.fn >> 30;
     const bool rev = (h.fn >> 29) & 1u;
@@ -1878,6 +1926,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     g.pos = 0;
     int rel;
     emit_event(g, r, in, skip, rel);
+  }
+    wave_sync();
   }
 }
 

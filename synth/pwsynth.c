@@ -628,6 +628,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(k, "--rev")) o.rev = atof(v);
     else if (!strcmp(k, "--partial")) o.partial = atof(v);
     else if (!strcmp(k, "--subrun")) o.p_subrun = atof(v);
+    else if (!strcmp(k, "--psub")) o.p_sub = atof(v);
+    else if (!strcmp(k, "--pdel")) o.p_del = atof(v);
+    else if (!strcmp(k, "--pins")) o.p_ins = atof(v);
     else if (!strcmp(k, "--longindel")) o.p_longindel = atof(v);
     else if (!strcmp(k, "--inframe")) o.p_inframe = atof(v);
     else if (!strcmp(k, "--margin")) o.margin = atoi(v);
