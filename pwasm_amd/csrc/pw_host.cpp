@@ -1157,8 +1157,9 @@ struct Device {
     HIPCHK(hipStreamSynchronize(stream));
     return true;
   }
-  // run the batch; fills text/results on the host
-  bool run(const Batch& b, bool skip_codan, std::vector<uint8_t>& text_h, std::vector<pw_aln_result>& res_h,
+  // run the batch; fills results / pages on the host (and the text, unless text_h is null: the
+  // CLI streams it with a TextStream instead)
+  bool run(const Batch& b, bool skip_codan, std::vector<uint8_t>* text_h, std::vector<pw_aln_result>& res_h,
            std::vector<pw_page>& pages_h) {
     const size_t na = b.desc.size();
     res_h.resize(na);
@@ -1201,13 +1202,14 @@ struct Device {
     HIPCHK(hipMemcpyAsync(res_h.data(), res.p, na * sizeof(pw_aln_result), hipMemcpyDeviceToHost, stream));
     if (np) HIPCHK(hipMemcpyAsync(pages_h.data(), pages.p, np * sizeof(pw_page), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
+    if (!text_h) return true;
     // copy back the used part of the text (pages + arena)
     uint64_t used = 0;
     for (const pw_page& pg : pages_h)
       if (pg.len && pg.off + pg.len > used) used = pg.off + pg.len;
     if (used > tcap) used = tcap;
-    text_h.resize(used);
-    if (used) HIPCHK(hipMemcpy(text_h.data(), text.p, used, hipMemcpyDeviceToHost));
+    text_h->resize(used);
+    if (used) HIPCHK(hipMemcpy(text_h->data(), text.p, used, hipMemcpyDeviceToHost));
     return true;
   }
   ~Device() {
@@ -1215,18 +1217,109 @@ struct Device {
   }
 };
 
+// The report text of a finished batch, streamed to the host in the order the emit loop reads
+// it: the page region [0, arena0) through two pinned windows (the DMA of window k + 1 runs while
+// window k is written out), the arena (pages that overflowed, read out of order) as one host copy.
+// Pages are PW_PAGE_BYTES-aligned and no longer than that, and the window is a multiple of it, so
+// a page never straddles two windows.
+struct TextStream {
+  static constexpr uint64_t kWin = 32ull << 20;
+  uint8_t* buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipStream_t st = nullptr;
+  uint64_t base[2] = {0, 0};
+  int cur = 0;
+  bool waited = false;
+  const uint8_t* dev = nullptr;
+  uint64_t region_end = 0, arena0 = 0;
+  std::vector<uint8_t> arena;
+  bool ok = false;
+  bool init() {
+    if (ok) return true;
+    for (int k = 0; k < 2; k++)
+      if (hipHostMalloc((void**)&buf[k], kWin, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess)
+        return false;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+    ok = true;
+    return true;
+  }
+  void fetch(int k) {
+    const uint64_t n = base[k] < region_end ? std::min(kWin, region_end - base[k]) : 0;
+    if (n) (void)hipMemcpyAsync(buf[k], dev + base[k], n, hipMemcpyDeviceToHost, st);
+    (void)hipEventRecord(ev[k], st);
+  }
+  // start streaming the text of a finished batch (pages on the host already)
+  bool begin(const uint8_t* text_dev, const std::vector<pw_page>& pages, uint64_t n_chunks) {
+    dev = text_dev;
+    arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
+    region_end = 0;
+    uint64_t aend = arena0;
+    for (const pw_page& pg : pages) {
+      if (!pg.len) continue;
+      if (pg.off < arena0) region_end = std::max(region_end, pg.off + pg.len);
+      else aend = std::max(aend, pg.off + pg.len);
+    }
+    arena.resize(aend - arena0);
+    if (!arena.empty() && hipMemcpy(arena.data(), dev + arena0, arena.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      return false;
+    cur = 0;
+    waited = false;
+    base[0] = 0;
+    base[1] = kWin;
+    fetch(0);
+    fetch(1);
+    return true;
+  }
+  const uint8_t* at(uint64_t off, size_t) {
+    if (off >= arena0) return arena.data() + (off - arena0);
+    while (off >= base[cur] + kWin) {  // window cur is done: refill it two windows ahead
+      if (!waited) (void)hipEventSynchronize(ev[cur]);
+      base[cur] += 2 * kWin;
+      fetch(cur);
+      cur ^= 1;
+      waited = false;
+    }
+    if (!waited) {
+      (void)hipEventSynchronize(ev[cur]);
+      waited = true;
+    }
+    return buf[cur] + (off - base[cur]);
+  }
+  void end() {  // nothing in flight after the batch (the buffers are reused)
+    if (st) (void)hipStreamSynchronize(st);
+  }
+  ~TextStream() {
+    end();
+    for (int k = 0; k < 2; k++) {
+      if (buf[k]) (void)hipHostFree(buf[k]);
+      if (ev[k]) (void)hipEventDestroy(ev[k]);
+    }
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
 // Print what the reference prints for one log item; returns -1 to continue, else the exit code
 // the reference ends with at this item.
 // Write the first `nlines` event lines of a record (all of them when nlines == n_events): the
 // bytes from text_off to text_end, crossing pages in chunk order (pwasm_amd.h, text pages).
-void write_lines(const uint8_t* text, const pw_page* pages, const pw_aln_result& r, uint32_t nlines, FILE* out) {
+// Where write_lines reads report text: a whole host copy (batch API), or a stream of pinned
+// windows copied from the device while the emit loop writes (CLI, TextStream below).
+struct TextSrc {
+  const uint8_t* host = nullptr;
+  struct TextStream* stream = nullptr;
+  const uint8_t* at(uint64_t off, size_t n) const;
+};
+const uint8_t* TextSrc::at(uint64_t off, size_t n) const { return host ? host + off : stream->at(off, n); }
+
+void write_lines(const TextSrc& text, const pw_page* pages, const pw_aln_result& r, uint32_t nlines, FILE* out) {
   if (r.n_events == 0 || nlines == 0) return;
   uint32_t seen = 0;
   for (uint32_t c = r.page_first;; c++) {
     const uint64_t lo = c == r.page_first ? r.text_off : pages[c].off;
     const uint64_t hi = c == r.page_last ? r.text_end : pages[c].off + pages[c].len;
-    const uint8_t* p = text + lo;
     size_t n = (size_t)(hi - lo);
+    const uint8_t* p = text.at(lo, n);
     if (nlines != r.n_events) {  // stop after the nlines-th newline
       size_t k = 0;
       while (k < n && seen < nlines) {
@@ -1240,7 +1333,7 @@ void write_lines(const uint8_t* text, const pw_page* pages, const pw_aln_result&
   }
 }
 
-int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_aln_result* res, const pw_page* pages,
+int emit_item(const Batch& b, const LogItem& it, const TextSrc& text, const pw_aln_result* res, const pw_page* pages,
               FILE* out, FILE* err) {
   if (it.kind == 0) {
     fputs(b.msgs[it.idx].c_str(), err);
@@ -1301,7 +1394,7 @@ int emit_item(const Batch& b, const LogItem& it, const uint8_t* text, const pw_a
 }
 
 // Print what the reference prints for this batch; returns -1 to continue, else an exit code.
-int emit(const Batch& b, const uint8_t* text, const pw_aln_result* res, const pw_page* pages, FILE* out) {
+int emit(const Batch& b, const TextSrc& text, const pw_aln_result* res, const pw_page* pages, FILE* out) {
   for (const LogItem& it : b.log) {
     const int rc = emit_item(b, it, text, res, pages, out, stderr);
     if (rc >= 0) return rc;
@@ -1408,6 +1501,19 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     return 1;
   }
   const bool verbose = args.set['v'] || debug;
+  // the HIP runtime / context comes up on its own thread while the FASTA and the first batch are
+  // read and packed (about 0.1 s of device initialisation hidden)
+  struct Warm {
+    std::thread t;
+    Warm() : t([] {
+      int n = 0;
+      if (hipGetDeviceCount(&n) == hipSuccess && n > 0) (void)hipFree(nullptr);
+    }) {}
+    void join() {
+      if (t.joinable()) t.join();
+    }
+    ~Warm() { join(); }
+  } warm;
   FileCloser in, out;
   in.f = stdin;
   if (!args.nonopt.empty() && args.nonopt[0][0]) {
@@ -1443,6 +1549,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
       fprintf(stderr, "Cannot open file %s for writing!\n", args.val['o']);
       return 1;
     }
+    setvbuf(out.f, nullptr, _IOFBF, 8u << 20);  // the report is written in large blocks
   }
   const char* fa = args.set['r'] ? args.val['r'] : "";
   if (!fa[0]) {
@@ -1481,9 +1588,6 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     }
   }
   Device dev;
-  if (!dev.init(qdb, skip_codan)) return 2;
-  const double t_dev = prof ? now() : 0;
-  if (prof) fprintf(stderr, "[cli] fasta %.3f s, device init %.3f s\n", t_fasta - t_start, t_dev - t_fasta);
   Packer pk;
   pk.qdb = &qdb;
   pk.nt = host_threads();
@@ -1496,7 +1600,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   // packed (by pk.nt threads); nothing past a fatal batch is packed.
   ChunkReader rd(in.f);
   Batch bb[2];
-  std::vector<uint8_t> text_h;
+  TextStream tstream;
   std::vector<pw_aln_result> res_h;
   std::vector<pw_page> pages_h;
   size_t kChunk = 256u << 20;  // input bytes per batch (PW_CHUNK_BYTES: tests force many batches)
@@ -1510,6 +1614,12 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   };
   int cur = 0;
   bool have = pack_next(bb[0]);
+  const double t_pack0 = prof ? now() : 0;
+  warm.join();
+  if (!dev.init(qdb, skip_codan)) return 2;
+  if (prof)
+    fprintf(stderr, "[cli] fasta %.3f s, first batch read + pack %.3f s, device init (after warm-up) %.3f s\n",
+            t_fasta - t_start, t_pack0 - t_fasta, now() - t_pack0);
   while (have) {
     Batch& B = bb[cur];
     const bool more = !B.fatal;
@@ -1519,11 +1629,16 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
       nxt = std::async(std::launch::async, [&, o] { return pack_next(bb[o]); });
     }
     const double t_r0 = prof ? now() : 0;
-    const bool ran = dev.run(B, skip_codan, text_h, res_h, pages_h);
+    bool ran = dev.run(B, skip_codan, nullptr, res_h, pages_h);
+    ran = ran && tstream.init() &&
+          tstream.begin(dev.text.p, pages_h, pw_report_page_count(B.n_events_max));
     const double t_r1 = prof ? now() : 0;
-    const int rc = ran ? emit(B, text_h.data(), res_h.data(), pages_h.data(), out.f) : 2;
+    TextSrc src;
+    src.stream = &tstream;
+    const int rc = ran ? emit(B, src, res_h.data(), pages_h.data(), out.f) : 2;
+    tstream.end();
     if (prof)
-      fprintf(stderr, "[cli] batch: gpu run + copies %.3f s (%zu text bytes), emit %.3f s\n", t_r1 - t_r0, text_h.size(),
+      fprintf(stderr, "[cli] batch: gpu run + result copies %.3f s, emit (text streamed) %.3f s\n", t_r1 - t_r0,
               now() - t_r1);
     if (rc >= 0) {
       if (more) nxt.wait();
@@ -1634,7 +1749,9 @@ extern "C" int pw_batch_write_report(const pw_batch* bt, const uint8_t* text_hos
   if (!bt || !path) return PW_E_ARG;
   FILE* f = fopen(path, "wb");
   if (!f) return PW_E_IO;
-  int rc = emit(bt->b, text_host, res_host, pages_host, f);
+  TextSrc src;
+  src.host = text_host;
+  int rc = emit(bt->b, src, res_host, pages_host, f);
   fclose(f);
   return rc < 0 ? 0 : rc;
 }
@@ -1659,7 +1776,9 @@ extern "C" int pw_batch_write_items(const pw_batch* bt, const uint8_t* text_host
       if (e) fclose(e);
       break;
     }
-    const int32_t st = emit_item(bt->b, it, text_host, res_host, pages_host, o, e);
+    TextSrc src;
+    src.host = text_host;
+    const int32_t st = emit_item(bt->b, it, src, res_host, pages_host, o, e);
     fclose(o);
     fclose(e);
     const uint32_t no = (uint32_t)on, ne = (uint32_t)en;

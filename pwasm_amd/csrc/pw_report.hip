@@ -66,7 +66,7 @@ constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, f
 constexpr uint32_t kNBig = (1u << 19) - 1;  // evtbases length field saturates here
 constexpr uint32_t kFnAcgt = 1u << 19;      // query + record literals all A/C/G/T (PW_REF_ACGT)
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
-constexpr int kIndexOcc = 4;    // index_kernel: waves per SIMD the register budget is sized for
+constexpr int kIndexOcc = 5;    // index_kernel: waves per SIMD the register budget is sized for
 constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)
 
 // Render record of one event (index_kernel -> render_kernel), 32 bytes.
