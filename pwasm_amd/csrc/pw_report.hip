@@ -1345,8 +1345,9 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
-  uint32_t ostart[kWave + 1];       // line starts in the page
-  uint8_t cmap[kMap];               // 16-byte output chunk -> lane of its first line
+  uint32_t ostart[kWave + 1];       // starts of the page's non-empty lines (+ the page end)
+  uint8_t olane[kWave + 1];         // their lanes
+  uint8_t cmap[kMap];               // 16-byte output block -> line holding its first byte
 };
 
 // the record owning event slot s: the last one whose first slot is <= s (error path only)
@@ -1612,56 +1613,62 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         f.dst = g0;
         W.fix[s] = f;
       }
-      // chunk map: 16-byte block ci of the page -> line holding its first byte (P is 16-byte
-      // aligned: pages are PW_PAGE_BYTES apart, arena allocations 16-byte multiples)
+      // the page's non-empty lines in order (k -> start, lane) and the chunk map: 16-byte block ci
+      // of the page -> k of the line holding its first byte (P is 16-byte aligned: pages are
+      // PW_PAGE_BYTES apart, arena allocations 16-byte multiples)
       uint8_t* const gb = A.text + P;
-      w->ostart[lane] = my_off;
-      if (lane == 0) w->ostart[kWave] = B;
+      const uint64_t ne = __ballot(linelen > 0);
+      const int nl = __popcll(ne);
+      const int kme = __popcll(ne & ((1ull << lane) - 1ull));
       if (linelen > 0) {
+        w->ostart[kme] = my_off;
+        st8(&w->olane[kme], (uint8_t)lane);
         const uint32_t c1 = (my_off + (uint32_t)linelen + 15) >> 4;
         // (byte stores: a vectorised fill would be unaligned ds_write_b128)
-        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) st8(&w->cmap[ci], (uint8_t)lane);
-        if (my_off == 0) st8(&w->cmap[0], (uint8_t)lane);
+        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) st8(&w->cmap[ci], (uint8_t)kme);
+        if (my_off == 0) st8(&w->cmap[0], (uint8_t)kme);
       }
+      if (lane == 0) w->ostart[nl] = B;
       wave_sync();
-      // gather: each lane assembles 16 output bytes from (at most a few) line buffers with
-      // aligned dword reads + byte-align shifts, then one 16-byte store
+      // gather: a 16-byte output block holds the tail of one line (A) and at most the head of the
+      // next (B): lines are >= 40 bytes.  Both are read as 16-byte images (aligned dword reads +
+      // byte-align shifts; B's image starts before its line — those bytes are masked off), merged
+      // by a byte mask, then one 16-byte store.
       for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {
-        uint32_t b = cc;
-        const uint32_t be = (cc + 16 < B) ? cc + 16 : B;
-        int oi;
+        int k;
         if ((cc >> 4) < (uint32_t)kMap) {
-          oi = w->cmap[cc >> 4];
-        } else {  // past the map (pages with long lines): last line starting at or before b
-          oi = 0;
+          k = w->cmap[cc >> 4];
+        } else {  // past the map (pages with long lines): last line starting at or before cc
+          k = 0;
 #pragma unroll
           for (int step = 32; step >= 1; step >>= 1)
-            if (oi + step <= kWave - 1 && w->ostart[oi + step] <= b) oi += step;
+            if (k + step < nl && w->ostart[k + step] <= cc) k += step;
         }
-        uint32_t v[4] = {0u, 0u, 0u, 0u};
-        while (b < be) {
-          const uint32_t s0 = w->ostart[oi], s1 = w->ostart[oi + 1];
-          const uint32_t pe = s1 < be ? s1 : be;
-          if (pe > b) {
-            int x = (int)cc - (int)s0;     // line offset at block position 0, >= -15
-            if (x > kLine) x = kLine;      // long line: garbage here, fixup_kernel rewrites it
-            const int a = oi * kLStride + x;
-            const LDS uint32_t* src = reinterpret_cast<const LDS uint32_t*>(w->line + (a & ~3));
-            const uint32_t sh = (uint32_t)a & 3u;
-            uint32_t dd[5];
+        const uint32_t s0 = w->ostart[k], s1 = w->ostart[k + 1];
+        const int la = w->olane[k], lb = w->olane[k + 1 < nl ? k + 1 : k];
+        int xa = (int)cc - (int)s0;  // >= 0
+        if (xa > kLine) xa = kLine;  // long line: garbage here, fixup_kernel rewrites it
+        int xb = (int)cc - (int)s1;  // < 0 while the block starts in line A
+        if (xb < -16) xb = -16;
+        const int aa = la * kLStride + xa, ab = lb * kLStride + xb;  // (ab >= 0: lb >= 1 when it is used)
+        const LDS uint32_t* pa = reinterpret_cast<const LDS uint32_t*>(w->line + (aa & ~3));
+        const LDS uint32_t* pb = reinterpret_cast<const LDS uint32_t*>(w->line + (ab > 0 ? (ab & ~3) : 0));
+        uint32_t da[5], db[5];
 #pragma unroll
-            for (int i = 0; i < 5; i++) dd[i] = src[i];
-            const uint32_t qlo = b - cc, qhi = pe - cc;
-            const uint32_t m16 = ((1u << qhi) - 1u) & ~((1u << qlo) - 1u);
+        for (int i = 0; i < 5; i++) {
+          da[i] = pa[i];
+          db[i] = pb[i];
+        }
+        const uint32_t sa = (uint32_t)aa & 3u, sb = (uint32_t)ab & 3u;
+        const int nka = (int)(s1 - cc);  // bytes of the block from line A (>= 16: all)
+        uint32_t v[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-              const uint32_t nib = (m16 >> (4 * i)) & 15u;
-              const uint32_t bm = ((nib * 0x00204081u) & 0x01010101u) * 0xFFu;
-              v[i] |= __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh) & bm;
-            }
-          }
-          b = pe > b ? pe : b;
-          oi++;
+        for (int i = 0; i < 4; i++) {
+          int n = nka - 4 * i;
+          n = n < 0 ? 0 : (n > 4 ? 4 : n);
+          const uint32_t m = (uint32_t)((1ull << (8 * n)) - 1ull);
+          v[i] = (__builtin_amdgcn_alignbyte(da[i + 1], da[i], sa) & m) |
+                 (__builtin_amdgcn_alignbyte(db[i + 1], db[i], sb) & ~m);
         }
         v4u vv;
         vv.x = v[0];

@@ -16,6 +16,8 @@ PATCHES = {
                ("        o.put_span(in.tx, (int)(in.tx[0] & 0xFFu));\n", "")],
     "noqctx": [("      o.put_bytes(rv, 10);\n      o.put_bytes(sv, sl);\n", "")],
     "nohead": [("      wr_num(o, r.tab, (uint32_t)(e.rloc + 1));\n", ""), ("      wr_num(o, r.tab, (uint32_t)(aap0 + 1));\n", "")],
+    "nocod_sub": [("    if (typ == PW_OP_SUB) {\n      const int p0 = e.rloc - e.r_trloc;", "    if (false) {\n      const int p0 = e.rloc - e.r_trloc;")],
+    "nocod_indel": [("      indel_impact(k, r, e, in.ns_pre);\n", "")],
     "nogather": [("for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {",
                   "for (uint32_t cc = (uint32_t)lane * 16; cc < 0u; cc += kWave * 16) {")],
 }
