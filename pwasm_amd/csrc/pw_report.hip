@@ -1140,7 +1140,12 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const uint32_t idx = 64 * k + lane;
-      wd[k] = sb == 0 ? (k == 0 ? pre.w0 : pre.w1) : (idx < nseg ? ops[sb + idx] : 0u);
+      if (sb == 0) {
+        wd[k] = k == 0 ? pre.w0 : pre.w1;
+      } else {  // (clamped index: an unconditional load)
+        const uint32_t w = ops[idx < nseg ? sb + idx : sb];
+        wd[k] = idx < nseg ? w : 0u;
+      }
       const uint32_t qa = idx < nseg ? op_qadv(wd[k]) : 0u, ta = idx < nseg ? op_tadv(wd[k]) : 0u,
                      la = idx < nseg ? op_ladv(wd[k]) : 0u;
       const uint32_t qi_ = wave_incl_scan(qa, lane), ti_ = wave_incl_scan(ta, lane), li_ = wave_incl_scan(la, lane);
@@ -1156,6 +1161,22 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       const int j = lane == 0 ? (int)sb - 1 : (int)(sb + nseg);
       w->opw[lane == 0 ? kOpHalo - 1 : kOpHalo + (int)nseg] = (j >= 0 && (uint32_t)j < n_ops) ? ops[j] : 0u;
     }
+    // ---- the segment's global reads, issued together before any is used (clamped indices, so
+    // no load sits in a branch): per op the query base and the cs query base of a '*' op, and the
+    // first 8 literal bytes of an event head (lits and qseq are readable PW_DEV_PAD bytes past
+    // their ends, and every query is followed by zero padding)
+    uint8_t qlit[2], qref[2];
+    uint32_t lw[2][3];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const int qp = d.offset + qs[k];
+      const int qc = qp < 0 ? 0 : (qp >= L ? (L > 0 ? L - 1 : 0) : qp);
+      qref[k] = R[rev ? (L > 0 ? L - 1 - qc : 0) : qc];
+      qlit[k] = A.lits[ls[k] + 1];
+      const uint32_t la = ls[k] >> 2;
+#pragma unroll
+      for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
+    }
     // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads
     uint64_t subm[2], hm[2];
     int bad_idx = INT_MAX;
@@ -1170,14 +1191,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       const bool prevsub = lane == 0 ? sm_prev != 0 : ((subm[k] >> (lane - 1)) & 1ull) != 0;
       sm_prev = (uint32_t)((subm[k] >> 63) & 1ull);
       hm[k] = __ballot(in && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub)));
-      bool bad = false;
-      uint8_t qch = 0, rch = 0;
       const int qp = d.offset + qs[k];
-      if (is_sub) {
-        qch = A.lits[ls[k] + 1];
-        rch = aligned_char_g(R, L, rev, tab, qp);
-        bad = qch != rch;
-      }
+      // aligned-strand query char at qp (refseq_rc for '-' records; 0 past the end)
+      const uint8_t rch = (unsigned)qp >= (unsigned)L ? (uint8_t)0 : (rev ? tab->comp[qref[k]] : qref[k]);
+      const uint8_t qch = qlit[k];
+      const bool bad = is_sub && qch != rch;
       const uint64_t bm = __ballot(bad);
       if (bm && bad_idx == INT_MAX) {
         const int fl = __builtin_ctzll(bm);
@@ -1238,8 +1256,8 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           // here, the last created one once the record is done (below)
           const bool first = !rev && kidx == 0, last = rev && kidx == 0;
           // the event's first 8 literal bytes
-          const uint32_t la = ls[k] >> 2, sh = ls[k] & 3u;
-          const uint32_t w0 = lits32[la], w1 = lits32[la + 1], w2 = lits32[la + 2];
+          const uint32_t sh = ls[k] & 3u;
+          const uint32_t w0 = lw[k][0], w1 = lw[k][1], w2 = lw[k][2];
           Hot hh;
           hh.qb = (uint32_t)(qb >> 4);
           hh.L = L;

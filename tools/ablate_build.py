@@ -18,6 +18,8 @@ PATCHES = {
     "nohead": [("      wr_num(o, r.tab, (uint32_t)(e.rloc + 1));\n", ""), ("      wr_num(o, r.tab, (uint32_t)(aap0 + 1));\n", "")],
     "nocod_sub": [("    if (typ == PW_OP_SUB) {\n      const int p0 = e.rloc - e.r_trloc;", "    if (false) {\n      const int p0 = e.rloc - e.r_trloc;")],
     "nocod_indel": [("      indel_impact(k, r, e, in.ns_pre);\n", "")],
+    "nocod_slow": [("    if (!indel_codons_fast(r, e, a, x, dl, mm, rr)) {", "    if (!indel_codons_fast(r, e, a, x, dl, mm, rr) && false) {")],
+    "nocod_long": [("  } else {  // long insertion: the reference loop as is", "  } else if (false) {  // long insertion: the reference loop as is")],
     "nogather": [("for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {",
                   "for (uint32_t cc = (uint32_t)lane * 16; cc < 0u; cc += kWave * 16) {")],
 }
