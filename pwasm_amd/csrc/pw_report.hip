@@ -1988,14 +1988,17 @@ __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W)
 }
 
 // ------------------------------------------------------------------ next-stop table
-// One 256-thread workgroup per query; tiles of 768 positions from the end, each thread owns
-// three consecutive positions (one per frame); per frame a suffix-min scan over the tile.
+// ns[p] = the first q >= p with q = p (mod 3) where codon Q[q, q+3) is a stop (kNoStop if none).
+// One 256-thread workgroup per query; tiles of 768 positions from the end.  Thread t owns the
+// three positions base + 3 * (255 - t) + f, so lanes in increasing order walk the tile
+// backwards: a DPP prefix-minimum over the lanes is the suffix minimum over positions, per frame
+// (positions 3j + f of a thread share the frame f + base mod 3); the four waves combine through
+// LDS, the tiles through a carry.
 __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, const uint64_t* qoff,
                                                          const int32_t* qlen, uint32_t nq, int32_t* ns) {
   __shared__ SmallTables tab;
-  __shared__ int32_t sm[3][256];
-  __shared__ int32_t carry[3];
-  const int t = threadIdx.x;
+  __shared__ int32_t wm[kWaves][3];
+  const int t = threadIdx.x, wv = t / kWave;
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, t, 256);
   __syncthreads();
@@ -2003,38 +2006,37 @@ __global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, co
     const uint8_t* R = qseq + qoff[qi];
     int32_t* out = ns + qoff[qi];
     const int L = qlen[qi];
-    if (t < 3) carry[t] = kNoStop;
-    __syncthreads();
+    int carry[3] = {kNoStop, kNoStop, kNoStop};
     const int ntile = (L + 767) / 768;
     for (int tile = ntile - 1; tile >= 0; tile--) {
-      const int base = tile * 768;
+      const int pb = tile * 768 + 3 * (255 - t);
+      // five bytes from pb (indices clamped to L: the query is followed by zero bytes)
+      uint8_t b[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) b[q] = R[pb + q < L ? pb + q : L];
+      int s[3];
 #pragma unroll
       for (int f = 0; f < 3; f++) {
-        const int p = base + 3 * t + f;
-        int32_t v = kNoStop;
-        if (p + 2 < L) {
-          if (translate(tp, R[p], R[p + 1], R[p + 2]) == '.') v = p;
-        }
-        sm[f][t] = v;
+        const int p = pb + f;
+        const int v = (p + 2 < L && translate(tp, b[f], b[f + 1], b[f + 2]) == '.') ? p : kNoStop;
+        s[f] = wave_min_incl(v);
+      }
+      if ((t & (kWave - 1)) == kWave - 1) {
+#pragma unroll
+        for (int f = 0; f < 3; f++) wm[wv][f] = s[f];
       }
       __syncthreads();
-      for (int dd = 1; dd < 256; dd <<= 1) {  // suffix min over t
-        int32_t v[3];
-#pragma unroll
-        for (int f = 0; f < 3; f++) v[f] = (t + dd < 256) ? sm[f][t + dd] : kNoStop;
-        __syncthreads();
-#pragma unroll
-        for (int f = 0; f < 3; f++) sm[f][t] = min(sm[f][t], v[f]);
-        __syncthreads();
-      }
+      // positions above this wave's: the waves before it in this tile, then the tiles above
 #pragma unroll
       for (int f = 0; f < 3; f++) {
-        const int p = base + 3 * t + f;
-        const int32_t v = min(sm[f][t], carry[f]);
-        if (p < L) out[p] = v;
+        int above = carry[f];
+        for (int w2 = 0; w2 < wv; w2++) above = min(above, wm[w2][f]);
+        const int p = pb + f;
+        if (p < L) out[p] = min(s[f], above);
       }
-      __syncthreads();
-      if (t < 3) carry[t] = min(carry[t], sm[t][0]);
+#pragma unroll
+      for (int f = 0; f < 3; f++)
+        for (int w2 = 0; w2 < kWaves; w2++) carry[f] = min(carry[f], wm[w2][f]);
       __syncthreads();
     }
   }

@@ -5,6 +5,7 @@
 #ifndef PW_WAVE_H
 #define PW_WAVE_H
 #include <hip/hip_runtime.h>
+#include <limits.h>
 #include <stdint.h>
 
 namespace pw {
@@ -26,6 +27,22 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t v) {
   return v;
 }
 __device__ __forceinline__ int wave_scan_incl(int v) { return (int)wave_scan_incl((uint32_t)v); }
+
+// inclusive prefix minimum over the 64 lanes (every lane active); lanes whose DPP source is
+// outside the row keep INT_MAX (the identity)
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_or_max(int v) {
+  return __builtin_amdgcn_update_dpp(INT_MAX, v, CTRL, ROW_MASK, 0xF, false);
+}
+__device__ __forceinline__ int wave_min_incl(int v) {
+  v = min(v, dpp_or_max<0x111>(v));
+  v = min(v, dpp_or_max<0x112>(v));
+  v = min(v, dpp_or_max<0x114>(v));
+  v = min(v, dpp_or_max<0x118>(v));
+  v = min(v, dpp_or_max<0x142, 0xA>(v));
+  v = min(v, dpp_or_max<0x143, 0xC>(v));
+  return v;
+}
 
 // value of lane 63 (wave-uniform)
 __device__ __forceinline__ uint32_t wave_last(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
