@@ -146,7 +146,9 @@ int pw_stop_table_build(const uint8_t* qseq, const uint64_t* qoff, const int32_t
  * seq[row_off[r] .. +row_len[r]) and the int16 gaps before each base (GASeq::ofs) at the same
  * indices; col0[r] = offset - minoffset (GapAssem.cpp:568); clip_l/clip_r are the clip lengths
  * already oriented by revcompl (GapAssem.cpp:557-564).  Rows are cut into 256-base chunks;
- * pw_msa_slots() assigns each row ceil(len/256)+1 slots (the last one is the row's end). */
+ * pw_msa_slots() assigns each row ceil(len/256)+1 slots (the last one is the row's end).
+ * seq / ofs of every row are readable up to the next multiple of 4 elements past its end (the
+ * stagers start rows 8-element aligned and zero-pad between them). */
 typedef struct pw_msa_args {
   const uint8_t* seq;       /* bases of all rows */
   const int16_t* ofs;       /* gaps before each base */

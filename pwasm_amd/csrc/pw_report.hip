@@ -56,8 +56,9 @@ constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
 constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
 constexpr int kQWin = 48;       // render_kernel: forward-query window per lane (bytes)
 constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dword reads at most 2-way)
-constexpr int kLine = 88;       // render_kernel: report lines up to this long are built in LDS (99.5 % at cfg2)
-constexpr int kLSlack = 44;     // ... + slack: a field block (<= 40 bytes) never needs a bounds check
+constexpr int kLine = 92;       // render_kernel: report lines up to this long are built in LDS (99.94 % at cfg2)
+constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
+                                // bases + tloc block of a 12-base S run), so none needs a bounds check
 constexpr int kLStride = kLine + kLSlack;  // 132 bytes = 33 dwords: per-lane byte stores conflict-free
 constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
@@ -375,7 +376,7 @@ struct LdsSink {
   }
 };
 // ClampSink: render_kernel's line buffer (kLine bytes + kLSlack).  Every field goes through a
-// block of at most 40 bytes written with a RawSink (no per-character checks): a block starting
+// block of at most 35 bytes written with a RawSink (no per-character checks): a block starting
 // at pos <= kLine ends inside the slack; once pos passes kLine the line is long (fixup_kernel
 // rewrites it) and the block is folded back onto the slack.
 struct ClampSink {
