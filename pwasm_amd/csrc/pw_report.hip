@@ -123,6 +123,14 @@ __device__ __forceinline__ void wave_sync() {
 typedef const PW_GLOBAL uint8_t* GU8;
 typedef PW_GLOBAL const v4u GV4;
 
+// Prefetched registers are first touched where they are consumed, one or two chunks later: an
+// empty asm that "rewrites" them there keeps the compiler from folding any use into the block
+// that issued the load.  Every prefetch load is unconditional (a clamped or dummy address when
+// the value is not needed): a load inside a branch costs an s_waitcnt vmcnt(0) at the join,
+// since the count of loads issued after it differs between the paths.
+__device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
 // ------------------------------------------------------------------ record context
 struct Rec {
   const uint32_t* ops;      // this record's ops (global)
@@ -1107,6 +1115,30 @@ __device__ __forceinline__ void rec_pre_ready(const pw_report_args& A, RecPre& p
   if ((uint32_t)(lane + 64) >= p.d.n_ops) p.w1 = 0u;
 }
 
+// A descriptor loaded two records ahead stays in VGPRs (a uniform load is otherwise moved to
+// SGPRs at once, which waits for it — and, vmcnt being in order, for every store before it)
+struct DescRaw {
+  v4u a, b;
+};
+__device__ __forceinline__ DescRaw load_desc(const pw_report_args& A, uint32_t i) {
+  const v4u* p = reinterpret_cast<const v4u*>(A.desc + i);
+  DescRaw r;
+  r.a = p[0];
+  r.b = p[1];
+  return r;
+}
+__device__ __forceinline__ pw_aln_desc unpack_desc(const DescRaw& r) {
+  pw_aln_desc d;
+  d.op_begin = __builtin_amdgcn_readfirstlane(r.a.x);
+  d.n_ops = __builtin_amdgcn_readfirstlane(r.a.y);
+  d.lit_begin = __builtin_amdgcn_readfirstlane(r.a.z);
+  d.ref = __builtin_amdgcn_readfirstlane(r.a.w);
+  d.offset = (int32_t)__builtin_amdgcn_readfirstlane(r.b.x);
+  d.t_len = (int32_t)__builtin_amdgcn_readfirstlane(r.b.y);
+  d.ev_begin = (uint64_t)__builtin_amdgcn_readfirstlane(r.b.z) | (uint64_t)__builtin_amdgcn_readfirstlane(r.b.w) << 32;
+  return d;
+}
+
 __device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
                                              LDS IndexWave* w, uint32_t ai, int lane, const RecPre& pre) {
   const pw_aln_desc d = pre.d;
@@ -1128,7 +1160,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   int qc = 0, tc = 0;
   uint32_t lc = d.lit_begin;
   bool prev_sub = false;
-  uint32_t ev = 0;
+  uint32_t ev = 0, ev_last_seg = 0;  // events created; by the last segment processed
   int err = layout_ok ? PW_REC_OK : PW_REC_LAYOUT, err_a = 0, err_b = 0, err_c = 0;
 
   for (uint32_t sb = 0; layout_ok && sb < n_ops; sb += kSegOps) {
@@ -1143,8 +1175,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       const uint32_t idx = 64 * k + lane;
       if (sb == 0) {
         wd[k] = k == 0 ? pre.w0 : pre.w1;
-      } else {  // (clamped index: an unconditional load)
-        const uint32_t w = ops[idx < nseg ? sb + idx : sb];
+      } else {  // (clamped index: an unconditional load, waited for inside this branch: a wait at
+                // the join would also hold the first segment for the next record's prefetch)
+        uint32_t w = ops[idx < nseg ? sb + idx : sb];
+        asm volatile("" : "+v"(w));
         wd[k] = idx < nseg ? w : 0u;
       }
       const uint32_t qa = idx < nseg ? op_qadv(wd[k]) : 0u, ta = idx < nseg ? op_tadv(wd[k]) : 0u,
@@ -1158,10 +1192,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       ltot += wave_last(li_);
       w->opw[kOpHalo + idx] = wd[k];
     }
-    if (lane < 2) {  // halo: the op words just before / after the segment (tctx_fast's neighbours)
-      const int j = lane == 0 ? (int)sb - 1 : (int)(sb + nseg);
-      w->opw[lane == 0 ? kOpHalo - 1 : kOpHalo + (int)nseg] = (j >= 0 && (uint32_t)j < n_ops) ? ops[j] : 0u;
-    }
+    // halo: the op words just before / after the segment (tctx_fast's neighbours; lanes 0 and 1),
+    // loaded with the segment's other reads below and stored once they are in
+    const int hj = lane == 0 ? (int)sb - 1 : (int)(sb + nseg);
+    const bool hok = lane < 2 && hj >= 0 && (uint32_t)hj < n_ops;
+    uint32_t halo = ops[hok ? (uint32_t)hj : sb];
     // ---- the segment's global reads, issued together before any is used (clamped indices, so
     // no load sits in a branch): per op the query base and the cs query base of a '*' op, and the
     // first 8 literal bytes of an event head (lits and qseq are readable PW_DEV_PAD bytes past
@@ -1206,14 +1241,26 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
         err_c = __shfl((int)rch, fl, kWave);
       }
     }
+    if (lane < 2) w->opw[lane == 0 ? kOpHalo - 1 : kOpHalo + (int)nseg] = hok ? halo : 0u;
     wave_sync();
     if (bad_idx != INT_MAX) {
       err = PW_REC_MISMATCH;
       break;
     }
+    // every event head's first 8 literal bytes, for both halves now: a load first consumed after
+    // the first half's Hot stores would make the compiler wait for those stores too (vmcnt(0))
+    uint32_t hl0[2], hl1[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const uint32_t sh = ls[k] & 3u;
+      hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
+      hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
+      asm volatile("" : "+v"(hl0[k]), "+v"(hl1[k]));  // (kept here, not sunk into the store branch)
+    }
     // ---- events of this segment: creation index, S-run length, target context
     const uint32_t n0 = (uint32_t)__popcll(hm[0]);
     const uint32_t nev = n0 + (uint32_t)__popcll(hm[1]);
+    const bool fin = sb + (uint32_t)kSegOps >= n_ops;  // the record's last segment
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -1253,12 +1300,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
         const uint32_t kidx = ev + (k == 0 ? (uint32_t)__popcll(hm[0] & lt) : n0 + (uint32_t)__popcll(hm[1] & lt));
         if (kidx < nmax) {
           s = rev ? evb + nmax - 1 - kidx : evb + kidx;
-          // first / last line of the record in output order: the first created event is flagged
-          // here, the last created one once the record is done (below)
-          const bool first = !rev && kidx == 0, last = rev && kidx == 0;
-          // the event's first 8 literal bytes
-          const uint32_t sh = ls[k] & 3u;
-          const uint32_t w0 = lw[k][0], w1 = lw[k][1], w2 = lw[k][2];
+          // first / last line of the record in output order: the first created event, and the
+          // last created one when this is the record's last segment (else flagged once the
+          // record is done, below)
+          const bool lastc = fin && kidx + 1 == ev + nev;
+          const bool first = rev ? lastc : kidx == 0, last = rev ? kidx == 0 : lastc;
           Hot hh;
           hh.qb = (uint32_t)(qb >> 4);
           hh.L = L;
@@ -1266,10 +1312,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           hh.tloc = rev ? T - ts[k] : ts[k];
           hh.ls = ls[k];
           hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, (d.ref & PW_REF_ACGT) != 0, n);
-          hh.l0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
-          hh.l1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+          hh.l0 = hl0[k];
+          hh.l1 = hl1[k];
           W.hot[s] = hh;
-          if (kidx == 0 || n >= kNBig) {  // only the first / last line and saturated lengths read it
+          if (kidx == 0 || lastc || n >= kNBig) {  // only the first / last line and saturated lengths read it
             Cold cd;
             cd.ai = ai;
             cd.j = j;
@@ -1291,20 +1337,24 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       }
     }
     ev += nev;
+    ev_last_seg = nev;
     prev_sub = (w->opw[kOpHalo + nseg - 1] >> 30) == PW_OP_SUB;
     qc += (int)qtot;
     tc += (int)ttot;
     lc += ltot;
     wave_sync();
   }
-  if (ev > nmax) {  // host event bound violated (cannot happen: every head is a counted op)
+  const bool ev_over = ev > nmax;
+  if (ev_over) {  // host event bound violated (cannot happen: every head is a counted op)
     err = PW_REC_OVERFLOW;
     ev = nmax;
   }
   // empty slots: merged '*' runs, or everything after a failure
   const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;  // (none if !layout_ok)
   for (uint64_t s = h0 + lane; s < h1; s += kWave) W.hot[s].fn = kNoEv;
-  if (lane == 0 && ev > 0 && err == PW_REC_OK) {
+  // the last created event was flagged when written unless the last segment had no event head
+  // (or the event bound was violated): then flag it now, after this wave's store of its record
+  if (lane == 0 && ev > 0 && err == PW_REC_OK && (ev_last_seg == 0 || ev_over)) {
     const uint64_t s_last = rev ? evb + nmax - ev : evb + ev - 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's store of that record first
     atomicOr(&W.hot[s_last].fn, rev ? 1u << 27 : 1u << 26);
@@ -1342,14 +1392,21 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
     const uint32_t nm1 = A.n_alns - 1;
     RecPre cur;
     rec_pre(A, ai, A.desc[ai], lane, cur);
-    pw_aln_desc dn = A.desc[ai + stride < A.n_alns ? ai + stride : nm1];
+    DescRaw dn = load_desc(A, ai + stride < A.n_alns ? ai + stride : nm1);
+    rec_pre_ready(A, cur, lane);
+    pin(dn.a);
+    pin(dn.b);
     for (; ai < A.n_alns; ai += stride) {
       const uint32_t an = ai + stride;
       RecPre nxt;
-      rec_pre(A, an < A.n_alns ? an : nm1, dn, lane, nxt);
-      const pw_aln_desc dnn = A.desc[an + stride < A.n_alns ? an + stride : nm1];
-      rec_pre_ready(A, cur, lane);
+      rec_pre(A, an < A.n_alns ? an : nm1, unpack_desc(dn), lane, nxt);
+      DescRaw dnn = load_desc(A, an + stride < A.n_alns ? an + stride : nm1);
       index_record(A, W, tp, w, ai, lane, cur);
+      // (first consumed here, where the record's segment loads have already waited for them:
+      // consumed at the top of the next iteration, the wait would also cover this record's stores)
+      rec_pre_ready(A, nxt, lane);
+      pin(dnn.a);
+      pin(dnn.b);
       cur = nxt;
       dn = dnn;
     }
@@ -1380,13 +1437,6 @@ __device__ __noinline__ uint32_t rec_of_slot(const pw_report_args& A, uint64_t s
   return lo;
 }
 
-// Prefetched registers are first touched where they are consumed, one or two chunks later: an
-// empty asm that "rewrites" them there keeps the compiler from folding any use into the block
-// that issued the load.  Every prefetch load is unconditional (a clamped or dummy address when
-// the value is not needed): a load inside a branch costs an s_waitcnt vmcnt(0) at the join,
-// since the count of loads issued after it differs between the paths.
-__device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
 struct HotRaw {
   v4u a, b;
