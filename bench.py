@@ -2,8 +2,8 @@
 """bench.py — pafreport hot path on MI355X: cs-events classified per second.
 
 A "step" = one pass of the hot path over one batch already resident in HBM: the next-stop
-table build (pw_stop_table_build) + the fused decode/classify/codon/render kernel
-(pw_report_events) over every record of the batch.  At N=1 the batch is BASELINE.json
+table build (pw_stop_table_build, on a side stream overlapping the decode kernels) + the
+decode/classify/codon/render kernels (pw_report_events_after) over every record of the batch.  At N=1 the batch is BASELINE.json
 configs[1] (cfg2: 100k synthetic minimap2-style records, 1,000 CDS of 1-5 kb, ~1% ONT-style
 errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard (different
 seed = different target genomes; weak scaling, no data-path collective); the timed region is
@@ -117,18 +117,29 @@ def main():
         gtab = (mgpu, rows, gt, torch.zeros(max(pad, 16), dtype=torch.uint8, device=dev_name),
                 torch.empty(world * max(pad, 16), dtype=torch.uint8, device=dev_name))
 
+    # the next-stop table is built on a side stream, overlapping the decode kernels (index, tctx);
+    # the pass waits for it before render (pw_report_events_after), the side stream waits for the
+    # previous pass before rebuilding it
+    side = torch.cuda.Stream()
+    ns_ready, pass_done = torch.cuda.Event(), torch.cuda.Event()
+
     def step(ev=None):
+        ready = None
         if not v.skip_codan:
+            side.wait_event(pass_done)
             rc = pw.lib().pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
-                                              int(v.n_queries), dev["next_stop"].data_ptr(), sp)
+                                              int(v.n_queries), dev["next_stop"].data_ptr(), side.cuda_stream)
             assert rc == 0
+            ns_ready.record(side)
+            ready = ns_ready.cuda_event
         a = pw.report_args(batch, dev)
         if ev is not None:
             ev[0].record(stream)
-        rc = pw.lib().pw_report_events(pw.ctypes.byref(a), sp)
+        rc = pw.lib().pw_report_events_after(pw.ctypes.byref(a), sp, ready)
         assert rc == 0
         if ev is not None:
             ev[1].record(stream)
+        pass_done.record(stream)
         if gtab is not None:
             mg, rows, gt, padded, gathered = gtab
             mg.launch_genome_table(dev, rows, gt, sp)

@@ -135,6 +135,13 @@ uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_alns);
  * descriptors, then wavefronts of 64 consecutive events render the report lines. */
 int pw_report_events(const pw_report_args* args, void* stream);
 
+/* As pw_report_events, but next_stop may still be being built on another stream: the pass waits
+ * for the HIP event next_stop_ready (a hipEvent_t recorded after pw_stop_table_build there; NULL =
+ * already complete in stream order) only before its first kernel that reads next_stop, so the table
+ * build overlaps the decode kernels.  The caller keeps the table alive and unmodified until the pass
+ * completes. */
+int pw_report_events_after(const pw_report_args* args, void* stream, void* next_stop_ready);
+
 /* Per-query stop-codon lookahead used by the codon pass (replaces the forward scan of
  * predictImpact, pafreport.cpp:854-870): next_stop[off+j] = smallest k >= j, k = j mod 3,
  * k+2 < len, translateCodon(q+k) == '.', else INT32_MAX. */

@@ -108,6 +108,7 @@ class GaRow(ctypes.Structure):
 # every function declared in include/pwasm_amd.h (tests check the export table against it)
 _SIGS = {
     "pw_report_events": (ctypes.c_int, [ctypes.POINTER(ReportArgs), ctypes.c_void_p]),
+    "pw_report_events_after": (ctypes.c_int, [ctypes.POINTER(ReportArgs), ctypes.c_void_p, ctypes.c_void_p]),
     "pw_stop_table_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "pw_msa_slots": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),

@@ -1483,13 +1483,17 @@ __device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& 
   const uint32_t typ = h.fn >> 30;
   const bool rev = (h.fn >> 29) & 1u;
   int n = (int)(h.fn & kNBig);
-  const uint64_t se = ev ? s : 0;  // (empty slots read slot 0's records: valid memory, unused)
+  // the tx record only for a pre-rendered target context, the Cold record only for a record's first
+  // / last line: other lanes read slot 0's (valid memory, an L2 hit, unused) — an unconditional
+  // load either way, without the HBM traffic of records nobody uses
+  const uint64_t se_tx = (ev && !((h.fn >> 28) & 1u)) ? s : 0;
+  const uint64_t se_cold = (ev && (h.fn & (3u << 26))) ? s : 0;
   {
-    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * se);
+    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * se_tx);
     p.t0 = tp4[0];
     p.t1 = tp4[1];
   }
-  p.ai = W.cold[se].ai;
+  p.ai = W.cold[se_cold].ai;
   if (ev && (uint32_t)n == kNBig) {  // saturated length: from the op stream (rare; dependent loads)
     const Cold cd = W.cold[s];
     const pw_aln_desc d = A.desc[cd.ai];
@@ -2132,7 +2136,11 @@ extern "C" uint64_t pw_report_text_bytes(uint64_t n_ev_slots, uint64_t text_boun
   return pw_report_page_count(n_ev_slots) * PW_PAGE_BYTES + pw::align_up(text_bound, 16) + 16;
 }
 
+extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, void* next_stop_ready);
 extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
+  return pw_report_events_after(args, stream, nullptr);
+}
+extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, void* next_stop_ready) {
   if (!args || !args->desc || !args->ops || !args->qseq || !args->qoff || !args->qlen || !args->results ||
       (!args->text && args->text_total))
     return PW_E_ARG;
@@ -2164,6 +2172,8 @@ extern "C" int pw_report_events(const pw_report_args* args, void* stream) {
     hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
     if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;
+    // (render is the first kernel that reads next_stop)
+    if (next_stop_ready && hipStreamWaitEvent(st, (hipEvent_t)next_stop_ready, 0) != hipSuccess) return PW_E_HIP;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);
   }

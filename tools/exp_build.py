@@ -31,12 +31,65 @@ def patched(s, pairs):
     return s
 
 
+PROBE = "{ const uint64_t t_ = __builtin_amdgcn_s_memtime(); pa.t[%d] += t_ - pa.last; pa.last = t_; }"
+PROF_PATCH = [
+    ("struct ClampSink {\n", """struct ProfAcc {
+  uint64_t t[16];
+  uint64_t last;
+};
+__device__ unsigned long long g_prof[16];
+struct ClampSink {
+  ProfAcc* pa;
+  __device__ __forceinline__ void probe(int i) {
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();
+    pa->t[i] += t_ - pa->last;
+    pa->last = t_;
+  }
+"""),
+    ("typedef ClampSink LineSink;\n", """typedef ClampSink LineSink;
+template <class S>
+__device__ __forceinline__ void sink_probe(S&, int) {}
+__device__ __forceinline__ void sink_probe(ClampSink& k, int i) { k.probe(i); }
+"""),
+    ("  // ---- bases field (\"[n]\" past MAX_EVLEN", "  sink_probe(k, 1);\n  // ---- bases field (\"[n]\" past MAX_EVLEN"),
+    ("  // ---- \"E\\trloc\\taapos(aa)\\t\"", "  sink_probe(k, 11);\n  // ---- \"E\\trloc\\taapos(aa)\\t\""),
+    ("      indel_impact(k, r, e, in.ns_pre);", "      sink_probe(k, 13);\n      indel_impact(k, r, e, in.ns_pre);"),
+    ("  if (stop_i >= 0) {", "  sink_probe(k, 12);\n  if (stop_i >= 0) {"),
+    ("  // ---- target context (setTContext", "  sink_probe(k, 2);\n  // ---- target context (setTContext"),
+    ("  k.put('\\t');\n  // ---- query context", "  k.put('\\t');\n  sink_probe(k, 3);\n  // ---- query context"),
+    ("  // ---- codon consequence (predictImpact", "  sink_probe(k, 4);\n  // ---- codon consequence (predictImpact"),
+    ("  k.put('\\n');\n  return modseq_err;", "  sink_probe(k, 5);\n  k.put('\\n');\n  return modseq_err;"),
+    ("  for (; c < W.n_chunks; c += nw) {\n", "  ProfAcc pa = {};\n  pa.last = __builtin_amdgcn_s_memtime();\n  for (; c < W.n_chunks; c += nw) {\n    " + (PROBE % 10) + "\n"),
+    ("      LineSink k;\n", "      LineSink k;\n      k.pa = &pa;\n"),
+    ("      const int merr = emit_event(k, r, in, skip, rel);", "      " + (PROBE % 0) + "\n      const int merr = emit_event(k, r, in, skip, rel);"),
+    ("    render_pre(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);\n",
+     "    " + (PROBE % 6) + "\n    render_pre(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);\n    " + (PROBE % 7) + "\n"),
+    ("    if (ok && B > 0) {\n", "    " + (PROBE % 8) + "\n    if (ok && B > 0) {\n"),
+    ("      for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {",
+     "      " + (PROBE % 9) + "\n      for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {"),
+    ("    wave_sync();\n  }\n}\n\n// ------------------------------------------------------------------ tctx_kernel",
+     "    wave_sync();\n  }\n  if (lane == 0)\n    for (int i = 0; i < 16; i++) atomicAdd(&g_prof[i], (unsigned long long)pa.t[i]);\n}\n\n// ------------------------------------------------------------------ tctx_kernel"),
+]
+PROF_HOST = """
+extern "C" int pw_exp_prof(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pw::g_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(pw::g_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+"""
+
+
+def profiled(s):
+    return patched(s, PROF_PATCH) + PROF_HOST
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
     return {
         "head": head,
         "cur": cur,
+        "prof": lambda: profiled(cur),
     }
 
 
@@ -48,7 +101,8 @@ def main(names):
         d = os.path.join(OUT, name)
         os.makedirs(os.path.join(d, "lib"), exist_ok=True)
         hip = os.path.join(d, "pw_report.hip")
-        open(hip, "w").write(vs[name])
+        v = vs[name]
+        open(hip, "w").write(v() if callable(v) else v)
         o = os.path.join(d, "pw_report.o")
         inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
