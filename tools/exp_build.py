@@ -83,6 +83,25 @@ def profiled(s):
     return patched(s, PROF_PATCH) + PROF_HOST
 
 
+def tc_lit(nbytes, back):
+    """tctx_kernel with an LDS window of nbytes literal bytes from (ls - back) & ~3"""
+    return [
+        ("  uint8_t qw[kTcQ];\n  uint8_t out[kTx + 4];", "  uint8_t qw[kTcQ];\n  uint8_t lw[%d];\n  uint8_t out[kTx + 4];" % nbytes),
+        ("        r.lw = nullptr;\n        r.l_lo = 0;\n        r.l_n = 0;\n        const int j = (int)p0.y;",
+         "        const uint32_t lw0 = (h.ls >= %du ? h.ls - %du : 0u) & ~3u;\n"
+         "        const PW_GLOBAL uint32_t* l32 = reinterpret_cast<const PW_GLOBAL uint32_t*>((GU8)(A.lits) + lw0);\n"
+         "        uint32_t lv[%d];\n#pragma unroll\n        for (int q = 0; q < %d; q++) lv[q] = l32[q];\n"
+         "        const int j = (int)p0.y;" % (back, back, nbytes // 4, nbytes // 4)),
+        ("        for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];\n",
+         "        for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];\n"
+         "#pragma unroll\n        for (int q = 0; q < %d; q++) reinterpret_cast<LDS uint32_t*>(me->lw)[q] = lv[q];\n"
+         "        r.lw = me->lw;\n        r.l_lo = lw0;\n        r.l_n = %du;\n" % (nbytes // 4, nbytes)),
+    ]
+
+
+TC_OPS8 = [("constexpr int kTcOps = 12;", "constexpr int kTcOps = 8;")]
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
@@ -90,6 +109,9 @@ def variants():
         "head": head,
         "cur": cur,
         "prof": lambda: profiled(cur),
+        "tc_lit32": lambda: patched(cur, tc_lit(32, 12)),
+        "tc_lit16_ops8": lambda: patched(cur, tc_lit(16, 8) + TC_OPS8),
+        "tc_ops8": lambda: patched(cur, TC_OPS8),
     }
 
 
