@@ -2164,7 +2164,7 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   if (W.n_chunks && hipMemsetAsync(W.sflag, 0, W.n_chunks * pw::kWave, st) != hipSuccess) return PW_E_HIP;
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
-  if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;
+  if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;  // (two rounds at 5 waves/SIMD; sweep: 16 -> 10 per CU saved ~10 us of index + tctx)
   hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
     uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;

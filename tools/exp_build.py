@@ -109,6 +109,10 @@ def variants():
         "head": head,
         "cur": cur,
         "prof": lambda: profiled(cur),
+        "ig5": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 5u) ig = (uint64_t)ncu * 5u;")]),
+        "ig10": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;")]),
+        "ig64": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 64u) ig = (uint64_t)ncu * 64u;")]),
+        "tg8": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 16u) tg = (uint64_t)ncu * 16u;")]),
         "tc_lit32": lambda: patched(cur, tc_lit(32, 12)),
         "tc_lit16_ops8": lambda: patched(cur, tc_lit(16, 8) + TC_OPS8),
         "tc_ops8": lambda: patched(cur, TC_OPS8),
