@@ -159,6 +159,36 @@ def test_batch_api_on_torch_stream(built, tmp_path):
     assert n_events == want.count(b"\n") - want.count(b">")
 
 
+def test_report_events_after_side_stream(built, tmp_path):
+    """pw_report_events_after: the next-stop table built on another stream (behind a long
+    dependency there), the pass waiting for its event before render — same report as the oracle,
+    twice in a row on the same buffers (the side stream waits for the previous pass)."""
+    import torch
+    fa, paf = synth_paf(tmp_path, 2, seed=11, scale=0.05)
+    b = pw.HostBatch(fa, paf, pw.FLAG_G | pw.FLAG_C)
+    v = b.view
+    dev = pw.stage_batch(b, "cuda:0")
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    ready, done = torch.cuda.Event(), torch.cuda.Event()
+    L = pw.lib()
+    _, want, _ = run([ORACLE, "-G", "-C", "-r", fa, paf])
+    for it in range(2):
+        dev["next_stop"].fill_(-7)  # stale table on the main stream: the side stream must come after it
+        done.record(main)
+        side.wait_event(done)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(2000000)  # keep the table build late on the side stream
+        assert L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                     int(v.n_queries), dev["next_stop"].data_ptr(), side.cuda_stream) == 0
+        ready.record(side)
+        a = pw.report_args(b, dev)
+        assert L.pw_report_events_after(pw.ctypes.byref(a), main.cuda_stream, ready.cuda_event) == 0
+        torch.cuda.synchronize()
+        outp = str(tmp_path / f"after{it}.txt")
+        assert b.write_report_from(dev, outp) == 0
+        assert open(outp, "rb").read() == want
+
+
 # ---------------------------------------------------------------- GapAssem consensus
 def ga_same(layout, tmp_path, extra=(), writers=True):
     """gapassem_consensus (GapAssem C++ API on the GPU) against the oracle: exit code, stderr, the
