@@ -296,6 +296,38 @@ def finish_rows(lay: Layout, rows, base: dict, alpos, cons: bytes, mincol: int, 
     return out
 
 
+def gather_rows(fin: dict, group, device):
+    """finish_rows' output of every rank, merged on every rank.  The per-row fields (messages,
+    offsets, clips: small) go through all_gather_object; the edited gap arrays (all rows with
+    removeConsGaps: ~2 bytes per base) as one byte tensor per rank through all_gather — device
+    tensors under RCCL (int16 is not an RCCL type: the bytes travel), host tensors under gloo."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rows = sorted(fin)
+    meta = {r: fin[r][:6] + (len(fin[r][6]),) for r in rows}
+    flat = (np.concatenate([np.asarray(fin[r][6], dtype="<i2") for r in rows]) if rows
+            else np.zeros(0, dtype="<i2")).view(np.uint8)
+    metas = [None] * world
+    dist.all_gather_object(metas, (meta, int(flat.size)), group=group)
+    nmax = max(1, max(n for _, n in metas))
+    dev = device if dist.get_backend(group) == "nccl" else "cpu"
+    buf = torch.zeros(nmax, dtype=torch.uint8, device=dev)
+    if flat.size:
+        buf[: flat.size] = torch.from_numpy(flat).to(dev)
+    outs = [torch.empty(nmax, dtype=torch.uint8, device=dev) for _ in range(world)]
+    dist.all_gather(outs, buf, group=group)
+    merged = {}
+    for (meta_p, n), t in zip(metas, outs):
+        b = t[:n].cpu().numpy().view("<i2") if n else np.zeros(0, dtype="<i2")
+        o = 0
+        for r in sorted(meta_p):
+            m = meta_p[r]
+            merged[r] = m[:6] + (b[o: o + m[6]].astype(np.int16),)
+            o += m[6]
+    return merged
+
+
 def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=None, refine_clipping: bool = True):
     """refineMSA's consensus with rows sharded over the ranks of `group` (torch.distributed; a
     single process when it is not initialised).  Returns (exit_code, stderr_text, pwc_bytes) on
@@ -368,9 +400,7 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
     fin = finish_rows(lay, [r for r in own if remove_gaps or (refine_clipping and (lay.clp5[r] or lay.clp3[r]))],
                       base, alpos, cons_s, mincol, remove_gaps, refine_clipping)
     if world > 1:
-        parts = [None] * world
-        dist.all_gather_object(parts, fin, group=group)
-        fin = {k: v for p in parts for k, v in p.items()}
+        fin = gather_rows(fin, group, counts.device)
     if rank != 0:
         return (1 if any(v[1] for v in fin.values()) else 0), "", None
     for r in range(hdr.n):  # the per-row messages in row order, up to a row that GErrors
