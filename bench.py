@@ -262,7 +262,8 @@ def main():
                          "alg_formula": "SURVEY 8(d): 16*n_alns + 4*n_ops + n_lits + 32*E + 13*sum(L unique queries)",
                          "achieved_text_variant": round(alg_text / (kern_ms * 1e-3) / 1e9, 2),
                          "alg_bytes_text_variant": alg_text,
-                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd")},
+                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd"),
+                         "issue_busy": issue_busy(prof, ("pw::render_kernel", "pw::index_kernel", "pw::tctx_kernel"))},
             "cpu_baseline": cpu,
             "e2e": e2e,
         }
@@ -403,6 +404,23 @@ def host_threads():
         if os.environ.get(k, "").isdigit() and int(os.environ[k]) > 0:
             return int(os.environ[k])
     return max(1, min(len(os.sched_getaffinity(0)), 16))
+
+
+def issue_busy(prof, kernels, n_cu=256, n_xcd=8, simd_per_cu=4):
+    """What bounds the report kernels instead of HBM, from the profile's PMC counters: the share of
+    the kernel's cycles the SIMDs spend issuing VALU (a wave64 VALU instruction occupies a 16-lane
+    SIMD for 4 cycles) and the LDS is busy (SQ_LDS_IDX_ACTIVE, bank-conflict cycles included).
+    GRBM_GUI_ACTIVE is summed over the XCDs."""
+    pmc = prof.get("pmc_per_launch") or {}
+    out = {}
+    for k in kernels:
+        c = pmc.get(k)
+        if not c or not c.get("GRBM_GUI_ACTIVE"):
+            continue
+        cyc = c["GRBM_GUI_ACTIVE"] / n_xcd
+        out[k] = {"valu_busy": round(4 * c.get("SQ_INSTS_VALU", 0) / (n_cu * simd_per_cu * cyc), 3),
+                  "lds_busy": round(c.get("SQ_LDS_IDX_ACTIVE", 0) / (n_cu * cyc), 3)}
+    return out or None
 
 
 def latest_profile(config):
