@@ -9,7 +9,7 @@ SRC_DIR  := pwasm_amd/csrc
 OBJ_DIR  := pwasm_amd/build
 LIB      := pwasm_amd/lib/libpwasm_amd.so
 CLI      := pwasm_amd/bin/pafreport
-OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o $(OBJ_DIR)/pw_ga_api.o $(OBJ_DIR)/pw_msa_comm.o
+OBJS     := $(OBJ_DIR)/pw_report.o $(OBJ_DIR)/pw_host.o $(OBJ_DIR)/pw_msa.o $(OBJ_DIR)/pw_gapassem.o $(OBJ_DIR)/pw_msa_layout.o $(OBJ_DIR)/pw_ga_api.o $(OBJ_DIR)/pw_msa_comm.o $(OBJ_DIR)/pw_pack.o
 GA_CLI   := pwasm_amd/bin/gapassem_consensus
 
 all: $(LIB) $(CLI) $(GA_CLI) oracle synth

@@ -204,7 +204,7 @@ def main():
             prof = json.load(open(args.traffic_json))
         traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
         flags_cli = ["-G", "-C"] if flags else []
-        parity, cpu, e2e = None, None, None
+        parity, cpu, e2e, gpack = None, None, None, None
         if not args.no_parity and world == 1 and v.n_alns <= 200000:
             # the benchmarked batch itself, copied back once (outside the timed region) and
             # diffed byte for byte against the oracle on the same input
@@ -230,6 +230,7 @@ def main():
                           f"{os.path.getsize(paf)} B in, {os.path.getsize(want)} B out)"}
             if not cli_ok:
                 parity = "FAIL"
+            gpack = gpu_pack_check(pw, paf)
         if cpu is None and not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(flags_cli, fa, paf, args.cpu_sample, tmp)
         out = {
@@ -266,6 +267,7 @@ def main():
                          "issue_busy": issue_busy(prof, ("pw::render_kernel", "pw::index_kernel", "pw::tctx_kernel"))},
             "cpu_baseline": cpu,
             "e2e": e2e,
+            "gpu_pack": gpack,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -404,6 +406,61 @@ def host_threads():
         if os.environ.get(k, "").isdigit() and int(os.environ[k]) > 0:
             return int(os.environ[k])
     return max(1, min(len(os.sched_getaffinity(0)), 16))
+
+
+def gpu_pack_check(pw, paf, reps=10):
+    """every cs string of the benchmarked PAF packed on the GPU (pw_pack_cs_batch,
+    inputs resident, HIP events over `reps` launches) and compared record by record with the host
+    packer pw_pack_cs (op words, literal bytes, totals)."""
+    import numpy as np
+    import torch
+    cs, offs, qls = [], [], []
+    for line in open(paf, "rb"):
+        f = line.rstrip(b"\r\n").split(b"\t")
+        if len(f) < 12 or line.startswith(b"#"):
+            continue
+        c = next((x[5:] for x in f[12:] if x.startswith(b"cs:Z:")), None)
+        if c is None:
+            continue
+        ql, qs, qe = int(f[1]), int(f[2]), int(f[3])
+        cs.append(c)
+        offs.append(qs if f[4] == b"+" else ql - qe)
+        qls.append(ql)
+    ops, lits, off, recs = pw.pack_cs_gpu(cs, offs, qls)
+    bad = 0
+    for i in range(len(cs)):
+        rc, hops, hlits, tot, _ = pw.pack_cs(cs[i].decode("latin-1"), offs[i], qls[i])
+        g, b = recs[i], int(off[i])
+        if g["flags"] & pw.PACK_HOST:
+            bad += rc == 0
+            continue
+        same = (rc == 0 and list(ops[b: b + g["n_ops"]]) == hops and bytes(lits[b: b + g["n_lits"]]) == hlits
+                and int(g["n_events_max"]) == tot.n_events_max and int(g["t_total"]) == tot.t_total)
+        bad += not same
+    # timing on device-resident inputs
+    n = len(cs)
+    o = np.zeros(n + 1, dtype=np.uint64)
+    o[1:] = np.cumsum([len(c) for c in cs], dtype=np.uint64)
+    t = lambda a: torch.from_numpy(np.array(a, copy=True)).cuda()
+    d_text = t(np.frombuffer(b"".join(cs) + b"\0" * 16, dtype=np.uint8))
+    d_off, d_o, d_q = t(o.view(np.int64)), t(np.asarray(offs, dtype=np.int32)), t(np.asarray(qls, dtype=np.int32))
+    d_ops = torch.empty(int(o[-1]) + 16, dtype=torch.int32, device="cuda")
+    d_lits = torch.empty(int(o[-1]) + 16, dtype=torch.uint8, device="cuda")
+    d_rec = torch.empty(n * pw.CS_REC.itemsize, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    call = lambda: pw.lib().pw_pack_cs_batch(d_text.data_ptr(), d_off.data_ptr(), d_o.data_ptr(), d_q.data_ptr(), n,
+                                             d_ops.data_ptr(), d_lits.data_ptr(), d_rec.data_ptr(), st.cuda_stream)
+    call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        call()
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1000.0 / reps
+    return {"records": n, "cs_bytes": int(o[-1]), "us_per_batch": round(us, 1),
+            "cs_GB_per_s": round(int(o[-1]) / us / 1e3, 1), "host_fallbacks": int((recs["flags"] & pw.PACK_HOST != 0).sum()),
+            "parity": "ok" if bad == 0 else f"FAIL ({bad} records)"}
 
 
 def issue_busy(prof, kernels, n_cu=256, n_xcd=8, simd_per_cu=4):

@@ -278,6 +278,25 @@ typedef struct pw_cs_totals {
 int pw_pack_cs(const char* cs, int32_t offset, int32_t qlen, uint32_t* ops, size_t ops_cap, uint8_t* lits,
                size_t lits_cap, pw_cs_totals* totals, int32_t* err_pos);
 
+/* The same packing for a whole batch on the GPU (pw_pack.hip): record i's cs
+ * field is cs_text[cs_off[i], cs_off[i+1]) (device arrays; offset / qlen as for pw_pack_cs).  Its
+ * op words go to ops[cs_off[i] ..] and its literal bytes to lits[cs_off[i] ..] (a record never
+ * has more ops or literal bytes than cs characters, so the field offsets are a valid layout),
+ * its totals to out[i].  A record that is not well-formed cs — or breaks a bounds check, or holds
+ * one op longer than 256 characters — gets PW_PACK_HOST and nothing else is defined for it: pack
+ * it with pw_pack_cs, which gives the reference's error.  PW_PACK_ACGT: every literal byte is
+ * A/C/G/T (the host's PW_REF_ACGT also needs the query to be). */
+#define PW_PACK_HOST 1u
+#define PW_PACK_ACGT 2u
+typedef struct pw_cs_rec {
+  int32_t q_total, t_total;
+  uint32_t n_ops, n_lits, n_events_max;
+  uint32_t flags;        /* PW_PACK_* */
+  uint64_t text_bound;
+} pw_cs_rec;
+int pw_pack_cs_batch(const uint8_t* cs_text, const uint64_t* cs_off, const int32_t* offset, const int32_t* qlen,
+                     uint32_t n, uint32_t* ops, uint8_t* lits, pw_cs_rec* out, void* stream);
+
 /* GSeqAlign::refineMSA consensus of a packed layout file (PWL1, tests/pwl_format.md) on the HIP
  * path, written as a PWC1 result; flags bit0 = MSAColumns::removeConsGaps, bit1 = disable
  * MSAColumns::refineClipping.  Returns the reference's exit code (0, 1 bad index / GError, 5 zero

@@ -12,6 +12,7 @@ import ctypes
 import os
 import pathlib
 import subprocess
+import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parent
 REPO = ROOT.parent
@@ -127,6 +128,7 @@ _SIGS = {
     "pw_ga_row_remove_columns": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_uint64]),
     "pw_ga_row_finish": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    "pw_pack_cs_batch": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4),
     "pw_pack_cs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),
                                   ctypes.POINTER(ctypes.c_int32)]),
@@ -190,6 +192,37 @@ def pack_cs(cs: str, offset: int, qlen: int):
     epos = ctypes.c_int32(0)
     rc = L.pw_pack_cs(cs.encode(), offset, qlen, ops, n, lits, n, ctypes.byref(tot), ctypes.byref(epos))
     return rc, list(ops[:tot.n_ops]), bytes(lits[:tot.n_lits]), tot, epos.value
+
+
+CS_REC = np.dtype([("q_total", "<i4"), ("t_total", "<i4"), ("n_ops", "<u4"), ("n_lits", "<u4"),
+                   ("n_events_max", "<u4"), ("flags", "<u4"), ("text_bound", "<u8")])
+PACK_HOST, PACK_ACGT = 1, 2
+
+
+def pack_cs_gpu(cs_list, offsets, qlens, device: str = "cuda:0"):
+    """pw_pack_cs_batch on the GPU for a list of cs strings (bytes) -> (ops uint32[], lits
+    uint8[], cs_off uint64[n+1], records CS_REC[n]); record i's ops / literal bytes start at
+    cs_off[i] (PACK_HOST records: pack them with pack_cs)."""
+    import torch
+    n = len(cs_list)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(c) for c in cs_list], dtype=np.uint64)
+    text = np.frombuffer(b"".join(cs_list) + b"\0" * 16, dtype=np.uint8)
+    t = lambda a: torch.from_numpy(np.array(a, copy=True)).to(device)
+    d_text, d_off = t(text), t(off.view(np.int64))
+    d_o, d_q = t(np.asarray(offsets, dtype=np.int32)), t(np.asarray(qlens, dtype=np.int32))
+    tot = int(off[-1]) + 16
+    d_ops = torch.zeros(tot, dtype=torch.int32, device=device)
+    d_lits = torch.zeros(tot, dtype=torch.uint8, device=device)
+    d_rec = torch.zeros(max(n, 1) * CS_REC.itemsize, dtype=torch.uint8, device=device)
+    rc = lib().pw_pack_cs_batch(d_text.data_ptr(), d_off.data_ptr(), d_o.data_ptr(), d_q.data_ptr(), n,
+                                d_ops.data_ptr(), d_lits.data_ptr(), d_rec.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"pw_pack_cs_batch: {rc}")
+    torch.cuda.synchronize()
+    recs = d_rec.cpu().numpy().view(CS_REC)[:n]
+    return d_ops.cpu().numpy().view(np.uint32), d_lits.cpu().numpy(), off, recs
 
 
 class HostBatch:
