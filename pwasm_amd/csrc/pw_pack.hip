@@ -11,9 +11,9 @@
 //   * each lane decodes the (at most two) ops starting in its 4 characters; wave scans of the
 //     query / target / literal advances and of the emitted-op counts place every op word and
 //     literal byte and give the positions of the reference's bounds checks.
-// Anything else — a character outside the grammar, a ':' run of more than 9 digits, a '*' not
-// followed by two letters, an empty indel, '~' / '=', a bounds violation, one op longer than a
-// window — flags the record PW_PACK_HOST: the caller packs it with pw_pack_cs, which produces
+// Anything else — a character outside [0-9A-Za-z:*+-], a ':' run of more than 9 digits, a '*'
+// not followed by exactly two characters, an empty indel or one holding a digit, '~' / '=', a
+// bounds violation, one op longer than a window — flags the record PW_PACK_HOST: the caller packs it with pw_pack_cs, which produces
 // the reference's exact error (such records are rare and end the report at their line anyway).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -95,21 +95,31 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
         bad = true;  // one op fills the window
         break;
       }
-      // decode this lane's ops (at most two: an op has >= 2 characters)
-      PkOp op[2];
-      int nop = 0;
+      // decode this lane's ops (one per op start among its 4 characters, in registers: j is a
+      // constant after unrolling).  An op ends at the next op start: the next set bit of this
+      // lane's starts, else the first start of the next lane that has one, else the window end.
+      const uint64_t nxt_l = lane == 63 ? 0ull : any & ~((2ull << lane) - 1ull);  // op-start lanes above
+      const int nl = nxt_l ? __builtin_ctzll(nxt_l) : 64;
+      const uint32_t nl_mask = (uint32_t)__shfl((int)smask, nl < 64 ? nl : 0, 64);
+      const int next_start = nl < 64 ? 4 * nl + __builtin_ctz(nl_mask) : wl;
+      PkOp op[4];
+      bool has[4];
       int la_q = 0, la_t = 0, la_l = 0, la_e = 0, la_v = 0;
       uint64_t la_b = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int s = 4 * lane + j;
-        if (((smask >> j) & 1u) && s < lim && nop < 2) {
-          const uint32_t c = w[s];
-          int e = s + 1;
-          while (e < wl && !pk_opc(w[e])) e++;
-          PkOp o;
-          o.s = s + 1;
-          o.e = e;
+        has[j] = ((smask >> j) & 1u) && s < lim;
+        PkOp& o = op[j];
+        o.type = PW_OP_MATCH;
+        o.n = 0;
+        o.s = s + 1;
+        o.emit = false;
+        const uint32_t later = (smask >> (j + 1)) << (j + 1);  // this lane's starts after j
+        const int e = later ? 4 * lane + __builtin_ctz(later) : next_start;
+        o.e = e;
+        if (has[j]) {
+          const uint32_t c = (c4 >> (8 * j)) & 0xFFu;
           const int len = e - s - 1;
           o.n = len;
           o.emit = true;
@@ -117,7 +127,7 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
             o.type = PW_OP_MATCH;
             if (len < 1 || len > 9) lbad = true;
             int v = 0;
-            for (int k = s + 1; k < e; k++) {
+            for (int k = s + 1; k < e && k < s + 10; k++) {
               const uint32_t d = w[k];
               if (!pk_digit(d)) lbad = true;
               v = v * 10 + (int)(d - '0');
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
             la_t += v;
           } else if (c == '*') {
             o.type = PW_OP_SUB;
-            if (len != 2 || !pk_alpha(w[s + 1]) || !pk_alpha(w[s + 2])) lbad = true;
+            if (len != 2) lbad = true;  // (any two characters, as the host packer takes them)
             o.n = 1;
             la_q += 1;
             la_t += 1;
@@ -138,7 +148,7 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
           } else {
             o.type = c == '-' ? PW_OP_INS : PW_OP_DEL;
             if (len < 1) lbad = true;
-            for (int k = s + 1; k < e; k++)
+            for (int k = s + 1; k < e; k++)  // (the host's is_alpha run ends at a digit: UNHANDLED)
               if (!pk_alpha(w[k])) lbad = true;
             if (c == '-') {
               la_t += len;
@@ -150,7 +160,6 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
             la_b += kPkBoundIndel;
           }
           la_e += o.emit ? 1 : 0;
-          op[nop++] = o;
         }
       }
       if (__ballot(lbad)) {
@@ -162,7 +171,9 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
                 ie = wave_scan_incl(la_e);
       int q = qpos + iq - la_q;
       uint32_t lp = nlits + (uint32_t)(il - la_l), op_i = nops + (uint32_t)(ie - la_e);
-      for (int k = 0; k < nop; k++) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (!has[k]) continue;
         const PkOp& o = op[k];
         const int qp = off + q;
         if (o.type == PW_OP_MATCH) {

@@ -12,7 +12,7 @@ import pwasm_amd as pw
 from conftest import synth_paf
 
 pytestmark = pytest.mark.gpu
-GRAMMAR = re.compile(rb"(?::[0-9]{1,9}|\*[A-Za-z]{2}|[+-][A-Za-z]+)*")
+GRAMMAR = re.compile(rb"(?::[0-9]{1,9}|\*[0-9A-Za-z]{2}|[+-][A-Za-z]+)*")
 
 
 def paf_records(paf):
@@ -38,7 +38,7 @@ def edge_records():
             (b":3*a", 0, 10), (b":3*a:2", 0, 10), (b": 3", 0, 10), (b":-3", 0, 10), (b":1234567890", 0, 2 ** 31 - 1),
             (b":123456789", 0, 2 ** 31 - 1), (b":5a", 0, 10), (b"-ac5", 0, 10), (b"*12", 0, 10), (b"x:5", 0, 10),
             (b":2*ac" * 40, 0, 400), (b"-" + b"a" * 300 + b":5", 0, 10), (b":5-" + b"c" * 255 + b":5", 0, 10),
-            (b"*NN*aT", 0, 5), (b"-acgtn", 0, 3)]
+            (b"*NN*aT", 0, 5), (b"-acgtn", 0, 3), (b"*a1:5", 0, 10), (b"*1a-ac", 0, 10)]
     # random well-formed strings of many windows, ops straddling window boundaries
     for _ in range(200):
         parts, q = [], 0
