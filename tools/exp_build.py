@@ -109,6 +109,10 @@ def variants():
         "head": head,
         "cur": cur,
         "prof": lambda: profiled(cur),
+        "s_maxilp": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
+        "s_maxmem": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]),
+        "s_iterilp": (cur, ["-mllvm", "-misched=gcn-iterative-ilp"]),
+        "s_bias100": (cur, ["-mllvm", "-amdgpu-schedule-metric-bias=100"]),
         "ig5": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 5u) ig = (uint64_t)ncu * 5u;")]),
         "ig10": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;")]),
         "ig64": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 16u) ig = (uint64_t)ncu * 16u;", "if (ig > (uint64_t)ncu * 64u) ig = (uint64_t)ncu * 64u;")]),
@@ -128,11 +132,14 @@ def main(names):
         os.makedirs(os.path.join(d, "lib"), exist_ok=True)
         hip = os.path.join(d, "pw_report.hip")
         v = vs[name]
+        extra = []
+        if isinstance(v, tuple):
+            v, extra = v
         open(hip, "w").write(v() if callable(v) else v)
         o = os.path.join(d, "pw_report.o")
         inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
-                        "-Wno-unused-function", *inc, "-c", hip, "-o", o], check=True)
+                        "-Wno-unused-function", *extra, *inc, "-c", hip, "-o", o], check=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
                         os.path.join(d, "lib", "libpwasm_amd.so"), o, *objs, "-ldl"], check=True)
         print("built", name, flush=True)
