@@ -109,6 +109,14 @@ def variants():
         "head": head,
         "cur": cur,
         "prof": lambda: profiled(cur),
+        "tc_small5": lambda: patched(cur, TC_OPS8 + [("constexpr int kTcQ = 48;", "constexpr int kTcQ = 32;"),
+                                               ("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 5u) tg = (uint64_t)ncu * 5u;")]),
+        "tc_small6": lambda: patched(cur, TC_OPS8 + [("constexpr int kTcQ = 48;", "constexpr int kTcQ = 32;"),
+                                               ("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 6u) tg = (uint64_t)ncu * 6u;")]),
+        "mem": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]),
+        "mem_nounroll": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-fno-unroll-loops"]),
+        "mem_o2": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-O2"]),
+        "mem_relaxocc": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-mllvm", "-amdgpu-schedule-relaxed-occupancy"]),
         "s_maxilp": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]),
         "s_maxmem": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]),
         "s_iterilp": (cur, ["-mllvm", "-misched=gcn-iterative-ilp"]),
@@ -132,9 +140,9 @@ def main(names):
         os.makedirs(os.path.join(d, "lib"), exist_ok=True)
         hip = os.path.join(d, "pw_report.hip")
         v = vs[name]
-        extra = []
+        extra = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]  # (as the Makefile builds pw_report)
         if isinstance(v, tuple):
-            v, extra = v
+            v, extra = v[0], extra + [f for f in v[1] if f not in extra]
         open(hip, "w").write(v() if callable(v) else v)
         o = os.path.join(d, "pw_report.o")
         inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
