@@ -190,3 +190,30 @@ def test_cli_many_batches(built, tmp_path, chunk, kind, monkeypatch):
         paf = str(p)
     monkeypatch.setenv("PW_CHUNK_BYTES", str(chunk))
     same(["-r", fa, paf])
+
+
+@pytest.mark.parametrize("chunk,kind", [(None, None), (3000, None), (20000, "dups"), (5000, "mismatch"),
+                                        (None, "cfg2")])
+def test_cli_output_file(built, tmp_path, chunk, kind, monkeypatch):
+    """-o to a regular file (a stale longer file is truncated), one batch or many, clean batches and
+    batches with messages / a fatal record: same bytes, stderr and exit code as the oracle."""
+    from test_gpu_parity import _inject
+    from test_shard import _with_duplicates_and_comments
+    if kind == "cfg2":
+        fa, paf = synth_paf(tmp_path, 2, seed=31, scale=0.2)
+        flags = ["-G", "-C"]
+    else:
+        fa, paf = synth_paf(tmp_path, 0, seed=29)
+        flags = []
+    if kind == "dups":
+        paf = _with_duplicates_and_comments(paf, tmp_path, 3)
+    elif kind == "mismatch":
+        paf = _inject(paf, tmp_path, "mismatch", seed=13)
+    if chunk:
+        monkeypatch.setenv("PW_CHUNK_BYTES", str(chunk))
+    want, got = tmp_path / "o.txt", tmp_path / "h.txt"
+    got.write_bytes(b"stale\n" * 3_000_000)
+    ro, _, eo = run([ORACLE, *flags, "-r", fa, paf, "-o", want])
+    rp, _, ep = run([CLI, *flags, "-r", fa, paf, "-o", got])
+    assert (rp, ep) == (ro, eo), (rp, ro, ep[-2000:], eo[-2000:])
+    assert got.read_bytes() == want.read_bytes()
