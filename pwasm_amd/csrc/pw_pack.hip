@@ -23,6 +23,7 @@
 
 namespace pw {
 
+#define LDS __attribute__((address_space(3)))
 constexpr int kPackWin = 256;  // characters per window (4 per lane)
 constexpr uint64_t kPkBoundSub = 190, kPkBoundIndel = 140;  // = the host packer's text bounds
 
@@ -44,7 +45,9 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
                                                       pw_cs_rec* out) {
   __shared__ uint8_t win[4][kPackWin + 4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint8_t* w = win[wv];
+  // (an address-space-3 pointer: through a generic one every window read would be a flat load,
+  // which also waits for the wave's outstanding global stores)
+  LDS uint8_t* w = (LDS uint8_t*)win[wv];
   const uint32_t nw = gridDim.x * 4;
   for (uint32_t ri = blockIdx.x * 4 + (uint32_t)wv; ri < n; ri += nw) {
     const uint64_t base = cs_off[ri], L = cs_off[ri + 1] - base;
@@ -65,8 +68,8 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
         const uint32_t c = i < wl ? text[base + pos + (uint64_t)i] : 0u;
         c4 |= c << (8 * j);
       }
-      *reinterpret_cast<uint32_t*>(w + 4 * lane) = c4;
-      if (lane == 0) *reinterpret_cast<uint32_t*>(w + kPackWin) = 0u;
+      *reinterpret_cast<LDS uint32_t*>(w + 4 * lane) = c4;
+      if (lane == 0) *reinterpret_cast<LDS uint32_t*>(w + kPackWin) = 0u;
       __builtin_amdgcn_wave_barrier();
       // character classes; op starts
       bool lbad = false;
@@ -244,7 +247,9 @@ extern "C" int pw_pack_cs_batch(const uint8_t* cs_text, const uint64_t* cs_off, 
                                 void* stream) {
   if (!cs_text || !cs_off || !offset || !qlen || !ops || !lits || !out) return PW_E_ARG;
   if (n == 0) return PW_OK;
-  const uint32_t grid = (n + 3) / 4 < 8192u ? (n + 3) / 4 : 8192u;
+  // a wavefront per record (the per-record work is a short dependent chain: more waves in flight,
+  // not a longer loop per wave, hide it)
+  const uint32_t grid = (n + 3) / 4 < (1u << 20) ? (n + 3) / 4 : (1u << 20);
   hipLaunchKernelGGL(pw::pack_cs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, cs_text, cs_off, offset, qlen,
                      n, ops, lits, out);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
