@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
                                                       const int32_t* qlen, uint32_t n, uint32_t* ops, uint8_t* lits,
                                                       pw_cs_rec* out) {
   __shared__ uint8_t win[4][kPackWin + 4];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar loop)
   // (an address-space-3 pointer: through a generic one every window read would be a flat load,
   // which also waits for the wave's outstanding global stores)
   LDS uint8_t* w = (LDS uint8_t*)win[wv];
