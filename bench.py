@@ -393,7 +393,8 @@ def bench_gapassem(args, world, rank, dev_name):
                          "kernel": "pw_msa_count+pw_msa_call+pw_msa_refine (rank 0)", "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg,
                          "alg_formula": "SURVEY 8(d): sum_rows(16 + 3*seqlen) + 25*n_cols",
-                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd")},
+                         "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd"),
+                         "issue_busy": issue_busy(prof, ("pw::tile_counts", "pw::row_chunk_sums"))},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
