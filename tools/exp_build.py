@@ -102,6 +102,27 @@ def tc_lit(nbytes, back):
 TC_OPS8 = [("constexpr int kTcOps = 12;", "constexpr int kTcOps = 8;")]
 
 
+WR_NUM_BF = ("template <class S, int N>\n__device__ __forceinline__ void wr_lit(", """// "%d" of v < 10^8 without the < 10^4 branch (4 digit-pair reads, digits counted by compares)
+template <class S>
+__device__ __forceinline__ void wr_num_bf(S& k, const LDS SmallTables* t, uint32_t v) {
+  if (v >= 100000000u) {
+    wr_dig(k, v);
+    return;
+  }
+  const LDS uint16_t* d2 = reinterpret_cast<const LDS uint16_t*>(t->dig2);
+  const uint32_t h = v / 10000u, l = v - 10000u * h;
+  const uint32_t hh = h / 100u, hl = h - 100u * hh, lh = l / 100u, ll = l - 100u * lh;
+  const uint64_t p = (uint64_t)d2[hh] | (uint64_t)d2[hl] << 16 | (uint64_t)d2[lh] << 32 | (uint64_t)d2[ll] << 48;
+  const int nd = 1 + (v >= 10u) + (v >= 100u) + (v >= 1000u) + (v >= 10000u) + (v >= 100000u) + (v >= 1000000u) +
+                 (v >= 10000000u);
+  const uint64_t q = p >> (8 * (8 - nd));
+  const uint32_t w[2] = {(uint32_t)q, (uint32_t)(q >> 32)};
+  k.put_bytes(w, nd);
+}
+template <class S, int N>
+__device__ __forceinline__ void wr_lit(""")
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
@@ -114,6 +135,10 @@ def variants():
         "tc_small6": lambda: patched(cur, TC_OPS8 + [("constexpr int kTcQ = 48;", "constexpr int kTcQ = 32;"),
                                                ("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 6u) tg = (uint64_t)ncu * 6u;")]),
         "mem": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]),
+        "num_tloc": lambda: patched(cur, [WR_NUM_BF, ("wr_num(o, r.tab, (uint32_t)(in.tloc + 1));", "wr_num_bf(o, r.tab, (uint32_t)(in.tloc + 1));")]),
+        "num_all": lambda: patched(cur, [WR_NUM_BF, ("wr_num(o, r.tab, (uint32_t)(in.tloc + 1));", "wr_num_bf(o, r.tab, (uint32_t)(in.tloc + 1));"),
+                                         ("wr_num(o, r.tab, (uint32_t)(e.rloc + 1));", "wr_num_bf(o, r.tab, (uint32_t)(e.rloc + 1));"),
+                                         ("wr_num(o, r.tab, (uint32_t)(aap0 + 1));", "wr_num_bf(o, r.tab, (uint32_t)(aap0 + 1));")]),
         "mem_nounroll": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-fno-unroll-loops"]),
         "mem_o2": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-O2"]),
         "mem_relaxocc": (cur, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause", "-mllvm", "-amdgpu-schedule-relaxed-occupancy"]),
