@@ -1165,6 +1165,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 
   for (uint32_t sb = 0; layout_ok && sb < n_ops; sb += kSegOps) {
     const uint32_t nseg = (n_ops - sb) < (uint32_t)kSegOps ? (n_ops - sb) : (uint32_t)kSegOps;
+    const bool two = nseg > (uint32_t)kWave;  // (uniform) a segment of <= 64 ops skips its empty second half
     // ---- op words (2 per lane) + wave scans of the query / target / literal advances
     uint32_t wd[2];
     int qs[2], ts[2];
@@ -1173,6 +1174,13 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       const uint32_t idx = 64 * k + lane;
+      if (k == 1 && !two) {
+        wd[1] = 0u;
+        qs[1] = qc + (int)qtot;
+        ts[1] = tc + (int)ttot;
+        ls[1] = lc + ltot;
+        continue;
+      }
       if (sb == 0) {
         wd[k] = k == 0 ? pre.w0 : pre.w1;
       } else {  // (clamped index: an unconditional load, waited for inside this branch: a wait at
@@ -1205,6 +1213,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     uint32_t lw[2][3];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
+      if (k == 1 && !two) {
+        qref[1] = qlit[1] = 0;
+        lw[1][0] = lw[1][1] = lw[1][2] = 0u;
+        continue;
+      }
       const int qp = d.offset + qs[k];
       const int qc = qp < 0 ? 0 : (qp >= L ? (L > 0 ? L - 1 : 0) : qp);
       qref[k] = R[rev ? (L > 0 ? L - 1 - qc : 0) : qc];
@@ -1219,6 +1232,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     uint32_t sm_prev = prev_sub ? 1u : 0u;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
+      if (k == 1 && !two) {
+        subm[1] = hm[1] = 0ull;
+        continue;
+      }
       const uint32_t idx = 64 * k + lane;
       const bool in = idx < nseg;
       const uint32_t typ = wd[k] >> 30;
