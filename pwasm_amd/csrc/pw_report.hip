@@ -1281,6 +1281,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
+      if (k == 1 && !two) continue;
       const uint32_t idx = 64 * k + lane;
       const uint32_t typ = wd[k] >> 30;
       bool slow = false;
