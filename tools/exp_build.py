@@ -123,12 +123,52 @@ template <class S, int N>
 __device__ __forceinline__ void wr_lit(""")
 
 
+FX_LDS = [
+    ("        f.pad = 0;\n        f.dst = g0;", "        f.pad = (uint32_t)linelen;\n        f.dst = g0;"),
+    ("  __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts\n",
+     "  __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts\n"
+     "  __shared__ uint32_t fxb[256][kFxBuf / 4 + 1];\n"),
+    ("constexpr int kFxLit = 32;\n", "constexpr int kFxLit = 32;\nconstexpr int kFxBuf = 160;\n"),
+    ("""    GlobalSink g;
+    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);
+    g.pos = 0;
+    int rel;
+    emit_event(g, r, in, skip, rel);
+""", """    int rel;
+    if (f.pad <= (uint32_t)kFxBuf) {
+      LDS uint8_t* lb = (LDS uint8_t*)&fxb[threadIdx.x][0];
+      LdsSink<kFxBuf> ls;
+      ls.buf = lb;
+      ls.junk = lb + kFxBuf;
+      ls.pos = 0;
+      emit_event(ls, r, in, skip, rel);
+      PW_GLOBAL uint8_t* d = (PW_GLOBAL uint8_t*)(A.text + f.dst);
+      const int n = (int)f.pad;
+      int hd = (int)((4u - ((uint32_t)f.dst & 3u)) & 3u);
+      if (hd > n) hd = n;
+      int i = 0;
+      for (; i < hd; i++) d[i] = lb[i];
+      for (; i + 4 <= n; i += 4)
+        *reinterpret_cast<PW_GLOBAL uint32_t*>(d + i) =
+            (uint32_t)lb[i] | ((uint32_t)lb[i + 1] << 8) | ((uint32_t)lb[i + 2] << 16) | ((uint32_t)lb[i + 3] << 24);
+      for (; i < n; i++) d[i] = lb[i];
+    } else {
+      GlobalSink g;
+      g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);
+      g.pos = 0;
+      emit_event(g, r, in, skip, rel);
+    }
+"""),
+]
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
     return {
         "head": head,
         "cur": cur,
+        "fx_lds": lambda: patched(cur, FX_LDS),
         "prof": lambda: profiled(cur),
         "tc_small5": lambda: patched(cur, TC_OPS8 + [("constexpr int kTcQ = 48;", "constexpr int kTcQ = 32;"),
                                                ("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 5u) tg = (uint64_t)ncu * 5u;")]),
