@@ -169,6 +169,10 @@ def variants():
         "head": head,
         "cur": cur,
         "fx_lds": lambda: patched(cur, FX_LDS),
+        "r_grid6": lambda: patched(cur, [("if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;",
+                                          "if (rg > (uint64_t)ncu * 6u) rg = (uint64_t)ncu * 6u;")]),
+        "tg3": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 3u) tg = (uint64_t)ncu * 3u;")]),
+        "tg6": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 6u) tg = (uint64_t)ncu * 6u;")]),
         "prof": lambda: profiled(cur),
         "tc_small5": lambda: patched(cur, TC_OPS8 + [("constexpr int kTcQ = 48;", "constexpr int kTcQ = 32;"),
                                                ("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 5u) tg = (uint64_t)ncu * 5u;")]),
