@@ -171,6 +171,8 @@ def variants():
         "fx_lds": lambda: patched(cur, FX_LDS),
         "r_grid6": lambda: patched(cur, [("if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;",
                                           "if (rg > (uint64_t)ncu * 6u) rg = (uint64_t)ncu * 6u;")]),
+        "r_grid9": lambda: patched(cur, [("rg = (uint64_t)ncu * 2u * pw::kRenderOcc;", "rg = (uint64_t)ncu * 3u * pw::kRenderOcc;")]),
+        "r_grid12": lambda: patched(cur, [("rg = (uint64_t)ncu * 2u * pw::kRenderOcc;", "rg = (uint64_t)ncu * 4u * pw::kRenderOcc;")]),
         "tg3": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 3u) tg = (uint64_t)ncu * 3u;")]),
         "tg6": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 6u) tg = (uint64_t)ncu * 6u;")]),
         "prof": lambda: profiled(cur),
