@@ -173,6 +173,8 @@ def variants():
                                           "if (rg > (uint64_t)ncu * 6u) rg = (uint64_t)ncu * 6u;")]),
         "r_grid9": lambda: patched(cur, [("rg = (uint64_t)ncu * 2u * pw::kRenderOcc;", "rg = (uint64_t)ncu * 3u * pw::kRenderOcc;")]),
         "r_grid12": lambda: patched(cur, [("rg = (uint64_t)ncu * 2u * pw::kRenderOcc;", "rg = (uint64_t)ncu * 4u * pw::kRenderOcc;")]),
+        "ig8": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;", "if (ig > (uint64_t)ncu * 8u) ig = (uint64_t)ncu * 8u;")]),
+        "ig12": lambda: patched(cur, [("if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;", "if (ig > (uint64_t)ncu * 12u) ig = (uint64_t)ncu * 12u;")]),
         "tg3": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 3u) tg = (uint64_t)ncu * 3u;")]),
         "tg6": lambda: patched(cur, [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", "if (tg > (uint64_t)ncu * 6u) tg = (uint64_t)ncu * 6u;")]),
         "prof": lambda: profiled(cur),
