@@ -162,6 +162,17 @@ FX_LDS = [
 ]
 
 
+FX_PAR = [
+    ("""    const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];
+    const Hot h = W.hot[f.s];""", """    const uint64_t sl = (c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm);  // (= f.s)
+    const uint64_t fdst = W.fix[sl].dst;
+    const Hot h = W.hot[sl];"""),
+    ("const Cold cd = W.cold[f.s];", "const Cold cd = W.cold[sl];"),
+    ("W.tx + (uint64_t)kTx * f.s);\n      t0 = tp4[0];", "W.tx + (uint64_t)kTx * sl);\n      t0 = tp4[0];"),
+    ("g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);", "g.p = (PW_GLOBAL uint8_t*)(A.text + fdst);"),
+]
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
@@ -169,6 +180,7 @@ def variants():
         "head": head,
         "cur": cur,
         "fx_lds": lambda: patched(cur, FX_LDS),
+        "fx_par": lambda: patched(cur, FX_PAR),
         "r_grid6": lambda: patched(cur, [("if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;",
                                           "if (rg > (uint64_t)ncu * 6u) rg = (uint64_t)ncu * 6u;")]),
         "r_grid9": lambda: patched(cur, [("rg = (uint64_t)ncu * 2u * pw::kRenderOcc;", "rg = (uint64_t)ncu * 3u * pw::kRenderOcc;")]),
