@@ -43,7 +43,9 @@ def main():
                     help="2 (default at N=1: BASELINE configs[1]); 3 (default at N>1: the 10M-record set sharded "
                          "by target genome, configs[2]); 5 (GapAssem, configs[4])")
     ap.add_argument("--scale", type=float, default=1.0)
-    ap.add_argument("--cpu-sample", type=int, default=100000, help="records timed on the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="records timed on the CPU oracle (default: the whole cfg2 batch; 100k records of cfg3, "
+                         "10 of cfg4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle diff + end-to-end CLI run")
     ap.add_argument("--remove-gaps", action="store_true", help="cfg5: MSAColumns::removeConsGaps=true")
@@ -205,7 +207,15 @@ def main():
         traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
         flags_cli = ["-G", "-C"] if flags else []
         parity, cpu, e2e, gpack = None, None, None, None
-        if not args.no_parity and world == 1 and v.n_alns <= 200000:
+        big = args.config == 4 or v.n_alns > 200000
+        if not args.no_parity and world == 1 and big:
+            # too large for files on both sides: the report of the benchmarked batch and the
+            # CLI's stdout streamed through CRC-32, against the oracle run over byte ranges of
+            # the PAF in parallel processes with the CRCs combined (hash_parity)
+            parity, e2e, n_or = hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp)
+            if n_or != n_events:
+                parity = "FAIL"
+        elif not args.no_parity and world == 1:
             # the benchmarked batch itself, copied back once (outside the timed region) and
             # diffed byte for byte against the oracle on the same input
             got = os.path.join(tmp, "hip.txt")
@@ -214,7 +224,7 @@ def main():
             el = run_oracle(flags_cli, fa, paf, want)
             parity = "ok" if rc == 0 and filecmp.cmp(got, want, shallow=False) else "FAIL"
             n_or = count_events(want)
-            if not args.no_cpu_baseline and args.cpu_sample >= v.n_alns:
+            if not args.no_cpu_baseline and (args.cpu_sample or v.n_alns) >= v.n_alns:
                 cpu = {"value": n_or / el, "unit": "events/s", "cores": 1, "kind": "port",
                        "sample": f"the whole benchmarked batch ({v.n_alns} records, {n_or} events, {el:.1f} s, "
                                  f"oracle/pafreport_oracle pinned to one core)"}
@@ -232,7 +242,10 @@ def main():
                 parity = "FAIL"
             gpack = gpu_pack_check(pw, paf)
         if cpu is None and not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(flags_cli, fa, paf, args.cpu_sample, tmp)
+            cpu = cpu_baseline(flags_cli, fa, paf, args.cpu_sample if args.cpu_sample else
+                               (10 if args.config == 4 else 100000), tmp)
+        if cpu is not None:
+            cpu.update(host_cpu())
         out = {
             "metric": "cs-events classified/sec (whole node) + achieved HBM GB/s, 1/2/4/8 MI355X",
             "value": tot_events * args.steps / max_el,
@@ -400,6 +413,141 @@ def bench_gapassem(args, world, rank, dev_name):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_cpu():
+    """CPU model and core counts of the host the baseline ran on."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
+def crc32_combine(crc1, crc2, len2):
+    """zlib's crc32_combine (GF(2) matrix powers): the CRC-32 of A+B from crc(A), crc(B), len(B)."""
+    def times(mat, vec):
+        s, i = 0, 0
+        while vec:
+            if vec & 1:
+                s ^= mat[i]
+            vec >>= 1
+            i += 1
+        return s
+
+    def square(mat):
+        return [times(mat, mat[n]) for n in range(32)]
+
+    if len2 <= 0:
+        return crc1
+    odd = [0xEDB88320] + [1 << n for n in range(31)]
+    even = square(odd)
+    odd = square(even)
+    while True:
+        even = square(odd)
+        if len2 & 1:
+            crc1 = times(even, crc1)
+        len2 >>= 1
+        if not len2:
+            break
+        odd = square(even)
+        if len2 & 1:
+            crc1 = times(odd, crc1)
+        len2 >>= 1
+        if not len2:
+            break
+    return crc1 ^ crc2
+
+
+def crc_stream(f, block=1 << 22):
+    """(crc32, bytes, event lines) of a binary stream read to its end."""
+    import zlib
+    crc, n, lines, hdr, tail = 0, 0, 0, 0, b"\n"
+    while True:
+        b = f.read(block)
+        if not b:
+            break
+        crc = zlib.crc32(b, crc)
+        n += len(b)
+        lines += b.count(b"\n")
+        hdr += b.count(b"\n>") + (tail == b"\n" and b[:1] == b">")
+        tail = b[-1:]
+    return crc, n, lines - hdr
+
+
+def oracle_crc(flags_cli, fa, paf, procs, chunks_per_proc=4):
+    """The oracle over the PAF in byte ranges (--range; --elide-dead skips the query-suffix copy
+    nothing reads when the codon pass is off), `procs` processes at a time, each stdout streamed
+    through CRC-32 and the CRCs combined in order.  A range split can only differ from one pass
+    through the gene-mode q~t dedupe across ranges, which would show as a mismatch, never hide
+    one.  Returns (crc, bytes, events, seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+    size = os.path.getsize(paf)
+    k = max(1, procs * chunks_per_proc)
+    cuts = [size * i // k for i in range(k + 1)]
+
+    def one(i):
+        p = subprocess.Popen([str(REPO / "oracle/build/pafreport_oracle"), "--elide-dead", "--range",
+                              f"{cuts[i]}:{cuts[i + 1]}", *flags_cli, "-r", fa, paf],
+                             stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+        r = crc_stream(p.stdout)
+        if p.wait() != 0:
+            raise RuntimeError(f"oracle range {i} failed")
+        return r
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(procs) as ex:
+        parts = list(ex.map(one, range(k)))
+    crc, n, ev = 0, 0, 0
+    for c, m, e in parts:
+        crc = crc32_combine(crc, c, m)
+        n += m
+        ev += e
+    return crc, n, ev, time.perf_counter() - t0
+
+
+def hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp):
+    """Parity of a large run (cfg3 at 10M records, cfg4): the benchmarked batch's report (written
+    by pw_batch_write_report into a FIFO) and the drop-in CLI's stdout (end to end, PAF text in)
+    vs the chunked oracle, by CRC-32 + length + event count.  -> (parity, e2e, oracle events)."""
+    import threading
+    want = oracle_crc(flags_cli, fa, paf, host_threads())
+    log(f"[parity] oracle: {want[1]} bytes, {want[2]} events in {want[3]:.1f}s ({host_threads()} processes)")
+    fifo = os.path.join(tmp, "report.fifo")
+    os.mkfifo(fifo)
+    got = {}
+
+    def reader():
+        with open(fifo, "rb") as f:
+            got["r"] = crc_stream(f)
+
+    th = threading.Thread(target=reader)
+    th.start()
+    rc = batch.write_report_from(dev, fifo)
+    if rc != 0 and "r" not in got:  # never opened: release the reader
+        open(fifo, "wb").close()
+    th.join()
+    batch_ok = rc == 0 and got.get("r") == want[:3]
+    t0 = time.perf_counter()
+    p = subprocess.Popen([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf], stdout=subprocess.PIPE,
+                         stderr=subprocess.DEVNULL)
+    cli = crc_stream(p.stdout)
+    cli_rc = p.wait()
+    cli_s = time.perf_counter() - t0
+    cli_ok = cli_rc == 0 and cli == want[:3]
+    e2e = {"cli_wall_s": round(cli_s, 3), "events_per_s": want[2] / cli_s, "parity": "ok" if cli_ok else "FAIL",
+           "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf > pipe (PAF text -> report stream, "
+                  f"{os.path.getsize(paf)} B in, {cli[1]} B out, CRC-32 checked)"}
+    log(f"[parity] batch report {'ok' if batch_ok else 'FAIL'} (crc {got.get('r')} vs {want[:3]}); "
+        f"CLI {'ok' if cli_ok else 'FAIL'} {cli_s:.1f}s")
+    parity = {"result": "ok" if batch_ok and cli_ok else "FAIL", "method": "CRC-32 + bytes + events, streamed",
+              "oracle": f"oracle/pafreport_oracle over {host_threads() * 4} byte ranges, {host_threads()} processes, "
+                        f"{want[3]:.1f}s", "bytes": want[1], "crc32": f"{want[0]:08x}"}
+    return parity, e2e, want[2]
 
 
 def host_threads():

@@ -962,6 +962,7 @@ static void predict_impact(gstr* txt, const tdiff* di, const gstr* r_trseq, int 
 }
 
 static int g_skip_codan = 0;
+static int g_elide_dead = 0; /* --elide-dead (parity tooling) */
 
 /* printDiffInfo, pafreport.cpp:885-955; ref = forward upper-case query */
 static void print_diff_info(FILE* f, const char* rlabel, const char* tlabel, const aln_info* al, int alnscore,
@@ -994,7 +995,9 @@ static void print_diff_info(FILE* f, const char* rlabel, const char* tlabel, con
     /* GStr r_trseq(ref + r_trloc, evtlen): the 2nd argument is a capacity, so the
        whole suffix is copied (pafreport.cpp:908) */
     gs_clear(&r_trseq);
-    if (r_trloc < L) gs_appendn(&r_trseq, ref + r_trloc, L - r_trloc);
+    /* (--elide-dead, parity tooling: with the codon pass skipped the copy is never read, so a
+       parity run may skip it; the CPU baseline keeps the reference's literal cost) */
+    if (r_trloc < L && !(g_skip_codan && g_elide_dead)) gs_appendn(&r_trseq, ref + r_trloc, L - r_trloc);
     if (status.len == 0) mmotif_check(&status, &rctx);
     gs_clear(&impact);
     if (!g_skip_codan) predict_impact(&impact, di, &r_trseq, r_trloc);
@@ -1144,8 +1147,26 @@ int main(int argc, char* argv[]) {
   comp_init();
   g_errf = stderr;
   const char* items_path = NULL;
-  if (argc > 2 && strcmp(argv[1], "--items") == 0) { /* test tooling, not a pafreport option */
-    items_path = argv[2];
+  long long range_a = 0, range_b = -1;
+  /* test tooling, not pafreport options (they precede the pafreport arguments):
+   *   --items PATH    line-tagged item stream (PWI1) instead of the report
+   *   --range A:B     only the PAF lines that start in bytes [A, B) (chunked parity runs)
+   *   --elide-dead    skip the query-suffix copy that nothing reads when the codon pass is off */
+  for (;;) {
+    if (argc > 2 && strcmp(argv[1], "--items") == 0) {
+      items_path = argv[2];
+    } else if (argc > 2 && strcmp(argv[1], "--range") == 0) {
+      if (sscanf(argv[2], "%lld:%lld", &range_a, &range_b) != 2 || range_a < 0 || range_b < range_a)
+        gerror("--range A:B\n");
+    } else if (argc > 1 && strcmp(argv[1], "--elide-dead") == 0) {
+      g_elide_dead = 1;
+      argv[1] = argv[0];
+      argc -= 1;
+      argv += 1;
+      continue;
+    } else {
+      break;
+    }
     argv[2] = argv[0];
     argc -= 2;
     argv += 2;
@@ -1174,6 +1195,12 @@ int main(int argc, char* argv[]) {
   if (args.n_nonopt > 0 && args.nonopt[0][0]) {
     inf = fopen(args.nonopt[0], "r");
     if (!inf) gerror("Cannot open input file %s!\n", args.nonopt[0]);
+  }
+  if (range_b >= 0 && range_a > 0) { /* start after the line break before byte A */
+    if (fseeko(inf, (off_t)(range_a - 1), SEEK_SET) != 0) gerror("--range: cannot seek\n");
+    int c;
+    while ((c = getc(inf)) != EOF && c != '\n') {
+    }
   }
   if (args.set['c'] && args.val['c'][0]) { /* -c clipmax: parsed, never consumed (:217-240) */
     char cbuf[64];
@@ -1239,7 +1266,8 @@ int main(int argc, char* argv[]) {
     fwrite("PWI1", 1, 4, g_items);
   }
   uint64_t line_no = 0;
-  for (; (line = get_line(inf, &lbuf)) != NULL; line_no++, item_end(-1)) { /* :303-436 */
+  for (; (range_b < 0 || ftello(inf) < (off_t)range_b) && (line = get_line(inf, &lbuf)) != NULL;
+       line_no++, item_end(-1)) { /* :303-436 */
     if (g_items) {
       item_begin(line_no);
       freport = g_item_out;

@@ -2,8 +2,9 @@
  * pwsynth.c — deterministic synthetic inputs for tests and bench.py (tooling, not product).
  *
  *   pwsynth paf    --config K [--scale F] [--seed S] --fa out.fa --paf out.paf [knobs]
- *                  (cfg3: [--threads T] [--shard r/N] — per-record random streams, so a shard
- *                  or a multi-threaded run writes exactly the lines of the full file it owns)
+ *                  (cfg3 / cfg4: [--threads T] — per-record random streams, so a multi-threaded
+ *                  run writes the same bytes; cfg3 also [--shard r/N]: a shard writes exactly
+ *                  the lines of the full file it owns)
  *   pwsynth layout --config 5 [--scale F] [--seed S] --out layout.pwl [knobs]
  *
  * PAF records are minimap2-style (`-c --cs`): 12 columns + NM/ms/AS/nn/tp/cm/s1/s2/de/rl/cg/cs
@@ -382,7 +383,7 @@ static void gen_record(const paf_ctx* c, int i, int r, aln_out* a, sbuf* line, s
   if (o->config == 0 && rndu() < o->p_dup) sb_putn(out, line->buf, line->len); /* duplicate q~t pair */
 }
 
-/* cfg3: record k = i * recs + r draws from its own stream (seed, k), so any subset of the
+/* cfg3 / cfg4: record k = i * recs + r draws from its own stream (seed, k), so any subset of the
  * records (a shard) or any split over threads generates the same bytes. */
 typedef struct {
   const paf_ctx* c;
@@ -450,15 +451,15 @@ static int cmd_paf(opts_t* o) {
   fclose(ff);
   paf_ctx c = {o, cds, rcs, clen, recs};
   long long nrec = 0;
-  if (o->config == 3) {
-    for (int i = 0; i < ncds; i++) {  /* reverse complements are generated lazily below */
+  if (o->config == 3 || o->config == 4) { /* per-record streams over worker threads */
+    for (int i = 0; i < ncds; i++) {
       rcs[i] = (char*)malloc((size_t)clen[i] + 1);
       for (int k = 0; k < clen[i]; k++) rcs[i][k] = comp(cds[i][clen[i] - 1 - k]);
       rcs[i][clen[i]] = 0;
     }
     const long long total = (long long)ncds * recs;
     int T = o->threads > 0 ? o->threads : 16;
-    const long long B = 4096;
+    const long long B = o->config == 4 ? 2 : 4096; /* records per job (cfg4 records are Mb each) */
     blk_job* jobs = (blk_job*)calloc((size_t)T, sizeof(blk_job));
     pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
     for (long long k0 = 0; k0 < total; k0 += B * T) {

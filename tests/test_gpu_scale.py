@@ -1,7 +1,8 @@
 """GPU parity at the benchmarked sizes and on the rare device paths.
 
 * cfg2 in full (100k records, -G -C), cfg3 at 100k records, cfg4 at real 1-5 Mb contigs (five
-  records, auto -F, whole report diffed; the smallest also with -G -C), cfg5 at full size
+  records, auto -F, whole report diffed; the smallest also with -G -C; and 1,024 records,
+  ~36 M events, CRC-checked against the chunked oracle), cfg5 at full size
   (200 rows x 1M columns, removeConsGaps=false): HIP CLI vs oracle, byte for byte.
 * cfg4 property checks that do not depend on the oracle: one event line per cs event head after
   the S-merge (pafreport.cpp:556-560), rloc non-decreasing within a record (tdiffs.Reverse()
@@ -86,6 +87,37 @@ def test_cfg4_megabase_contigs(built, tmp_path):
     lines = open(paf).read().splitlines(keepends=True)
     one.write_text(lines[lens.index(min(lens))])
     same(["-G", "-C", "-r", fa, str(one)], timeout=600)
+
+
+def test_cfg4_1k_records(built, tmp_path):
+    """cfg4 at >= 1k Mb-contig records (BASELINE configs[3], scale 0.102: 1,024 records over 32
+    contigs of 1-5 Mb, ~36 M events, auto -F): the CLI's whole report streamed through CRC-32
+    against the oracle over byte ranges of the PAF in parallel processes (bench.oracle_crc), plus
+    the oracle-independent properties on every 64th record."""
+    import subprocess
+    import threading
+
+    from bench import crc_stream, host_threads, oracle_crc
+    fa, paf = synth_paf(tmp_path, 4, seed=4, scale=0.102, extra=["--threads", host_threads()])
+    want = oracle_crc([], fa, paf, host_threads())
+    p = subprocess.Popen([str(CLI), "-r", fa, paf], stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    err = {}
+    th = threading.Thread(target=lambda: err.setdefault("e", p.stderr.read()))
+    th.start()
+    got = crc_stream(p.stdout)
+    rc = p.wait(timeout=300)
+    th.join()
+    assert rc == 0 and err["e"] == b"", err["e"][-2000:]
+    assert got == want[:3], (got, want)
+    assert want[2] > 30_000_000
+    sub = tmp_path / "sub.paf"
+    with open(paf, "rb") as f, open(sub, "wb") as g:
+        for i, line in enumerate(f):
+            if i % 64 == 0:
+                g.write(line)
+    rp, out, ep = run([CLI, "-r", fa, sub])
+    assert rp == 0, ep
+    _check_report_properties(str(sub), out)
 
 
 def test_cfg5_full_layout(built, tmp_path):
