@@ -17,6 +17,23 @@ here as a literal.  Derivations (line refs into /root/reference/pafreport.cpp):
                   (:319-333), self alignment skipped (:314-317), '#' comment (:304).
   kat4_fullgenome - -F: rlabel "q:start-end" (:368-372), codon analysis skipped (:259,915)
                   so each line ends with a tab.
+  kat6_msa_w    - -w progressive MSA (:382-421, 447-450; GapAssem.cpp:605-753 GSeqAlign(s1,s2) /
+                  addAlign / injectGap / addSeq, :1039-1046 + :482-520 writeMSA): query qa aligned
+                  to t1, then qb to t2 (another query: qa's GASeq and MSA are dropped, :338-351,
+                  rseqs never filled), then qa again to t3, t4, t5 — a fresh MSA, the one written
+                  (refMSA = the last query's).  Derivation with qa = AACCGGTTAACC:
+                  t3 ":4-tt:8" / 4M2D8M: rgap (CIGAR D, :689-697) qa.setGap(4,2); GSeqAlign(qa,t3)
+                    length 14.
+                  t4 ":4-ggg:4+a:3" / 4M3D4M1I3M: rseq(qa copy).setGap(4,3); tgap (CIGAR I, :681-688)
+                    at tpos 11: t4.setGap(11,1).  addAlign: i=4 d = 2-3 < 0 -> injectGap(qa,4,1) in the
+                    MSA: alpos = 0+4+2 = 6; qa.addGap(4,1); t3 walks to spos 6 (salpos 7 > 6) ->
+                    t3.addGap(6,1); length 15; t4 added at offset 0.
+                  t5 ":10-c:2" / 10M1D2M: rseq.setGap(10,1).  addAlign: i=4 d = 3-0 > 0 ->
+                    omsa.injectGap(rseq,4,3): t5.addGap(4,3); i=10 d = 0-1 -> injectGap(qa,10,1):
+                    alpos = 0+10+3 = 13; qa.addGap(10,1); t3 walks to spos 12 (its gap at 6 counted)
+                    -> t3.addGap(12,1); t4 to spos 12 (gap at 11) -> t4.addGap(12,1); t5 added.
+                  Rows (all offset 0, forward; finalize changes nothing): qa gaps {4:3, 10:1},
+                  t3 {6:1, 12:1}, t4 {11:1, 12:1}, t5 {4:3}; printMFasta prints '-' per gap.
   err_*         - the reference's error messages (format strings copied from the source
                   lines cited in each case), exit code 1, and report lines printed before it.
 Each case dir holds: q.fa, in.paf, args.json ({"args": [...], "rc": N}), stdout, stderr.
@@ -93,6 +110,21 @@ K4_OUT = (">cds:0-30--asm1:10-41+ coverage:100.00 score=50 edit_distance=2\n"
           "I\t16\t6(K)\t:T\t16\tGGTTTtAAACC\tGTTTAAACC\t[unknown]\t\n")
 
 
+# -w (kat6_msa_w): two queries, qa repeated after qb
+QA = "AACCGGTTAACC"
+FA6 = ">qa\n" + QA + "\n>qb\nGGGGAAAA\n"
+K6 = (paf("qa", 12, 0, 12, "+", "t1", 200, 100, 113, 12, 13, 60, "NM:i:1", "AS:i:10", "cg:Z:6M1D6M", "cs:Z::6-g:6") +
+      paf("qb", 8, 0, 8, "+", "t2", 200, 100, 108, 8, 8, 60, "NM:i:0", "AS:i:16", "cg:Z:8M", "cs:Z::8") +
+      paf("qa", 12, 0, 12, "+", "t3", 200, 100, 114, 12, 14, 60, "NM:i:2", "AS:i:10", "cg:Z:4M2D8M", "cs:Z::4-tt:8") +
+      paf("qa", 12, 0, 12, "+", "t4", 200, 100, 114, 11, 15, 60, "NM:i:4", "AS:i:8", "cg:Z:4M3D4M1I3M",
+          "cs:Z::4-ggg:4+a:3") +
+      paf("qa", 12, 0, 12, "+", "t5", 200, 100, 113, 12, 13, 60, "NM:i:1", "AS:i:12", "cg:Z:10M1D2M", "cs:Z::10-c:2"))
+K6_MSA = (">qa\nAACC---GGTTAA-CC\n"
+          ">t3:100-114+\nAACCtt-GGTTAA-CC\n"
+          ">t4:100-114+\nAACCgggGGTT-A-CC\n"
+          ">t5:100-113+\nAACC---GGTTAAcCC\n")
+
+
 def line(s):
     return s.rstrip("\n")
 
@@ -103,6 +135,7 @@ CASES = {
     "kat2_reverse": (FA1, K2, ["-r", "q.fa", "in.paf"], 0, K2_OUT, ""),
     "kat3_status": (FA3, K3, ["-r", "q.fa", "in.paf"], 0, K3_OUT, K3_ERR),
     "kat4_fullgenome": (FA1, K1, ["-F", "-r", "q.fa", "in.paf"], 0, K4_OUT, ""),
+    "kat6_msa_w": (FA6, K6, ["-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", ""),
     "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
                        K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
     # pafreport.cpp:551-553 base check; records before the failing one are already reported
@@ -172,6 +205,9 @@ def main():
         if name == "kat1_outfile":
             spec["outfile"] = "out.txt"
             spec["outfile_expected"] = K1_OUT
+        if name == "kat6_msa_w":
+            spec["outfile"] = "msa.mfa"
+            spec["outfile_expected"] = K6_MSA
         with open(os.path.join(d, "args.json"), "w") as f:
             json.dump(spec, f, indent=1)
         with open(os.path.join(d, "stdout"), "w") as f:
