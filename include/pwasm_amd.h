@@ -116,7 +116,13 @@ typedef struct pw_report_args {
   uint64_t workspace_bytes;
   uint64_t n_ev_slots;      /* event slots of the batch = sum of pw_cs_totals.n_events_max */
   pw_page* pages;           /* [pw_report_page_count(n_ev_slots)] */
+  uint32_t max_rec_ops;     /* largest desc[].n_ops of the batch, or 0 = unknown.  Records of more
+                               than PW_BLOCK_OPS ops are decoded as blocks of PW_BLOCK_OPS ops by
+                               several wavefronts (block carries from a pre-pass); a value
+                               <= PW_BLOCK_OPS lets the pass skip that pre-pass. */
+  uint32_t reserved;        /* 0 */
 } pw_report_args;
+#define PW_BLOCK_OPS 2048
 
 /* Pages of a batch with n_ev_slots event slots, and the text capacity that always suffices:
  * the page area plus an arena of text_bound bytes (sum of pw_cs_totals.text_bound). */
@@ -361,6 +367,38 @@ pw_batch* pw_batch_from_files_shard(const char* fasta, const char* paf, uint32_t
  * err_path (NULL = stderr).  Returns the exit code the single-process run ends with (>= 0) or a
  * negative PW_E_* status. */
 int pw_items_merge(const char* const* paths, uint32_t n, const char* out_path, const char* err_path);
+
+/* Scalable host path of the multi-GPU driver (pwasm_amd/mgpu.py):
+ * pw_paf_split: rank r reads only the PAF lines that START in bytes [lo, hi) of the file (a line
+ *   starts at byte 0 or after a '\n'; lines are cut as the CLI cuts them: \n, \r or \r\n) and
+ *   routes each to the rank owning its target genome (the shard rule above); every line, comments
+ *   included, keeps its index in the range, so global line = (lines of the ranges before) + index.
+ *   Getters: lines in the range; per owner the bytes (its lines, each ended by '\n') and the count.
+ * pw_batch_from_buffer: a batch from received lines (n_lines lines ended by '\n' in text, global
+ *   input lines in line_no, ascending) — the pre-pass of pw_batch_from_files without the file.  prev
+ *   (or NULL): the batch of the lines before these; its gene-mode q~t dedupe state moves over
+ *   (pafreport.cpp:319-334), so a rank's lines can be packed batch by batch.
+ * pw_batch_items / pw_batch_write_at: the batch's output items (log items up to the first that
+ *   ends the run, as in pw_batch_write_items): global line, status (-1 = continue, else the exit
+ *   code), stdout / stderr byte counts; then the stdout bytes of the first n_items written with
+ *   pwrite at out_off[k] of fd (ranks write disjoint ranges of one output file, the offsets from an
+ *   exclusive scan of all ranks' per-line byte counts) and their stderr bytes, back to back, into
+ *   err_buf (capacity err_cap). */
+typedef struct pw_split pw_split;
+pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uint32_t nshards, char* errbuf, size_t errlen);
+uint64_t pw_split_lines(const pw_split* sp);
+uint64_t pw_split_bytes(const pw_split* sp, uint32_t owner);
+uint64_t pw_split_count(const pw_split* sp, uint32_t owner);
+int pw_split_get(const pw_split* sp, uint32_t owner, char* bytes, uint32_t* local_lines);
+void pw_split_free(pw_split* sp);
+pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, uint64_t len, const uint64_t* line_no,
+                               uint64_t n_lines, uint32_t flags, pw_batch* prev, char* errbuf, size_t errlen);
+uint64_t pw_batch_item_count(const pw_batch* b);
+int pw_batch_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host, const pw_page* pages_host,
+                   uint64_t* line, int32_t* status, uint64_t* out_len, uint64_t* err_len, uint64_t* n_items);
+int pw_batch_write_at(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
+                      const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items, char* err_buf,
+                      uint64_t err_cap);
 
 /* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
  * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its

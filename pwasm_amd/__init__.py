@@ -68,7 +68,8 @@ class ReportArgs(ctypes.Structure):
                 ("next_stop", ctypes.c_void_p), ("text", ctypes.c_void_p), ("results", ctypes.c_void_p),
                 ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
-                ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p)]
+                ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p), ("max_rec_ops", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class CsTotals(ctypes.Structure):
@@ -153,6 +154,20 @@ _SIGS = {
                                                     ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
     "pw_items_merge": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32, ctypes.c_char_p,
                                       ctypes.c_char_p]),
+    "pw_paf_split": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_char_p, ctypes.c_size_t]),
+    "pw_split_lines": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "pw_split_bytes": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32]),
+    "pw_split_count": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32]),
+    "pw_split_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "pw_split_free": (None, [ctypes.c_void_p]),
+    "pw_batch_from_buffer": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                               ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_char_p,
+                                               ctypes.c_size_t]),
+    "pw_batch_item_count": (ctypes.c_uint64, [ctypes.c_void_p]),
+    "pw_batch_items": (ctypes.c_int, [ctypes.c_void_p] * 8 + [ctypes.POINTER(ctypes.c_uint64)]),
+    "pw_batch_write_at": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                                                 ctypes.c_void_p, ctypes.c_uint64]),
     "pw_batch_genomes": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -225,20 +240,91 @@ def pack_cs_gpu(cs_list, offsets, qlens, device: str = "cuda:0"):
     return d_ops.cpu().numpy().view(np.uint32), d_lits.cpu().numpy(), off, recs
 
 
+def paf_split(paf: str, lo: int, hi: int, nshards: int):
+    """pw_paf_split: the lines starting in bytes [lo, hi) of the PAF routed to their target-genome
+    shards -> (lines in the range, [bytes uint8 per owner], [index in the range uint32 per owner])."""
+    L = lib()
+    err = ctypes.create_string_buffer(4096)
+    h = L.pw_paf_split(str(paf).encode(), lo, hi, nshards, err, 4096)
+    if not h:
+        raise RuntimeError("pw_paf_split: " + err.value.decode(errors="replace"))
+    try:
+        n = int(L.pw_split_lines(h))
+        data, idx = [], []
+        for o in range(nshards):
+            b = np.empty(int(L.pw_split_bytes(h, o)), dtype=np.uint8)
+            i = np.empty(int(L.pw_split_count(h, o)), dtype=np.uint32)
+            if L.pw_split_get(h, o, b.ctypes.data, i.ctypes.data) != 0:
+                raise RuntimeError("pw_split_get failed")
+            data.append(b)
+            idx.append(i)
+        return n, data, idx
+    finally:
+        L.pw_split_free(h)
+
+
 class HostBatch:
     """A PAF batch packed by the C++ pre-pass (pw_batch_from_files), arrays viewable as numpy."""
 
-    def __init__(self, fasta: str, paf: str, flags: int = 0, shard: int = 0, nshards: int = 1):
+    def __init__(self, fasta: str, paf: str = None, flags: int = 0, shard: int = 0, nshards: int = 1, _handle=None):
         """shard / nshards: pack only this rank's lines (target-name hash, pw_batch_from_files_shard)."""
         L = lib()
-        err = ctypes.create_string_buffer(4096)
-        h = L.pw_batch_from_files_shard(fasta.encode(), paf.encode(), flags, shard, nshards, err, 4096)
-        if not h:
-            raise RuntimeError("pw_batch_from_files: " + err.value.decode(errors="replace"))
+        if _handle is None:
+            err = ctypes.create_string_buffer(4096)
+            h = L.pw_batch_from_files_shard(fasta.encode(), paf.encode(), flags, shard, nshards, err, 4096)
+            if not h:
+                raise RuntimeError("pw_batch_from_files: " + err.value.decode(errors="replace"))
+        else:
+            h = _handle
         self._h = h
         self.view = BatchView()
         if L.pw_batch_view_get(h, ctypes.byref(self.view)) != 0:
             raise RuntimeError("pw_batch_view_get failed")
+
+    @classmethod
+    def from_buffer(cls, fasta: str, text, line_no, flags: int = 0, prev=None):
+        """pw_batch_from_buffer: lines ended by '\\n' in `text` (uint8 array) with their global input
+        lines `line_no` (uint64, ascending); prev = the batch of the lines before (its q~t dedupe
+        state moves over)."""
+        L = lib()
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        line_no = np.ascontiguousarray(line_no, dtype=np.uint64)
+        err = ctypes.create_string_buffer(4096)
+        h = L.pw_batch_from_buffer(fasta.encode(), text.ctypes.data if text.size else None, text.size,
+                                   line_no.ctypes.data if line_no.size else None, line_no.size, flags,
+                                   prev._h if prev is not None else None, err, 4096)
+        if not h:
+            raise RuntimeError("pw_batch_from_buffer: " + err.value.decode(errors="replace"))
+        return cls(fasta, _handle=h)
+
+    def items(self, text_host, results_host, pages_host):
+        """Output items (global line, status, stdout bytes, stderr bytes) up to the first that ends
+        the run (pw_batch_items)."""
+        L = lib()
+        n = int(L.pw_batch_item_count(self._h))
+        line = np.zeros(max(n, 1), dtype=np.uint64)
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        on = np.zeros(max(n, 1), dtype=np.uint64)
+        en = np.zeros(max(n, 1), dtype=np.uint64)
+        k = ctypes.c_uint64(0)
+        rc = L.pw_batch_items(self._h, text_host.ctypes.data, results_host.ctypes.data, pages_host.ctypes.data,
+                              line.ctypes.data, st.ctypes.data, on.ctypes.data, en.ctypes.data, ctypes.byref(k))
+        if rc != 0:
+            raise RuntimeError(f"pw_batch_items: {rc}")
+        k = int(k.value)
+        return line[:k], st[:k], on[:k], en[:k]
+
+    def write_at(self, text_host, results_host, pages_host, fd: int, out_off, err_bytes: int) -> bytes:
+        """pw_batch_write_at: stdout of the first len(out_off) items pwritten at out_off into fd; returns
+        their stderr bytes."""
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+        eb = ctypes.create_string_buffer(max(int(err_bytes), 1))
+        rc = lib().pw_batch_write_at(self._h, text_host.ctypes.data, results_host.ctypes.data, pages_host.ctypes.data,
+                                     fd, out_off.ctypes.data if out_off.size else None, out_off.size, eb,
+                                     int(err_bytes))
+        if rc != 0:
+            raise RuntimeError(f"pw_batch_write_at: {rc}")
+        return eb.raw[: int(err_bytes)]
 
     def array(self, name: str):
         import numpy as np
@@ -253,6 +339,13 @@ class HostBatch:
         ct = np.ctypeslib.as_ctypes_type(dt)
         buf = (ct * int(n)).from_address(int(ptr))
         return np.ctypeslib.as_array(buf).copy()
+
+    def max_rec_ops(self) -> int:
+        """Largest op count of a record (pw_report_args.max_rec_ops)."""
+        if getattr(self, "_max_ops", None) is None:
+            d = self.array("desc").view(np.uint32).reshape(-1, 8)
+            self._max_ops = int(d[:, 1].max()) if d.size else 0
+        return self._max_ops
 
     def write_report(self, text_host, results_host, pages_host, path: str) -> int:
         """Headers + event text for a finished batch (numpy arrays on the host)."""
@@ -325,6 +418,7 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     a.workspace_bytes = dev["work"].numel()
     a.n_ev_slots = int(v.n_events_max)
     a.pages = dev["pages"].data_ptr()
+    a.max_rec_ops = batch.max_rec_ops()
     return a
 
 
@@ -341,6 +435,17 @@ def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
     rc = L.pw_report_events(ctypes.byref(a), stream_ptr)
     if rc != 0:
         raise RuntimeError(f"pw_report_events: {rc}")
+
+
+def fetch_outputs(dev: dict):
+    """Host copies of a finished pass: (text up to its last used byte, results, pages) as numpy."""
+    res = dev["results"].cpu().numpy()
+    pages = dev["pages"].cpu().numpy()
+    pg = pages.view(np.uint8)[: pages.size - pages.size % 16].view(np.dtype([("off", "<u8"), ("len", "<u4"),
+                                                                              ("pad", "<u4")]))
+    used = int((pg["off"] + pg["len"]).max()) if pg.size else 0
+    text = dev["text"][: max(used, 1)].cpu().numpy()
+    return text, res, pages
 
 
 def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:

@@ -9,7 +9,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <sched.h>
 
@@ -426,6 +428,7 @@ struct Batch {
   PodVec<char> buf;
   PodVec<LineRef> lines;
   uint64_t line0 = 0;   // global input line of lines[0]
+  PodVec<uint64_t> line_no;  // (multi-GPU exchange) the global input line of each line, when set
   PodVec<char> hdr;     // report headers
   std::vector<std::string> msgs;
   PodVec<LogItem> log;
@@ -699,7 +702,7 @@ struct Packer {
       for (int k; (k = next.fetch_add(1)) < np;) {
         Batch& p = parts[(size_t)k];
         for (size_t i = cut[(size_t)k]; i < cut[(size_t)k + 1] && !p.fatal; i++) {
-          p.cur_line = b.line0 + i;
+          p.cur_line = b.line_no.empty() ? b.line0 + i : b.line_no[i];
           pack_line(p, b.buf.data(), b.lines[i], info[i], fs);
         }
       }
@@ -1195,6 +1198,9 @@ struct Device {
     a.workspace_bytes = pw_report_workspace_bytes(b.n_events_max, na);
     a.n_ev_slots = b.n_events_max;
     a.pages = pages.p;
+    a.max_rec_ops = 0;
+    for (const pw_aln_desc& d : b.desc) a.max_rec_ops = d.n_ops > a.max_rec_ops ? d.n_ops : a.max_rec_ops;
+    a.reserved = 0;
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
       return false;
@@ -1917,6 +1923,310 @@ extern "C" int pw_items_merge(const char* const* paths, uint32_t n, const char* 
   else if (out) fflush(out);
   if (err && err != stderr) fclose(err);
   return ret;
+}
+
+// ----------------------------------------------------------------- multi-GPU host path
+// Byte-range split of the PAF: the lines that START in [lo, hi) (a line starts at byte 0 or after a
+// '\n'), cut into lines as ChunkReader does, each routed to the rank that owns its target genome
+// (the classify() shard rule: crc32 of column 6 mod nshards; fewer than six tabs -> 0; comment
+// lines -> nobody, though they are counted: every line keeps its index in the range).
+struct pw_split {
+  uint64_t n_lines = 0;
+  std::vector<std::string> bytes;               // per owner: its lines, each ended by '\n'
+  std::vector<std::vector<uint32_t>> local;     // per owner: the lines' indices in the range
+};
+
+extern "C" pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uint32_t nshards, char* errbuf,
+                                  size_t errlen) {
+  auto fail = [&](const std::string& m) -> pw_split* {
+    if (errbuf && errlen) snprintf(errbuf, errlen, "%s", m.c_str());
+    return nullptr;
+  };
+  if (!paf || nshards == 0 || hi < lo) return fail("bad arguments");
+  const int fd = open(paf, O_RDONLY);
+  if (fd < 0) return fail(strf("cannot open %s", paf));
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return fail(strf("cannot stat %s", paf));
+  }
+  const uint64_t size = (uint64_t)st.st_size;
+  if (hi > size) hi = size;
+  if (lo > hi) lo = hi;
+  // [start, end): from the first line start >= lo to the first line start >= hi
+  auto line_start_at = [&](uint64_t x) -> uint64_t {
+    if (x == 0) return 0;
+    if (x >= size) return size;
+    char buf[1 << 16];
+    uint64_t p = x - 1;  // a line starts at x iff byte x-1 is '\n'
+    while (p < size) {
+      const ssize_t k = pread(fd, buf, sizeof buf, (off_t)p);
+      if (k <= 0) return size;
+      const char* q = (const char*)memchr(buf, '\n', (size_t)k);
+      if (q) return p + (uint64_t)(q - buf) + 1;
+      p += (uint64_t)k;
+    }
+    return size;
+  };
+  const uint64_t start = line_start_at(lo), end = line_start_at(hi);
+  pw_split* sp = new pw_split();
+  sp->bytes.resize(nshards);
+  sp->local.resize(nshards);
+  std::vector<char> data((size_t)(end - start) + 1);
+  for (uint64_t got = 0; got < end - start;) {
+    const ssize_t k = pread(fd, data.data() + got, (size_t)(end - start - got), (off_t)(start + got));
+    if (k <= 0) {
+      close(fd);
+      delete sp;
+      return fail(strf("cannot read %s", paf));
+    }
+    got += (uint64_t)k;
+  }
+  close(fd);
+  const size_t n = (size_t)(end - start);
+  // threads take sub-ranges cut after a '\n' (line splitting is local to such a cut)
+  const int nt = std::max(1, std::min<int>(host_threads(), (int)(n >> 20) + 1));
+  std::vector<size_t> cut((size_t)nt + 1, n);
+  cut[0] = 0;
+  for (int t = 1; t < nt; t++) {
+    size_t x = n * (size_t)t / (size_t)nt;
+    if (x < cut[(size_t)t - 1]) x = cut[(size_t)t - 1];
+    const char* q = x < n ? (const char*)memchr(data.data() + x, '\n', n - x) : nullptr;
+    cut[(size_t)t] = q ? (size_t)(q - data.data()) + 1 : n;
+  }
+  struct Part {
+    std::vector<std::string> bytes;
+    std::vector<std::vector<uint32_t>> local;
+    uint64_t lines = 0;
+  };
+  std::vector<Part> parts((size_t)nt);
+  parallel_for(nt, [&](int t) {
+    Part& pt = parts[(size_t)t];
+    pt.bytes.resize(nshards);
+    pt.local.resize(nshards);
+    const char* s = data.data();
+    const size_t a = cut[(size_t)t], b = cut[(size_t)t + 1];
+    const bool has_cr = memchr(s + a, '\r', b - a) != nullptr;
+    size_t p = a;
+    std::vector<std::pair<size_t, size_t>> ls;  // this sub-range's lines
+    while (p < b) {
+      size_t e;
+      if (!has_cr) {
+        const char* q = (const char*)memchr(s + p, '\n', b - p);
+        e = q ? (size_t)(q - s) : b;
+      } else {
+        e = p;
+        while (e < b && s[e] != '\n' && s[e] != '\r') e++;
+      }
+      if (e == b && e == p) break;
+      ls.push_back({p, e});
+      size_t nx = e + 1;
+      if (e < b && s[e] == '\r' && e + 1 < b && s[e + 1] == '\n') nx = e + 2;
+      p = nx;
+    }
+    pt.lines = ls.size();
+    for (size_t i = 0; i < ls.size(); i++) {
+      const char* l = s + ls[i].first;
+      const size_t ln = ls[i].second - ls[i].first;
+      if (ln > 0 && l[0] == '#') continue;
+      uint32_t owner = 0;
+      if (nshards > 1) {
+        const char* t5 = nullptr;
+        size_t t5n = 0;
+        int tabs = 0;
+        for (size_t k = 0; k < ln; k++)
+          if (l[k] == '\t') {
+            tabs++;
+            if (tabs == 5) t5 = l + k + 1;
+            if (tabs == 6) {
+              t5n = (size_t)(l + k - t5);
+              break;
+            }
+          }
+        owner = tabs >= 6 ? crc32_ieee(t5, t5n) % nshards : 0u;
+      }
+      pt.bytes[owner].append(l, ln);
+      pt.bytes[owner].push_back('\n');
+      pt.local[owner].push_back((uint32_t)i);  // (rebased below)
+    }
+  });
+  uint64_t base = 0;
+  for (auto& pt : parts) {
+    for (uint32_t o = 0; o < nshards; o++) {
+      sp->bytes[o] += pt.bytes[o];
+      for (uint32_t x : pt.local[o]) sp->local[o].push_back((uint32_t)(base + x));
+    }
+    base += pt.lines;
+  }
+  sp->n_lines = base;
+  return sp;
+}
+extern "C" uint64_t pw_split_lines(const pw_split* sp) { return sp ? sp->n_lines : 0; }
+extern "C" uint64_t pw_split_bytes(const pw_split* sp, uint32_t owner) {
+  return sp && owner < sp->bytes.size() ? sp->bytes[owner].size() : 0;
+}
+extern "C" uint64_t pw_split_count(const pw_split* sp, uint32_t owner) {
+  return sp && owner < sp->local.size() ? sp->local[owner].size() : 0;
+}
+extern "C" int pw_split_get(const pw_split* sp, uint32_t owner, char* bytes, uint32_t* local_lines) {
+  if (!sp || owner >= sp->bytes.size()) return PW_E_ARG;
+  if (bytes && !sp->bytes[owner].empty()) memcpy(bytes, sp->bytes[owner].data(), sp->bytes[owner].size());
+  if (local_lines && !sp->local[owner].empty())
+    memcpy(local_lines, sp->local[owner].data(), sp->local[owner].size() * 4);
+  return PW_OK;
+}
+extern "C" void pw_split_free(pw_split* sp) { delete sp; }
+
+// A batch from lines already in memory (the lines a rank received in the exchange): text holds
+// n_lines lines, each ended by '\n', with their global input lines in line_no (ascending).
+extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, uint64_t len, const uint64_t* line_no,
+                                          uint64_t n_lines, uint32_t flags, pw_batch* prev, char* errbuf,
+                                          size_t errlen) {
+  auto fail = [&](const std::string& m) -> pw_batch* {
+    if (errbuf && errlen) snprintf(errbuf, errlen, "%s", m.c_str());
+    return nullptr;
+  };
+  if (!fasta || (len && !text) || (n_lines && !line_no)) return fail("bad arguments");
+  pw_batch* bt = new pw_batch();
+  std::string err;
+  if (!bt->q.load(fasta, err)) {
+    delete bt;
+    return fail(err);
+  }
+  struct stat st;
+  const long long fsize = (stat(fasta, &st) == 0) ? (long long)st.st_size : -1;
+  bool gene = flags & 1u, full = flags & 2u, fc = flags & 4u, fn = flags & 8u;
+  if (!full && !gene && fsize > 120000) full = true;
+  bool skip = full || fn;
+  if (!skip && !fc && fsize > 120000) skip = true;
+  bt->skip_codan = skip;
+  bt->pk.qdb = &bt->q;
+  bt->pk.nt = host_threads();
+  bt->pk.opt.fullgenome = full;
+  bt->pk.opt.skip_codan = skip;
+  bt->pk.opt.single_query_gene = (bt->q.ids.size() == 1 && !full);
+  bt->pk.opt.msa = false;
+  if (prev) {  // the next batch of the same input: the q~t pairs seen so far move over
+    bt->pk.alnpairs = std::move(prev->pk.alnpairs);
+    bt->pk.n_lines = prev->pk.n_lines;
+  }
+  Batch& b = bt->b;
+  b.buf.resize((size_t)len + 1);
+  if (len) memcpy(b.buf.data(), text, (size_t)len);
+  b.buf[(size_t)len] = '\0';
+  char* s = b.buf.data();
+  size_t p = 0;
+  while (p < len) {
+    const char* q = (const char*)memchr(s + p, '\n', (size_t)len - p);
+    const size_t e = q ? (size_t)(q - s) : (size_t)len;
+    b.lines.push_back({p, (uint32_t)(e - p)});
+    s[e] = '\0';
+    p = e + 1;
+  }
+  if (b.lines.size() != n_lines) {
+    delete bt;
+    return fail(strf("line count mismatch (%zu vs %llu)", b.lines.size(), (unsigned long long)n_lines));
+  }
+  b.line_no.resize((size_t)n_lines);
+  if (n_lines) memcpy(b.line_no.data(), line_no, (size_t)n_lines * 8);
+  if (n_lines) bt->pk.pack(b);
+  bt->alg_in = alg_bytes(b, bt->q, skip);
+  return bt;
+}
+
+// Output items of a finished batch (the log items up to and including the first one that ends the
+// run, as pw_batch_write_items): their global line, status (-1 = continue, else the exit code) and
+// the bytes each writes to stdout / stderr.
+namespace {
+struct CountCookie {
+  uint64_t n = 0;
+};
+ssize_t count_write(void* c, const char*, size_t n) {
+  static_cast<CountCookie*>(c)->n += n;
+  return (ssize_t)n;
+}
+struct PwriteCookie {
+  int fd;
+  uint64_t off;
+  bool bad = false;
+};
+ssize_t pwrite_write(void* c, const char* buf, size_t n) {
+  PwriteCookie* k = static_cast<PwriteCookie*>(c);
+  size_t done = 0;
+  while (done < n) {
+    const ssize_t w = pwrite(k->fd, buf + done, n - done, (off_t)(k->off + done));
+    if (w <= 0) {
+      k->bad = true;
+      return done ? (ssize_t)done : -1;
+    }
+    done += (size_t)w;
+  }
+  k->off += n;
+  return (ssize_t)n;
+}
+}  // namespace
+
+extern "C" uint64_t pw_batch_item_count(const pw_batch* bt) { return bt ? bt->b.log.size() : 0; }
+
+extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                              const pw_page* pages_host, uint64_t* line, int32_t* status, uint64_t* out_len,
+                              uint64_t* err_len, uint64_t* n_items) {
+  if (!bt || !n_items) return PW_E_ARG;
+  TextSrc src;
+  src.host = text_host;
+  uint64_t k = 0;
+  for (const LogItem& it : bt->b.log) {
+    CountCookie co, ce;
+    FILE* o = fopencookie(&co, "w", cookie_io_functions_t{nullptr, count_write, nullptr, nullptr});
+    FILE* e = fopencookie(&ce, "w", cookie_io_functions_t{nullptr, count_write, nullptr, nullptr});
+    if (!o || !e) {
+      if (o) fclose(o);
+      if (e) fclose(e);
+      return PW_E_NOMEM;
+    }
+    const int32_t st = emit_item(bt->b, it, src, res_host, pages_host, o, e);
+    fclose(o);
+    fclose(e);
+    if (line) line[k] = it.line;
+    if (status) status[k] = st;
+    if (out_len) out_len[k] = co.n;
+    if (err_len) err_len[k] = ce.n;
+    k++;
+    if (st >= 0) break;
+  }
+  *n_items = k;
+  return PW_OK;
+}
+
+// Write the stdout bytes of the batch's first n_items items at out_off[k] of fd (pwrite: ranks
+// write disjoint ranges of one file) and their stderr bytes back to back into err_buf.
+extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                                 const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items,
+                                 char* err_buf, uint64_t err_cap) {
+  if (!bt || (n_items && !out_off) || n_items > bt->b.log.size()) return PW_E_ARG;
+  TextSrc src;
+  src.host = text_host;
+  uint64_t eo = 0;
+  for (uint64_t k = 0; k < n_items; k++) {
+    PwriteCookie pc{fd, out_off[k]};
+    FILE* o = fopencookie(&pc, "w", cookie_io_functions_t{nullptr, pwrite_write, nullptr, nullptr});
+    char* eb = nullptr;
+    size_t en = 0;
+    FILE* e = open_memstream(&eb, &en);
+    if (!o || !e) {
+      if (o) fclose(o);
+      if (e) fclose(e);
+      return PW_E_NOMEM;
+    }
+    emit_item(bt->b, bt->b.log[(size_t)k], src, res_host, pages_host, o, e);
+    fclose(o);
+    fclose(e);
+    if (en && err_buf && eo + en <= err_cap) memcpy(err_buf + eo, eb, en);
+    eo += en;
+    free(eb);
+    if (pc.bad) return PW_E_IO;
+  }
+  return eo <= err_cap || !err_buf ? PW_OK : PW_E_ARG;
 }
 
 extern "C" void pw_batch_free(pw_batch* bt) { delete bt; }

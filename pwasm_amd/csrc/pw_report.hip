@@ -1011,9 +1011,18 @@ struct Work {
   uint8_t* sflag;
   Fixup* fix;         // per slot: the destination of a long line (written only for long lines)
   uint64_t* lmask;    // per chunk: lanes whose line is longer than the LDS line buffer
+  // records of more than kBlkOps ops, decoded block by block (plan_kernel / carry_kernel):
+  uint32_t* rec_blk;  // per record: its first entry in blist, or kNoBlk
+  uint32_t* rec_bad;  // per record: the first block (>= 1) with a base mismatch (atomicMin), or kNoBlk
+  uint64_t* blist;    // entries record << 32 | block, a record's blocks consecutive
+  v4u* bcarry;        // per entry: query / target / literal advance and event heads of the block
+  v4u* berr;          // per entry (blocks >= 1): mismatch details {err, q_pos, query char, aligned char}
+  uint32_t blk_cap;
   uint64_t n_slots, n_chunks;
   uint64_t arena0;  // first arena byte in text (= n_chunks * PW_PAGE_BYTES)
 };
+constexpr int kBlkOps = PW_BLOCK_OPS;   // ops per block of a long record (16 segments)
+constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
 
 __host__ __device__ inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
@@ -1036,6 +1045,18 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
   o = align_up(o + sizeof(Fixup) * ns, 256);
   const uint64_t o_lmask = o;
   o = align_up(o + 8 * (n_chunks ? n_chunks : 1), 256);
+  // block list capacity: a record of n > kBlkOps ops has ceil(n / kBlkOps) < 2n / kBlkOps blocks,
+  // and a well-formed record has n <= 2 * (its event slots) + 1 ops; a record that does not get
+  // room is decoded by one wavefront
+  const uint64_t bcap = 4 * (n_slots + n_alns) / kBlkOps + 64;
+  const uint64_t o_rblk = o;
+  o = align_up(o + 8 * n_alns, 256);
+  const uint64_t o_blist = o;
+  o = align_up(o + 8 * bcap, 256);
+  const uint64_t o_bcarry = o;
+  o = align_up(o + 16 * bcap, 256);
+  const uint64_t o_berr = o;
+  o = align_up(o + 16 * bcap, 256);
   if (w && base) {
     w->ctr = reinterpret_cast<uint32_t*>(base);
     w->arena_used = reinterpret_cast<unsigned long long*>(base + 16);
@@ -1046,6 +1067,12 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->sflag = base + o_sflag;
     w->fix = reinterpret_cast<Fixup*>(base + o_fix);
     w->lmask = reinterpret_cast<uint64_t*>(base + o_lmask);
+    w->rec_blk = reinterpret_cast<uint32_t*>(base + o_rblk);
+    w->rec_bad = w->rec_blk + n_alns;
+    w->blist = reinterpret_cast<uint64_t*>(base + o_blist);
+    w->bcarry = reinterpret_cast<v4u*>(base + o_bcarry);
+    w->berr = reinterpret_cast<v4u*>(base + o_berr);
+    w->blk_cap = (uint32_t)(bcap < 0xFFFFFFF0ull ? bcap : 0xFFFFFFF0ull);
     w->n_slots = n_slots;
     w->n_chunks = n_chunks;
     w->arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
@@ -1139,8 +1166,69 @@ __device__ __forceinline__ pw_aln_desc unpack_desc(const DescRaw& r) {
   return d;
 }
 
+// The op range a wavefront decodes: a whole record, or one block of a record of more than
+// kBlkOps ops (its coordinates and event count at the block start from carry_kernel's totals of
+// the blocks before it; the record's event count is then known up front, so its last line is
+// flagged when written).
+struct IdxBlk {
+  uint32_t sb0, sb1;   // ops [sb0, sb1) of the record
+  int qc, tc;          // query / target position at sb0
+  uint32_t lc;         // literal index at sb0
+  uint32_t ev0;        // events created before sb0
+  uint32_t ev1;        // ... before sb1 (blocked)
+  uint32_t tot;        // events of the record (blocked)
+  uint32_t k, bidx;    // block index in the record, its blist entry
+  bool prev_sub;       // the op before sb0 is a '*'
+  bool blocked;
+};
+__device__ __forceinline__ IdxBlk whole_record(const pw_aln_desc& d) {
+  IdxBlk B;
+  B.sb0 = 0;
+  B.sb1 = d.n_ops;
+  B.qc = B.tc = 0;
+  B.lc = d.lit_begin;
+  B.ev0 = B.ev1 = B.tot = 0;
+  B.k = B.bidx = 0;
+  B.prev_sub = false;
+  B.blocked = false;
+  return B;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return wave_last(wave_scan_incl(v)); }
+// block k of a record whose blocks are blist entries [base, base + nb): prefix of the carries
+__device__ __forceinline__ IdxBlk block_of(const Work& W, const pw_aln_desc& d, uint32_t base, uint32_t nb, uint32_t k,
+                                          int lane) {
+  IdxBlk B;
+  uint32_t q = 0, t = 0, l = 0, e = 0, tot = 0, ek = 0;
+  for (uint32_t j0 = 0; j0 < nb; j0 += kWave) {
+    const uint32_t j = j0 + (uint32_t)lane;
+    v4u c = W.bcarry[base + (j < nb ? j : 0u)];
+    if (j >= nb) c = (v4u){0u, 0u, 0u, 0u};
+    const bool b = j < k;
+    q += wave_sum(b ? c.x : 0u);
+    t += wave_sum(b ? c.y : 0u);
+    l += wave_sum(b ? c.z : 0u);
+    e += wave_sum(b ? c.w : 0u);
+    ek += wave_sum(j == k ? c.w : 0u);
+    tot += wave_sum(c.w);
+  }
+  B.sb0 = k * (uint32_t)kBlkOps;
+  B.sb1 = d.n_ops - B.sb0 < (uint32_t)kBlkOps ? d.n_ops : B.sb0 + (uint32_t)kBlkOps;
+  B.qc = (int)q;
+  B.tc = (int)t;
+  B.lc = d.lit_begin + l;
+  B.ev0 = e;
+  B.ev1 = e + ek;
+  B.tot = tot;
+  B.k = k;
+  B.bidx = base + k;
+  B.prev_sub = false;  // (set by the caller from the op before sb0)
+  B.blocked = true;
+  return B;
+}
+
 __device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
-                                             LDS IndexWave* w, uint32_t ai, int lane, const RecPre& pre) {
+                                             LDS IndexWave* w, uint32_t ai, int lane, const RecPre& pre,
+                                             const IdxBlk& B) {
   const pw_aln_desc d = pre.d;
   const uint32_t* ops = A.ops + d.op_begin;
   const uint64_t qb = pre.qb;
@@ -1157,14 +1245,14 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   const uint32_t nmax = layout_ok ? (uint32_t)(ev_next - evb) : 0u;
   const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
 
-  int qc = 0, tc = 0;
-  uint32_t lc = d.lit_begin;
-  bool prev_sub = false;
-  uint32_t ev = 0, ev_last_seg = 0;  // events created; by the last segment processed
+  int qc = B.qc, tc = B.tc;
+  uint32_t lc = B.lc;
+  bool prev_sub = B.prev_sub;
+  uint32_t ev = B.ev0, ev_last_seg = 0;  // events created; by the last segment processed
   int err = layout_ok ? PW_REC_OK : PW_REC_LAYOUT, err_a = 0, err_b = 0, err_c = 0;
 
-  for (uint32_t sb = 0; layout_ok && sb < n_ops; sb += kSegOps) {
-    const uint32_t nseg = (n_ops - sb) < (uint32_t)kSegOps ? (n_ops - sb) : (uint32_t)kSegOps;
+  for (uint32_t sb = B.sb0; layout_ok && sb < B.sb1; sb += kSegOps) {
+    const uint32_t nseg = (B.sb1 - sb) < (uint32_t)kSegOps ? (B.sb1 - sb) : (uint32_t)kSegOps;
     const bool two = nseg > (uint32_t)kWave;  // (uniform) a segment of <= 64 ops skips its empty second half
     // ---- op words (2 per lane) + wave scans of the query / target / literal advances
     uint32_t wd[2];
@@ -1321,7 +1409,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           // first / last line of the record in output order: the first created event, and the
           // last created one when this is the record's last segment (else flagged once the
           // record is done, below)
-          const bool lastc = fin && kidx + 1 == ev + nev;
+          const bool lastc = B.blocked ? kidx + 1 == B.tot : (fin && kidx + 1 == ev + nev);
           const bool first = rev ? lastc : kidx == 0, last = rev ? kidx == 0 : lastc;
           Hot hh;
           hh.qb = (uint32_t)(qb >> 4);
@@ -1361,6 +1449,38 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     tc += (int)ttot;
     lc += ltot;
     wave_sync();
+  }
+  if (B.blocked) {
+    // slots nobody writes: this block's after a mismatch, and (last block) those past the
+    // record's last event; creation index e sits in slot evb + e ('+') or evb + nmax - 1 - e ('-')
+    const uint32_t f0 = ev < nmax ? ev : nmax, f1 = B.ev1 < nmax ? B.ev1 : nmax;
+    if (f1 > f0) {
+      const uint64_t a0 = rev ? evb + nmax - f1 : evb + f0, a1 = rev ? evb + nmax - f0 : evb + f1;
+      for (uint64_t s = a0 + lane; s < a1; s += kWave) W.hot[s].fn = kNoEv;
+    }
+    if (B.sb1 == n_ops && B.tot < nmax) {
+      const uint64_t a0 = rev ? evb : evb + B.tot, a1 = rev ? evb + nmax - B.tot : evb + nmax;
+      for (uint64_t s = a0 + lane; s < a1; s += kWave) W.hot[s].fn = kNoEv;
+    }
+    if (lane == 0) {
+      if (B.k == 0) {
+        pw_aln_result res;
+        res.text_off = res.text_end = 0;
+        res.page_first = res.page_last = 0;
+        res.text_len = 0;
+        res.n_events = B.tot < nmax ? B.tot : nmax;
+        res.err = err == PW_REC_OK && B.tot > nmax ? PW_REC_OVERFLOW : err;
+        res.err_a = err_a;
+        res.err_b = err_b;
+        res.err_c = err_c;
+        A.results[ai] = res;
+        W.rec_mod[ai] = ~0ull;
+      } else if (err != PW_REC_OK) {  // (finalize_kernel takes the first failing block)
+        W.berr[B.bidx] = (v4u){(uint32_t)err, (uint32_t)err_a, (uint32_t)err_b, (uint32_t)err_c};
+        atomicMin(&W.rec_bad[ai], B.k);
+      }
+    }
+    return;
   }
   const bool ev_over = ev > nmax;
   if (ev_over) {  // host event bound violated (cannot happen: every head is a counted op)
@@ -1404,6 +1524,7 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
   // records ai, ai + stride, ...: the next record's head loads are issued before this record is
   // processed (its descriptor two records ahead), so their latency overlaps the work
   const uint32_t stride = gridDim.x * kWaves;
+  const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;  // plan_kernel ran
   uint32_t ai = blockIdx.x * kWaves + wv;
   if (ai < A.n_alns) {
     // (indices past the batch are clamped to its last record: the loads stay unconditional)
@@ -1419,7 +1540,13 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
       RecPre nxt;
       rec_pre(A, an < A.n_alns ? an : nm1, unpack_desc(dn), lane, nxt);
       DescRaw dnn = load_desc(A, an + stride < A.n_alns ? an + stride : nm1);
-      index_record(A, W, tp, w, ai, lane, cur);
+      IdxBlk B = whole_record(cur.d);
+      if (planned && cur.d.n_ops > (uint32_t)kBlkOps) {  // a long record: this wave decodes its block 0
+        const uint32_t base = W.rec_blk[ai];
+        if (base != kNoBlk)
+          B = block_of(W, cur.d, base, (cur.d.n_ops + kBlkOps - 1) / kBlkOps, 0u, lane);
+      }
+      index_record(A, W, tp, w, ai, lane, cur, B);
       // (first consumed here, where the record's segment loads have already waited for them:
       // consumed at the top of the next iteration, the wait would also cover this record's stores)
       rec_pre_ready(A, nxt, lane);
@@ -1429,10 +1556,92 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
       dn = dnn;
     }
   }
+  // blocks 1.. of the long records, spread over all wavefronts (a record of 1-5 Mb walked by one
+  // wave would be the whole kernel's critical path)
+  if (planned) {
+    const uint32_t nbl = W.ctr[3] < W.blk_cap ? W.ctr[3] : W.blk_cap;
+    for (uint32_t i = blockIdx.x * kWaves + wv; i < nbl; i += stride) {
+      const uint64_t e = W.blist[i];
+      const uint32_t bai = (uint32_t)(e >> 32), k = (uint32_t)e;
+      if (k == 0) continue;
+      RecPre p;
+      rec_pre(A, bai, A.desc[bai], lane, p);
+      rec_pre_ready(A, p, lane);
+      IdxBlk B = block_of(W, p.d, i - k, (p.d.n_ops + kBlkOps - 1) / kBlkOps, k, lane);
+      B.prev_sub = (A.ops[p.d.op_begin + B.sb0 - 1] >> 30) == PW_OP_SUB;
+      index_record(A, W, tp, w, bai, lane, p, B);
+    }
+  }
   // the padding slots of the last chunk are empty
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
   if (blockIdx.x == 0)
     for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) W.hot[s].fn = kNoEv;
+}
+
+// ------------------------------------------------------------------ long records: plan + carries
+// plan_kernel: a thread per record; a record of more than kBlkOps ops reserves ceil(n / kBlkOps)
+// consecutive blist entries (no room: it is decoded by one wavefront, and the entries it did get
+// are marked block 0, which nobody decodes twice).
+__global__ __launch_bounds__(256) void plan_kernel(pw_report_args A, Work W) {
+  const uint32_t ai = blockIdx.x * 256 + threadIdx.x;
+  if (ai >= A.n_alns) return;
+  W.rec_bad[ai] = kNoBlk;
+  const uint32_t n = A.desc[ai].n_ops;
+  uint32_t base = kNoBlk;
+  if (n > (uint32_t)kBlkOps) {
+    const uint32_t nb = (n + kBlkOps - 1) / kBlkOps;
+    const uint32_t b = atomicAdd(&W.ctr[3], nb);
+    const bool fits = (uint64_t)b + nb <= W.blk_cap;
+    for (uint32_t k = 0; k < nb && (uint64_t)b + k < W.blk_cap; k++)
+      W.blist[b + k] = (uint64_t)ai << 32 | (fits ? k : 0u);
+    if (fits) base = b;
+  }
+  W.rec_blk[ai] = base;
+}
+
+// carry_kernel: a wavefront per blist entry — the block's query / target / literal advance and
+// its event heads (an indel op, or a '*' op not directly after another, pafreport.cpp:556-560),
+// the quantities index_kernel's scans accumulate.
+__global__ __launch_bounds__(kWave* kWaves) void carry_kernel(pw_report_args A, Work W) {
+  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t nbl = W.ctr[3] < W.blk_cap ? W.ctr[3] : W.blk_cap;
+  for (uint32_t i = blockIdx.x * kWaves + wv; i < nbl; i += gridDim.x * kWaves) {
+    const uint64_t e = W.blist[i];
+    const uint32_t ai = (uint32_t)(e >> 32), k = (uint32_t)e;
+    const pw_aln_desc d = A.desc[ai];
+    const uint32_t* ops = A.ops + d.op_begin;
+    const uint32_t j0 = k * (uint32_t)kBlkOps;
+    const uint32_t j1 = d.n_ops - j0 < (uint32_t)kBlkOps ? d.n_ops : j0 + (uint32_t)kBlkOps;
+    uint32_t prev = j0 > 0 && (ops[j0 - 1] >> 30) == PW_OP_SUB ? 1u : 0u;
+    uint32_t q = 0, t = 0, l = 0, h = 0;
+    for (uint32_t jb = j0; jb < j1; jb += 4 * kWave) {
+      uint32_t wd[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t j = jb + 64 * u + (uint32_t)lane;
+        wd[u] = ops[j < j1 ? j : j0];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t j = jb + 64 * u + (uint32_t)lane;
+        const bool in = j < j1;
+        const uint32_t w = in ? wd[u] : 0u, typ = w >> 30;
+        const bool is_sub = in && typ == PW_OP_SUB;
+        const uint64_t m = __ballot(is_sub);
+        const bool prevsub = lane == 0 ? prev != 0 : ((m >> (lane - 1)) & 1ull) != 0;
+        prev = (uint32_t)((m >> 63) & 1ull);
+        q += in ? op_qadv(w) : 0u;
+        t += in ? op_tadv(w) : 0u;
+        l += in ? op_ladv(w) : 0u;
+        h += (in && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub))) ? 1u : 0u;
+      }
+    }
+    q = wave_sum(q);
+    t = wave_sum(t);
+    l = wave_sum(l);
+    h = wave_sum(h);
+    if (lane == 0) W.bcarry[i] = (v4u){q, t, l, h};
+  }
 }
 
 // ------------------------------------------------------------------ render_kernel
@@ -2033,9 +2242,17 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
 __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W) {
   const uint32_t ai = blockIdx.x * 256 + threadIdx.x;
   if (ai >= A.n_alns) return;
+  const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;
   pw_aln_result r = A.results[ai];
   if (W.ctr[2]) {
     r.err = PW_REC_OVERFLOW;
+  } else if (r.err == PW_REC_OK && planned && W.rec_blk[ai] != kNoBlk && W.rec_bad[ai] != kNoBlk) {
+    // a long record's first block with a base mismatch (blocks decoded by other wavefronts)
+    const v4u e = W.berr[W.rec_blk[ai] + W.rec_bad[ai]];
+    r.err = (int32_t)e.x;
+    r.err_a = (int32_t)e.y;
+    r.err_b = (int32_t)e.z;
+    r.err_c = (int32_t)e.w;
   } else if (r.err == PW_REC_OK) {
     if (r.n_events) {  // bytes of the lines, across the pages they span
       uint64_t len;
@@ -2044,7 +2261,16 @@ __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W)
       } else {
         const pw_page p0 = A.pages[r.page_first];
         len = p0.off + p0.len - r.text_off;
-        for (uint32_t c = r.page_first + 1; c < r.page_last; c++) len += A.pages[c].len;
+        // (eight independent page loads per step: a record of a Mb contig spans ~500 pages)
+        uint32_t c = r.page_first + 1;
+        for (; c + 8 <= r.page_last; c += 8) {
+          uint32_t pl[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) pl[u] = A.pages[c + u].len;
+#pragma unroll
+          for (int u = 0; u < 8; u++) len += pl[u];
+        }
+        for (; c < r.page_last; c++) len += A.pages[c].len;
         len += r.text_end - A.pages[r.page_last].off;
       }
       r.text_len = (uint32_t)len;
@@ -2182,7 +2408,14 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   if (W.n_chunks && hipMemsetAsync(W.sflag, 0, W.n_chunks * pw::kWave, st) != hipSuccess) return PW_E_HIP;
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
-  if (ig > (uint64_t)ncu * 10u) ig = (uint64_t)ncu * 10u;  // (two rounds at 5 waves/SIMD; sweep: 16 -> 10 per CU saved ~10 us of index + tctx)
+  const bool planned = args->max_rec_ops == 0 || args->max_rec_ops > (uint32_t)pw::kBlkOps;
+  // (two rounds at 5 waves/SIMD; sweep: 16 -> 10 per CU saved ~10 us of index + tctx); with long
+  // records the blocks of 1.. are spread over the full grid whatever the record count
+  if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;
+  if (planned) {  // records of more than PW_BLOCK_OPS ops
+    hipLaunchKernelGGL(pw::plan_kernel, dim3((args->n_alns + 255) / 256), dim3(256), 0, st, *args, W);
+    hipLaunchKernelGGL(pw::carry_kernel, dim3((uint32_t)ncu * 8u), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+  }
   hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
     uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;

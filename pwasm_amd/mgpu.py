@@ -5,17 +5,24 @@
 
 Replaces the reference's sequential record loop (pafreport.cpp:303-436) over a node:
 
-  every rank    packs ONLY the PAF lines of its target-genome shard (crc32 of PAF column 6 mod
-                world; pw_batch_from_files_shard, multi-threaded host pre-pass) — gene mode's
-                first-occurrence q~t dedupe (pafreport.cpp:319-334) is keyed by the target, so it
-                is shard-local — stages them in its GPU's HBM and runs the HIP pass
-                (pw_stop_table_build + pw_report_events);
+  read + route  rank r reads only bytes [r*S/N, (r+1)*S/N) of the PAF (pw_paf_split: the lines
+                starting there, cut as the CLI cuts them) and sends each line to the rank owning
+                its target genome (crc32 of PAF column 6 mod world) with its global input line
+                (exclusive scan of the ranges' line counts): two all_to_all_single calls (RCCL over
+                xGMI with the nccl backend).  Gene mode's first-occurrence q~t dedupe
+                (pafreport.cpp:319-334) is keyed by the target, so it stays shard-local.
+  batches       the rank's lines in pipelined batches (PW_CHUNK_BYTES, default 256 MB): batch k+1
+                is packed on host threads while the GPU runs batch k (pw_batch_from_buffer, the
+                dedupe state moving from batch to batch; pw_stop_table_build + pw_report_events).
+  output        no rank-0 merge: the first fatal input line over all ranks ends the run (all-reduce
+                MIN); every rank's per-line stdout byte counts are summed over the ranks (all-reduce
+                of one int64 per input line) and exclusive-scanned into file offsets, and each rank
+                pwrites its own items there (pw_batch_write_at).  stderr lines (warnings, the fatal
+                message) are gathered to rank 0 and written in input-line order; the exit code is
+                the fatal item's.  stdout without -o: the file is assembled in a temporary file and
+                streamed out by rank 0.
   per-genome    pw_genome_table sums each target's alignments / event lines / aligned bases on the
-  tables        device; the rows and target names of all ranks are all-gathered (RCCL over xGMI
-                with the "nccl" backend) so rank 0 holds the node-wide table (--genome-table);
-  items         every rank writes its report as line-tagged items (PWI1, pw_batch_write_items);
-                rank 0 merges them by global input line (pw_items_merge) into exactly the stdout /
-                stderr / exit code of a single-process run.
+  tables        device; the rows and target names of all ranks are all-gathered (--genome-table).
 No collective touches the per-record data path: records are independent.
 
 PW_DIST_BACKEND=gloo runs the collectives on the host (tests put several ranks on one GPU,
@@ -123,7 +130,153 @@ def write_genome_table(path, all_rows, all_names):
                 f.write(f"{nm.decode()}\t{rec[k]}\t{ev[k]}\t{tb[k]}\n")
 
 
+def _coll(t, backend):
+    """A tensor where the process group's backend wants it (gloo: host)."""
+    return t.cpu() if backend == "gloo" else t
+
+
+def exchange(paf, world, rank, device, backend):
+    """Rank r reads only bytes [r*S/N, (r+1)*S/N) of the PAF (pw_paf_split: the lines starting
+    there), routes each line to the rank owning its target genome and receives its own lines from
+    every rank (all_to_all_single of the bytes and of the global line numbers; over RCCL with the
+    nccl backend).  -> (text uint8 with '\\n'-ended lines, global lines uint64, lines in the file)."""
+    import torch
+    import torch.distributed as dist
+
+    import pwasm_amd as pw
+    size = os.path.getsize(paf)
+    lo, hi = size * rank // world, size * (rank + 1) // world
+    n_local, data, idx = pw.paf_split(paf, lo, hi, world)
+    if world == 1:
+        return data[0], idx[0].astype(np.uint64), n_local
+    dv = device if backend != "gloo" else "cpu"
+    cnt = _coll(torch.tensor([n_local], dtype=torch.int64, device=dv), backend)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    base = sum(counts[:rank])
+    sizes = torch.tensor([[d.size for d in data], [i.size for i in idx]], dtype=torch.int64, device=dv)
+    rsizes = torch.empty_like(sizes)
+    dist.all_to_all_single(rsizes.view(-1), sizes.t().contiguous().view(-1), [2] * world, [2] * world)
+    rsizes = rsizes.view(world, 2).cpu().numpy()
+    sb, sl = [d.size for d in data], [i.size for i in idx]
+    rb, rl = [int(x) for x in rsizes[:, 0]], [int(x) for x in rsizes[:, 1]]
+    send = torch.from_numpy(np.concatenate(data) if sum(sb) else np.zeros(0, np.uint8)).to(dv)
+    recv = torch.empty(sum(rb), dtype=torch.uint8, device=dv)
+    dist.all_to_all_single(recv, send, rb, sb)
+    lines = np.concatenate(idx).astype(np.int64) + base if sum(sl) else np.zeros(0, np.int64)
+    sendl = torch.from_numpy(lines).to(dv)
+    recvl = torch.empty(sum(rl), dtype=torch.int64, device=dv)
+    dist.all_to_all_single(recvl, sendl, rl, sl)
+    return recv.cpu().numpy(), recvl.cpu().numpy().astype(np.uint64), sum(counts)
+
+
+def batch_cuts(text, line_no, target):
+    """Sub-batches of about `target` bytes ending at line ends -> [(byte lo, hi, line lo, hi)]."""
+    n = text.size
+    if n == 0:
+        return []
+    ends = np.flatnonzero(text == 10) + 1  # one past each line's '\\n'
+    cuts, b0, l0 = [], 0, 0
+    while b0 < n:
+        k = int(np.searchsorted(ends, b0 + target, side="left"))
+        k = min(max(k, l0 + 1), ends.size) - 1  # last line of this batch
+        b1 = int(ends[k])
+        cuts.append((b0, b1, l0, k + 1))
+        b0, l0 = b1, k + 1
+    return cuts
+
+
+def write_items_at(outs, n_total, out_path, world, rank, dv, tmpdir=None):
+    """Output of all ranks' finished batches without a merge pass: outs = [(batch, text, results,
+    pages, (line, status, stdout bytes, stderr bytes))] of this rank in line order.  The first fatal
+    input line over all ranks ends the run (all-reduce MIN); per-line stdout byte counts (one owner
+    per line) are summed over the ranks and exclusive-scanned into offsets of one output file, where
+    each rank pwrites its items (pw_batch_write_at).  stderr is gathered to rank 0 and written in
+    input-line order; stdout (out_path None) is assembled in a temporary file that rank 0 streams
+    out.  Returns the exit code of the single-process run."""
+    import torch
+    import torch.distributed as dist
+
+    def all_reduce_i64(vals, op):
+        t = torch.tensor(vals, dtype=torch.int64, device=dv)
+        if world > 1:
+            dist.all_reduce(t, op=op)
+        return t.cpu().numpy()
+
+    big = np.iinfo(np.int64).max
+    mine = [int(it[0][it[1] >= 0][0]) for _, _, _, _, it in outs if (it[1] >= 0).any()]
+    stop = int(all_reduce_i64([min(mine) if mine else big], dist.ReduceOp.MIN if world > 1 else None)[0])
+    lens = np.zeros(max(n_total, 1), dtype=np.int64)
+    for _, _, _, _, (ln, st, on, en) in outs:
+        keep = ln <= stop
+        lens[ln[keep].astype(np.int64)] = on[keep].astype(np.int64)
+    if world > 1:
+        tl = torch.from_numpy(lens).to(dv)
+        dist.all_reduce(tl, op=dist.ReduceOp.SUM)
+        lens = tl.cpu().numpy()
+    off = np.zeros(lens.size + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    total = int(off[-1])
+    tmp_out = None
+    if out_path is None:  # stdout: assembled in a file, then streamed out by rank 0
+        if rank == 0:
+            fd0, tmp_out = tempfile.mkstemp(prefix="pwmg_out_", dir=tmpdir)
+            os.close(fd0)
+        if world > 1:
+            o = [tmp_out]
+            dist.broadcast_object_list(o, src=0)
+            tmp_out = o[0]
+        out_path = tmp_out
+    if rank == 0:
+        fd = os.open(out_path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+        os.ftruncate(fd, total)
+        os.close(fd)
+    if world > 1:
+        dist.barrier()
+    fd = os.open(out_path, os.O_WRONLY)
+    errs = []
+    try:
+        for b, text_h, res_h, pages_h, (ln, st, on, en) in outs:
+            k = int((ln <= stop).sum())  # (items are in line order)
+            if k == 0:
+                continue
+            eb = b.write_at(text_h, res_h, pages_h, fd, off[ln[:k].astype(np.int64)], int(en[:k].sum()))
+            p = 0
+            for i in range(k):
+                if en[i]:
+                    errs.append((int(ln[i]), eb[p:p + int(en[i])]))
+                    p += int(en[i])
+    finally:
+        os.close(fd)
+    code = 0
+    if stop != big:
+        owner = [int(st[ln == stop][0]) for _, _, _, _, (ln, st, on, en) in outs if (ln == stop).any()]
+        code = int(all_reduce_i64([owner[0] if owner else -1], dist.ReduceOp.MAX if world > 1 else None)[0])
+    if world > 1:
+        allerr = [None] * world
+        dist.all_gather_object(allerr, errs)
+        errs = sorted((x for e in allerr for x in e), key=lambda t: t[0])
+        dist.barrier()
+    if rank == 0:
+        if tmp_out:
+            with open(tmp_out, "rb") as f:
+                while True:
+                    blk = f.read(1 << 24)
+                    if not blk:
+                        break
+                    sys.stdout.buffer.write(blk)
+            sys.stdout.buffer.flush()
+            os.remove(tmp_out)
+        for _, e in errs:
+            sys.stderr.buffer.write(e)
+        sys.stderr.buffer.flush()
+    return code
+
+
 def main(argv=None) -> int:
+    import threading
+
     import torch
     import torch.distributed as dist
 
@@ -136,6 +289,8 @@ def main(argv=None) -> int:
     backend = os.environ.get("PW_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if world > 1 and not dist.is_initialized():
         dist.init_process_group(backend=backend)
+    if world > 1:
+        backend = dist.get_backend()
     ndev = torch.cuda.device_count()
     if ndev == 0:
         print("pafreport: no HIP device available (this build has no CPU path)", file=sys.stderr)
@@ -159,64 +314,88 @@ def main(argv=None) -> int:
         return 1
     flags = ((pw.FLAG_G if "G" in opts else 0) | (pw.FLAG_F if "F" in opts else 0) |
              (pw.FLAG_C if "C" in opts else 0) | (pw.FLAG_N if "N" in opts else 0))
-    # a shared scratch directory for the item streams (one node)
-    if world > 1:
-        obj = [extra.get("tmpdir") or (tempfile.mkdtemp(prefix="pwmg_") if rank == 0 else None)]
-        dist.broadcast_object_list(obj, src=0)
-        tmp = obj[0]
-    else:
-        tmp = extra.get("tmpdir") or tempfile.mkdtemp(prefix="pwmg_")
-    os.makedirs(tmp, exist_ok=True)
+    dv = device if backend != "gloo" else "cpu"
+
+    # ---- 1. read 1/N of the PAF, exchange lines by target genome
+    text, line_no, n_total = exchange(nonopt[0], world, rank, device, backend)
+
+    # ---- 2. this rank's lines in pipelined batches: batch k + 1 is packed (host threads, no GIL)
+    # while the GPU runs batch k and its outputs come back (as the CLI pipelines its chunks)
+    target = int(os.environ.get("PW_CHUNK_BYTES", str(256 << 20)))
+    cuts = batch_cuts(text, line_no, target)
     err = None
-    try:
-        b = pw.HostBatch(fa, nonopt[0], flags, rank, world)
-    except RuntimeError as e:
-        err = str(e)
+    made = {}
+
+    def make(k, prev):
+        b0, b1, l0, l1 = cuts[k]
+        try:
+            made[k] = pw.HostBatch.from_buffer(fa, text[b0:b1], line_no[l0:l1], flags, prev)
+        except RuntimeError as e:
+            made[k] = e
+
+    stream = torch.cuda.current_stream()
+    outs, gtabs = [], {}
+    th = None
+    if cuts:
+        th = threading.Thread(target=make, args=(0, None))
+        th.start()
+    for k in range(len(cuts)):
+        th.join()
+        b = made.pop(k)
+        if isinstance(b, RuntimeError):
+            err = str(b)
+            break
+        if k + 1 < len(cuts):
+            th = threading.Thread(target=make, args=(k + 1, b))
+            th.start()
+        dev = pw.stage_batch(b, device)
+        pw.run_report(b, dev, stream.cuda_stream)
+        rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
+        launch_genome_table(dev, rows, gt, stream.cuda_stream)
+        text_h, res_h, pages_h = pw.fetch_outputs(dev)  # (synchronises the stream)
+        r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
+        for nm, row in zip(names, r):  # per-genome rows of all batches, summed by target
+            acc = gtabs.setdefault(nm, np.zeros(3, np.uint64))
+            acc += np.array([row[0:4].view("<u4")[0], row[4:8].view("<u4")[0], row[8:16].view("<u8")[0]], np.uint64)
+        items = b.items(text_h, res_h, pages_h)
+        outs.append((b, text_h, res_h, pages_h, items))
+        del dev
+        if (items[1] >= 0).any():  # a fatal item: nothing after it is reached
+            break
+    if th is not None and th.is_alive():
+        th.join()
+    made.clear()
     if world > 1:
         errs = [None] * world
         dist.all_gather_object(errs, err)
         err = next((e for e in errs if e), None)
     if err:
         if rank == 0:
-            sys.stderr.write(err.split(": ", 1)[-1] if err.startswith("pw_batch_from_files") else err)
+            sys.stderr.write(err.split(": ", 1)[-1] if err.startswith("pw_batch_from_buffer") else err)
         return 1
-    stream = torch.cuda.current_stream()
-    dev = pw.stage_batch(b, device)
-    pw.run_report(b, dev, stream.cuda_stream)
-    rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
-    launch_genome_table(dev, rows, gt, stream.cuda_stream)
-    items = os.path.join(tmp, f"items{rank}.pwi")
-    rc = b.write_items_from(dev, items)
-    if rc != 0:
-        raise RuntimeError(f"pw_batch_write_items: {rc}")
-    want_table = "genome-table" in extra
-    if world > 1:
-        all_rows = [x.cpu().numpy() for x in gather_ragged(rows)]
+
+    # ---- 3-5. stop line, offsets, every rank's pwrite, stderr in line order, exit code
+    out_path = opts.get("o") or None
+    code = write_items_at(outs, n_total, out_path, world, rank, dv, extra.get("tmpdir"))
+    if "genome-table" in extra:
+        names = list(gtabs.keys())
+        rows = (np.stack([gtabs[n] for n in names]) if names else np.zeros((0, 3), np.uint64))
+        packed = np.zeros((len(names), 16), np.uint8)
+        packed[:, 0:4] = rows[:, 0].astype("<u4").reshape(-1, 1).view(np.uint8)
+        packed[:, 4:8] = rows[:, 1].astype("<u4").reshape(-1, 1).view(np.uint8)
+        packed[:, 8:16] = rows[:, 2].astype("<u8").reshape(-1, 1).view(np.uint8)
+        rt = torch.from_numpy(packed.reshape(-1).copy()).to(device)
         nb = b"\0".join(names)
         nt = torch.from_numpy(np.frombuffer(nb, dtype=np.uint8).copy() if nb else np.zeros(0, np.uint8)).to(device)
-        all_names = [bytes(x.cpu().numpy()).split(b"\0") if x.numel() else [] for x in gather_ragged(nt)]
-        dist.barrier()
-    else:
-        torch.cuda.synchronize()
-        all_rows, all_names = [rows.cpu().numpy()], [names]
-    code = 0
-    if rank == 0:
-        code = pw.items_merge([os.path.join(tmp, f"items{r}.pwi") for r in range(world)], opts.get("o") or None)
-        if want_table:
+        if world > 1:  # (RCCL all-gather of the rows; the names ride along)
+            all_rows = [x.cpu().numpy() for x in gather_ragged(rt)]
+            all_names = [bytes(x.cpu().numpy()).split(b"\0") if x.numel() else [] for x in gather_ragged(nt)]
+        else:
+            all_rows, all_names = [rt.cpu().numpy()], [names]
+        if rank == 0:
             write_genome_table(extra["genome-table"], all_rows, all_names)
     if world > 1:
-        c = torch.tensor([code], dtype=torch.int64, device=device)
-        if dist.get_backend() == "gloo":
-            c = c.cpu()
-        dist.broadcast(c, src=0)
-        code = int(c.item())
         dist.barrier()
-    if rank == 0 and not extra.get("tmpdir"):
-        for r in range(world):
-            try:
-                os.remove(os.path.join(tmp, f"items{r}.pwi"))
-            except OSError:
-                pass
     return code
 
 

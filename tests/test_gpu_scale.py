@@ -181,6 +181,85 @@ def test_event_length_past_render_field(built, tmp_path):
         assert out.count(b">") == 4 and b"[530000]" in out
 
 
+def _dense_record(rng, q, strand, tname, bad_sub_at=None, sub_run_at=None):
+    """One PAF line over the whole query with an event every few bases (thousands of cs ops):
+    matches of 1-6, '*' runs, 1-3 base indels.  bad_sub_at=k: the k-th op is a '*' whose query
+    base is wrong (the reference's base mismatch error); sub_run_at=k: ops k-2 .. k+2 are one run
+    of five directly consecutive '*' ops (an S run across op k)."""
+    a = q if strand == "+" else _comp(q)
+    L = len(a)
+    cs, cg = [], []
+    i = t = 0
+    cur_m = 0
+
+    def flush():
+        nonlocal cur_m
+        if cur_m:
+            cg.append(f"{cur_m}M")
+            cur_m = 0
+
+    nops = 0
+    while i < L:
+        run = sub_run_at is not None and sub_run_at - 2 <= nops <= sub_run_at + 2
+        if nops % 2 == 0 and not run:
+            n = min(rng.randint(1, 6), L - i)
+            cs.append(f":{n}")
+            cur_m += n
+            i += n
+            t += n
+        else:
+            kind = "*" if run else rng.choice("*+-")
+            if kind == "*" or i + 3 >= L:
+                qb = a[i].lower()
+                tb = rng.choice([c for c in "acgt" if c != qb])
+                if nops == bad_sub_at:
+                    qb = rng.choice([c for c in "acgt" if c != a[i].lower()])
+                cs.append(f"*{tb}{qb}")
+                cur_m += 1
+                i += 1
+                t += 1
+            elif kind == "+":  # query-only bases: event 'D'
+                n = min(rng.randint(1, 3), L - i - 1)
+                flush()
+                cs.append("+" + a[i:i + n].lower())
+                cg.append(f"{n}I")
+                i += n
+            else:  # target-only bases: event 'I'
+                n = rng.randint(1, 3)
+                flush()
+                cs.append("-" + "".join(rng.choice("acgt") for _ in range(n)))
+                cg.append(f"{n}D")
+                t += n
+        nops += 1
+    flush()
+    return _paf_line("big", L, 0, L, strand, tname, t + 200, 100, 100 + t, "".join(cg), "".join(cs)), nops
+
+
+@pytest.mark.parametrize("flags", [["-G", "-C"], []])
+def test_long_records_blocks(built, tmp_path, flags):
+    """Records of more than PW_BLOCK_OPS (2048) cs ops are decoded as blocks by several
+    wavefronts (plan_kernel / carry_kernel / index_kernel): both strands, an S run across a block
+    boundary, short records between them, and a base mismatch in a later block of a long record
+    (the reference's error for that record; nothing after it)."""
+    rng = random.Random(77)
+    q = _rand_cds(rng, 30000)
+    (tmp_path / "q.fa").write_text(f">big\n{q}\n")
+    lines = []
+    for r, strand in enumerate("+-+-"):
+        ln, nops = _dense_record(rng, q, strand, f"t{r}", sub_run_at=2048 + 2 * r)
+        assert nops > 3 * 2048
+        lines.append(ln)
+        lines.append(_paf_line("big", 30000, 0, 60, "+", f"s{r}", 500, 10, 70, "60M", ":60"))
+    (tmp_path / "a.paf").write_text("".join(lines))
+    out = same([*flags, "-r", "q.fa", "a.paf"], cwd=str(tmp_path), timeout=600)
+    assert out.count(b">") == 8
+    bad, _ = _dense_record(random.Random(5), q, "-", "tbad", bad_sub_at=5 * 2048 + 17)
+    (tmp_path / "b.paf").write_text("".join(lines[:2]) + bad + "".join(lines[2:]))
+    rc, _, err = run([ORACLE, *flags, "-r", "q.fa", "b.paf"], cwd=str(tmp_path))
+    assert rc == 1 and b"base mismatch" in err
+    same([*flags, "-r", "q.fa", "b.paf"], cwd=str(tmp_path), timeout=600)
+
+
 def test_modseq_mismatch_reverse_u(built, tmp_path):
     """A reverse-strand substitution at a 'U' of the query passes the cs base check (comp(U) =
     A on the aligned strand) but fails predictImpact's modseq check (comp(A) = T != U): the

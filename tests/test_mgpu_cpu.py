@@ -96,3 +96,92 @@ def test_genome_table_writer(tmp_path):
     p = tmp_path / "t.tsv"
     mgpu.write_genome_table(p, [rows], [[b"tA", b"tB"]])
     assert p.read_text().splitlines()[1:] == ["tA\t3\t17\t12345", "tB\t1\t0\t0"]
+
+
+# ---------------------------------------------------------------- byte-range exchange + offset writes
+def _paf_with_everything(tmp_path, fatal):
+    """An edge-mix PAF with duplicate q~t pairs (dedupe warnings), comments, CRLF line ends on some
+    lines and, optionally, a short line two thirds in (the fatal that ends the run)."""
+    from conftest import synth_paf
+    from test_shard import _with_duplicates_and_comments
+    fa, paf = synth_paf(tmp_path, 0, seed=41)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 2)
+    lines = open(dup, "rb").read().splitlines(keepends=True)
+    lines = [ln.replace(b"\n", b"\r\n") if k % 7 == 3 else ln for k, ln in enumerate(lines)]
+    if fatal:
+        lines.insert(2 * len(lines) // 3, b"cds0\t30\t0\t30\t+\n")
+    p = tmp_path / "all.paf"
+    p.write_bytes(b"".join(lines))
+    return fa, str(p)
+
+
+def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+    os.dup2(fd, 2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        text, line_no, n_total = mgpu.exchange(paf, world, rank, "cpu", "gloo")
+        # every received line belongs to this rank: target genome hash (column 6) mod world
+        got = bytes(text).split(b"\n")[:-1]
+        for ln in got:
+            assert shard.shard_of(ln, world) == rank
+        # the batches of this rank without a GPU: every record "ran" with zero events (results of
+        # zeros), so each prints its header — headers, messages, dedupe and the fatal stop all go
+        # through the offset-write path
+        outs = []
+        prev = None
+        for b0, b1, l0, l1 in mgpu.batch_cuts(text, line_no, 3000):
+            b = pw.HostBatch.from_buffer(fa, text[b0:b1], line_no[l0:l1], 0, prev)
+            prev = b
+            res = np.zeros(max(int(b.view.n_alns), 1) * 48, np.uint8)
+            pages, txt = np.zeros(16, np.uint8), np.zeros(16, np.uint8)
+            outs.append((b, txt, res, pages, b.items(txt, res, pages)))
+        code = mgpu.write_items_at(outs, n_total, out_path, world, rank, "cpu")
+        q.put((rank, code, n_total, [int(x) for x in line_no]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fatal", [(2, False), (2, True), (3, True)])
+def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal):
+    """mgpu's scalable host path on the CPU (gloo): each rank reads 1/N of the PAF by byte range
+    (pw_paf_split), lines are exchanged by target genome (all_to_all_single), packed in several
+    batches per rank (the q~t dedupe state carried over), and written at offsets from an
+    exclusive scan of the all-reduced per-line byte counts.  The file, stderr and exit code must
+    equal the single-process batch (pw_batch_from_files + write_items + merge) on the same zero
+    results."""
+    fa, paf = _paf_with_everything(tmp_path, fatal)
+    single = pw.HostBatch(fa, paf, 0)
+    res = np.zeros(max(int(single.view.n_alns), 1) * 48, np.uint8)
+    z = np.zeros(16, np.uint8)
+    items = tmp_path / "single.pwi"
+    assert single.write_items(z, res, z, str(items)) == 0
+    want_rc = pw.items_merge([items], tmp_path / "want.out", tmp_path / "want.err")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    out = tmp_path / "got.out"
+    ps = [ctx.Process(target=_exchange_rank, args=(r, world, port, fa, paf, str(out), str(tmp_path / f"e{r}"), q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r, (c, n, ln)) for r, c, n, ln in (q.get(timeout=90) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n_lines = len(open(paf, "rb").read().replace(b"\r\n", b"\n").split(b"\n")) - 1
+    assert all(v[1] == n_lines for v in res.values())
+    assert {v[0] for v in res.values()} == {want_rc}
+    assert want_rc == (1 if fatal else 0)
+    noise = (b"/opt/amdgpu/", b"[W", b"[Gloo]", b"[I")
+    err = b"".join(ln for ln in open(tmp_path / "e0", "rb").read().splitlines(keepends=True)
+                   if not ln.startswith(noise))
+    assert out.read_bytes() == (tmp_path / "want.out").read_bytes()
+    assert err == (tmp_path / "want.err").read_bytes()
+    # every non-comment line went to exactly one rank, with its global line number
+    got = sorted(x for v in res.values() for x in v[2])
+    lines = open(paf, "rb").read().replace(b"\r\n", b"\n").split(b"\n")[:-1]
+    assert got == [k for k, ln in enumerate(lines) if not ln.startswith(b"#")]
