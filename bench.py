@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle diff + end-to-end CLI run")
     ap.add_argument("--remove-gaps", action="store_true", help="cfg5: MSAColumns::removeConsGaps=true")
+    ap.add_argument("--no-e2e", action="store_true", help="N > 1: skip the end-to-end pwasm_amd.mgpu leg")
+    ap.add_argument("--e2e-parity", action="store_true", help="N > 1: CRC the end-to-end report against the oracle")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
@@ -82,17 +84,27 @@ def main():
     # at N > 1: one independent batch per rank (weak scaling).
     sharded = args.config == 3
     tmp = tempfile.mkdtemp(prefix=f"pwbench{rank}_")
-    fa, paf = os.path.join(tmp, "q.fa"), os.path.join(tmp, "a.paf")
+    if sharded and world > 1:  # one 10M-record file for the node (rank 0 writes it; ranks share it)
+        box = [tmp if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        shared = box[0]
+    else:
+        shared = tmp
+    fa, paf = os.path.join(shared, "q.fa"), os.path.join(shared, "a.paf")
     seed = 3 if sharded else (2 + 1000 * rank if args.config == 2 else args.config + 1000 * rank)
     t0 = time.time()
     cmd = [str(REPO / "synth/build/pwsynth"), "paf", "--config", str(args.config), "--scale", str(args.scale),
            "--seed", str(seed), "--fa", fa, "--paf", paf]
-    if sharded:
-        cmd += ["--threads", str(host_threads())] + (["--shard", f"{rank}/{world}"] if world > 1 else [])
-    subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
+    if args.config in (3, 4):
+        cmd += ["--threads", str(host_threads())]
+    if not (sharded and world > 1 and rank != 0):
+        subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
+    if sharded and world > 1:
+        dist.barrier()
     t_gen = time.time() - t0
     flags = pw.FLAG_G | pw.FLAG_C if args.config in (1, 2, 3) else 0
-    batch = pw.HostBatch(fa, paf, flags)
+    # cfg3 over N ranks: rank r packs the lines of its target-genome shard (crc32 of PAF column 6)
+    batch = pw.HostBatch(fa, paf, flags, rank, world) if sharded else pw.HostBatch(fa, paf, flags)
     v = batch.view
     dev = pw.stage_batch(batch, dev_name)
     torch.cuda.synchronize()
@@ -179,14 +191,41 @@ def main():
     tot_events = n_events
     tot_records = int(v.n_alns)
     max_el = t_el
+    red_dev = dev_name if dist.is_initialized() and dist.get_backend() != "gloo" else "cpu"
     if world > 1:
-        t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
+        t = torch.tensor([t_el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         max_el = float(t.item())
-        e = torch.tensor([n_events, int(v.n_alns)], dtype=torch.float64, device=dev_name)
+        e = torch.tensor([n_events, int(v.n_alns)], dtype=torch.float64, device=red_dev)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
         tot_events = int(e[0].item())
         tot_records = int(e[1].item())
+    e2e_node = None
+    if sharded and world > 1 and not args.no_e2e:
+        # end to end over the node: pwasm_amd.mgpu (every rank reads 1/N of the PAF, exchanges lines
+        # by target genome, packs / runs / writes its own records at their offsets of one report)
+        from pwasm_amd import mgpu
+        del dev
+        torch.cuda.empty_cache()
+        out_path = os.path.join(shared, "report_e2e.txt")
+        dist.barrier()
+        t0 = time.perf_counter()
+        code = mgpu.main(["-G", "-C", "-r", fa, paf, "-o", out_path])
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+        if rank == 0:
+            e2e_node = {"wall_s": round(wall, 3), "events_per_s": tot_events / wall, "rc": code,
+                        "cmd": f"torchrun x{world} -m pwasm_amd.mgpu -G -C -r q.fa a.paf -o report.txt "
+                               f"({os.path.getsize(paf)} B in, {os.path.getsize(out_path)} B out)"}
+            if args.e2e_parity:
+                want = oracle_crc(["-G", "-C"], fa, paf, host_threads())
+                with open(out_path, "rb") as f:
+                    got = crc_stream(f)
+                e2e_node["parity"] = "ok" if code == 0 and got == want[:3] else "FAIL"
+            log(f"[e2e] {world} ranks: {wall:.2f} s, rc {code}")
+        dist.barrier()
 
     if rank == 0:
         report = {}
@@ -279,7 +318,7 @@ def main():
                          "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd"),
                          "issue_busy": issue_busy(prof, ("pw::render_kernel", "pw::index_kernel", "pw::tctx_kernel"))},
             "cpu_baseline": cpu,
-            "e2e": e2e,
+            "e2e": e2e if e2e is not None else e2e_node,
             "gpu_pack": gpack,
         }
         print(json.dumps(out), flush=True)

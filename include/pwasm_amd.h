@@ -262,6 +262,13 @@ typedef struct pw_ga_row {
 int pw_ga_row_remove_columns(pw_ga_row* row, const int32_t* alpos, uint64_t n);
 int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int32_t cpos_base, uint32_t flags,
                      char* msgbuf, size_t msglen);
+/* Both for n rows in one call: rows with replay[k] != 0 get pw_ga_row_remove_columns(alpos) first,
+ * then every row pw_ga_row_finish; messages back to back in msgbuf (row k: [msg_off[k],
+ * msg_off[k+1]), msg_off has n + 1 entries), failed[k] = 1 after a GError, after which it stops.
+ * Returns the rows processed (or a negative PW_E_* status). */
+int64_t pw_ga_rows_finish(pw_ga_row* rows, uint64_t n, const uint8_t* replay, const int32_t* alpos, uint64_t n_alpos,
+                          const uint8_t* cons, int32_t cons_len, int32_t cpos_base, uint32_t flags, char* msgbuf,
+                          uint64_t msg_cap, uint64_t* msg_off, int32_t* failed);
 
 /* ---------------------------------------------------------------- host pre-pass + CLI */
 

@@ -129,6 +129,10 @@ _SIGS = {
     "pw_ga_row_remove_columns": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_uint64]),
     "pw_ga_row_finish": (ctypes.c_int, [ctypes.POINTER(GaRow), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                         ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    "pw_ga_rows_finish": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     "pw_pack_cs_batch": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4),
     "pw_pack_cs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t,
                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),

@@ -1231,3 +1231,35 @@ extern "C" int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t con
   if (msgbuf && msglen) snprintf(msgbuf, msglen, "%s", msgs.c_str());
   return status;
 }
+
+// The per-row tail for many rows in one call (the multi-GPU driver's own rows): rows with
+// replay[k] != 0 first get removeColumn replayed for alpos (pw_ga_row_remove_columns), then every
+// row pw_ga_row_finish.  Messages back to back in msgbuf (row k's are [msg_off[k], msg_off[k+1]));
+// failed[k] = 1 after a GError.  Stops after the first failing row (the reference exits there);
+// returns the number of rows processed.
+extern "C" int64_t pw_ga_rows_finish(pw_ga_row* rows, uint64_t n, const uint8_t* replay, const int32_t* alpos,
+                                     uint64_t n_alpos, const uint8_t* cons, int32_t cons_len, int32_t cpos_base,
+                                     uint32_t flags, char* msgbuf, uint64_t msg_cap, uint64_t* msg_off,
+                                     int32_t* failed) {
+  if ((n && (!rows || !msg_off || !failed)) || (n_alpos && !alpos)) return PW_E_ARG;
+  std::vector<char> one(1 << 16);
+  uint64_t used = 0;
+  msg_off[0] = 0;
+  uint64_t k = 0;
+  for (; k < n; k++) {
+    failed[k] = 0;
+    if (replay && replay[k] && pw_ga_row_remove_columns(&rows[k], alpos, n_alpos) != PW_OK) return PW_E_ARG;
+    const int rc = pw_ga_row_finish(&rows[k], cons, cons_len, cpos_base, flags, one.data(), one.size());
+    if (rc < 0) return rc;
+    const size_t m = strlen(one.data());
+    if (msgbuf && used + m <= msg_cap) memcpy(msgbuf + used, one.data(), m);
+    used += m;
+    msg_off[k + 1] = used;
+    if (rc == 1) {
+      failed[k] = 1;
+      k++;
+      break;
+    }
+  }
+  return (int64_t)k;
+}

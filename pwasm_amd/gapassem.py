@@ -260,63 +260,99 @@ def _i32(v: int) -> int:
 
 def finish_rows(lay: Layout, rows, base: dict, alpos, cons: bytes, mincol: int, remove_gaps: bool,
                 refine_clipping: bool):
-    """refineMSA's per-row tail for `rows` on the host (GapAssem.cpp:1163-1181) through the C-ABI:
-    rows holding deleted bases (ofs < 0) get removeColumn replayed from their input gaps
-    (pw_ga_row_remove_columns), every row then refineClipping / removeClipGaps / refineClipping
-    (pw_ga_row_finish).  base = {row: (offset, numgaps, ofs)} after the GPU's removeColumn edits.
-    -> {row: (messages, failed, offset, numgaps, clp5, clp3, ofs)}."""
+    """refineMSA's per-row tail for `rows` on the host (GapAssem.cpp:1163-1181), all rows in one
+    C call (pw_ga_rows_finish): rows holding deleted bases (ofs < 0) get removeColumn replayed from
+    their input gaps, every row then refineClipping / removeClipGaps / refineClipping.  base =
+    {row: (offset, numgaps, ofs)} after the GPU's removeColumn edits.  Stops after a row that
+    GErrors (the reference exits there).  -> {row: (messages, failed, offset, numgaps, clp5,
+    clp3, ofs)} for the rows processed."""
     from pwasm_amd import GaRow, lib
+    rows = list(rows)
+    n = len(rows)
+    if n == 0:
+        return {}
     L = lib()
     flags = (1 if remove_gaps else 0) | (2 if refine_clipping else 0)
     al = np.ascontiguousarray(np.asarray(alpos, dtype=np.int32))
     cons_a = np.frombuffer(cons, dtype=np.uint8) if cons else np.zeros(1, dtype=np.uint8)
-    cpos_base = _i32(lay.minoffset + mincol)
-    msg = ctypes.create_string_buffer(1 << 16)
+    replay = np.array([remove_gaps and int(lay.ofs[r].min(initial=0)) < 0 for r in rows], dtype=np.uint8)
+    lens = np.array([int(lay.seqlen[r]) for r in rows], dtype=np.int64)
+    start = np.concatenate([[0], np.cumsum(lens)])
+    seq = np.concatenate([np.asarray(lay.seq[r], dtype=np.uint8) for r in rows] + [np.zeros(1, np.uint8)])
+    ofs = np.concatenate([np.asarray(lay.ofs[r] if replay[k] else base[r][2], dtype=np.int16)
+                          for k, r in enumerate(rows)] + [np.zeros(1, np.int16)])
+    off0 = np.array([int(lay.offset[r]) if replay[k] else int(base[r][0]) for k, r in enumerate(rows)], np.int64)
+    ng0 = np.array([int(lay.numgaps[r]) if replay[k] else int(base[r][1]) for k, r in enumerate(rows)], np.int64)
+    ids = b"".join(b"row%d\0" % r for r in rows)
+    id_off = np.concatenate([[0], np.cumsum([len(b"row%d" % r) + 1 for r in rows])])[:n]
+    idbuf = ctypes.create_string_buffer(ids, len(ids))
+    arr = (GaRow * n)()
+    dt = np.dtype({"names": ["seq", "ofs", "seqlen", "offset", "numgaps", "clp5", "clp3", "rev", "id"],
+                   "formats": ["<u8", "<u8", "<i4", "<i4", "<i4", "<i4", "<i4", "<i4", "<u8"],
+                   "offsets": [GaRow.seq.offset, GaRow.ofs.offset, GaRow.seqlen.offset, GaRow.offset.offset,
+                               GaRow.numgaps.offset, GaRow.clp5.offset, GaRow.clp3.offset, GaRow.revcompl.offset,
+                               GaRow.id.offset], "itemsize": ctypes.sizeof(GaRow)})
+    v = np.frombuffer(arr, dtype=dt)
+    ri = np.array(rows, dtype=np.int64)
+    v["seq"] = seq.ctypes.data + start[:n]
+    v["ofs"] = ofs.ctypes.data + 2 * start[:n]
+    v["seqlen"] = lens
+    v["offset"] = off0
+    v["numgaps"] = ng0
+    v["clp5"] = lay.clp5[ri]
+    v["clp3"] = lay.clp3[ri]
+    v["rev"] = lay.rev[ri]
+    v["id"] = ctypes.addressof(idbuf) + id_off
+    cap = 1 << 16
+    while True:
+        msg = ctypes.create_string_buffer(cap)
+        moff = np.zeros(n + 1, dtype=np.uint64)
+        failed = np.zeros(n, dtype=np.int32)
+        k = L.pw_ga_rows_finish(arr, n, replay.ctypes.data, al.ctypes.data if al.size else None, al.size,
+                                cons_a.ctypes.data, len(cons), _i32(lay.minoffset + mincol), flags, msg, cap,
+                                moff.ctypes.data, failed.ctypes.data)
+        if k < 0:
+            raise RuntimeError(f"pw_ga_rows_finish: {k}")
+        if int(moff[k]) <= cap:
+            break
+        cap = int(moff[k])
+    raw = msg.raw
     out = {}
-    for r in rows:
-        neg = remove_gaps and int(lay.ofs[r].min(initial=0)) < 0
-        if neg:
-            off, ng, ofs = int(lay.offset[r]), int(lay.numgaps[r]), lay.ofs[r].astype(np.int16).copy()
-        else:
-            off, ng, ofs = base[r]
-            ofs = np.array(ofs, dtype=np.int16)
-        seq = np.ascontiguousarray(lay.seq[r])
-        row = GaRow()
-        row.seq, row.ofs, row.seqlen = seq.ctypes.data, ofs.ctypes.data, int(lay.seqlen[r])
-        row.offset, row.numgaps = off, ng
-        row.clp5, row.clp3, row.revcompl = int(lay.clp5[r]), int(lay.clp3[r]), int(lay.rev[r])
-        rid = b"row%d" % r
-        row.id = rid
-        if neg and L.pw_ga_row_remove_columns(ctypes.byref(row), al.ctypes.data, al.size) != 0:
-            raise RuntimeError("pw_ga_row_remove_columns")
-        rc = L.pw_ga_row_finish(ctypes.byref(row), cons_a.ctypes.data, len(cons), cpos_base, flags, msg, len(msg))
-        if rc < 0:
-            raise RuntimeError(f"pw_ga_row_finish: {rc}")
-        out[r] = (msg.value.decode(), rc == 1, row.offset, row.numgaps, row.clp5, row.clp3, ofs)
+    for j in range(int(k)):
+        out[rows[j]] = (raw[int(moff[j]):int(moff[j + 1])].decode(), bool(failed[j]), int(v["offset"][j]),
+                        int(v["numgaps"][j]), int(v["clp5"][j]), int(v["clp3"][j]),
+                        ofs[int(start[j]):int(start[j + 1])].copy())
     return out
 
 
 def gather_rows(fin: dict, group, device):
-    """finish_rows' output of every rank, merged on every rank.  The per-row fields (messages,
-    offsets, clips: small) go through all_gather_object; the edited gap arrays (all rows with
-    removeConsGaps: ~2 bytes per base) as one byte tensor per rank through all_gather — device
-    tensors under RCCL (int16 is not an RCCL type: the bytes travel), host tensors under gloo."""
+    """finish_rows' output of every rank, merged on rank 0 only (the one that writes the result;
+    None elsewhere).  The per-row fields (messages, offsets, clips: small) go through
+    gather_object; the edited gap arrays (all rows with removeConsGaps: ~2 bytes per base) as one
+    byte tensor per rank through gather — device tensors under RCCL (int16 is not an RCCL type:
+    the bytes travel), host tensors under gloo."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     rows = sorted(fin)
     meta = {r: fin[r][:6] + (len(fin[r][6]),) for r in rows}
     flat = (np.concatenate([np.asarray(fin[r][6], dtype="<i2") for r in rows]) if rows
             else np.zeros(0, dtype="<i2")).view(np.uint8)
-    metas = [None] * world
-    dist.all_gather_object(metas, (meta, int(flat.size)), group=group)
-    nmax = max(1, max(n for _, n in metas))
+    metas = [None] * world if rank == 0 else None
+    dist.gather_object((meta, int(flat.size)), metas, dst=0, group=group)
+    nmax = torch.tensor([int(flat.size)], dtype=torch.int64)
     dev = device if dist.get_backend(group) == "nccl" else "cpu"
+    nmax = nmax.to(dev)
+    dist.all_reduce(nmax, op=dist.ReduceOp.MAX, group=group)
+    nmax = max(1, int(nmax.item()))
     buf = torch.zeros(nmax, dtype=torch.uint8, device=dev)
     if flat.size:
         buf[: flat.size] = torch.from_numpy(flat).to(dev)
-    outs = [torch.empty(nmax, dtype=torch.uint8, device=dev) for _ in range(world)]
-    dist.all_gather(outs, buf, group=group)
+    outs = [torch.empty(nmax, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, outs, dst=0, group=group)
+    if rank != 0:
+        return None
     merged = {}
     for (meta_p, n), t in zip(metas, outs):
         b = t[:n].cpu().numpy().view("<i2") if n else np.zeros(0, dtype="<i2")
@@ -400,9 +436,13 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
     fin = finish_rows(lay, [r for r in own if remove_gaps or (refine_clipping and (lay.clp5[r] or lay.clp3[r]))],
                       base, alpos, cons_s, mincol, remove_gaps, refine_clipping)
     if world > 1:
+        # the exit code everywhere: a GError on any row ends the run (1); the rows only on rank 0
+        bad_any = torch.tensor([1 if any(v[1] for v in fin.values()) else 0], dtype=torch.int64,
+                               device=counts.device if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(bad_any, op=dist.ReduceOp.MAX, group=group)
         fin = gather_rows(fin, group, counts.device)
-    if rank != 0:
-        return (1 if any(v[1] for v in fin.values()) else 0), "", None
+        if rank != 0:
+            return int(bad_any.item()), "", None
     for r in range(hdr.n):  # the per-row messages in row order, up to a row that GErrors
         if r in fin:
             err.append(fin[r][0])
