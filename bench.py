@@ -329,9 +329,9 @@ def main():
 def bench_gapassem(args, world, rank, dev_name):
     """BASELINE.json configs[4]: GapAssem consensus of one 200-row, ~1M-column layout (pwsynth
     cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step = pw_msa_count on the
-    rank's rows + all-reduce of the [n_cols x 6] histograms and of mincol/-maxcol (RCCL) +
-    pw_msa_call + pw_msa_refine (consensus string; with --remove-gaps also the removeConsGaps row
-    edits).  Default removeConsGaps=false: pafreport's setting (pafreport.cpp:31,203), which is
+    rank's rows + pw_msa_call_sharded (RCCL reduce-scatter of the [n_cols x 6] histograms by
+    column range + bounds, bestChar of the rank's columns, all-gather of the consensus) +
+    pw_msa_refine (consensus string; with --remove-gaps also the removeConsGaps row edits).  Default removeConsGaps=false: pafreport's setting (pafreport.cpp:31,203), which is
     also what the linear-time CPU oracle can time at full size.  Throughput = layout bases per
     second (all rows, whole job)."""
     import numpy as np
@@ -350,7 +350,9 @@ def bench_gapassem(args, world, rank, dev_name):
     lo, hi = gapassem.shard_rows(hdr.seqlen, world)[rank]
     lay = gapassem.Layout(lay_path, load=set(range(lo, hi)))
     eng = gapassem.HipEngine(dev_name)
-    st = eng.stage(lay, range(lo, hi), lay.length)
+    rccl = world > 1 and dist.get_backend() == "nccl"
+    st = eng.stage(lay, range(lo, hi), lay.length, world if rccl else 1)
+    comm = gapassem.rccl_comm() if rccl else None
     total_bases = int(hdr.seqlen.sum())
     log(f"[rank {rank}] layout {hdr.n} rows, {lay.length} columns, {total_bases} bases; rows [{lo},{hi}) "
         f"({time.time() - t0:.1f}s host prep)")
@@ -359,7 +361,11 @@ def bench_gapassem(args, world, rank, dev_name):
 
     def step():
         counts, _ = eng.count(st)
-        if world > 1:
+        if rccl:  # column-sharded: reduce-scatter by column range, own-range bestChar, all-gather
+            eng.call_sharded(st, lo, comm, rank, world)
+            eng.refine(st, remove)
+            return
+        if world > 1:  # (gloo rehearsal: host all-reduce of the whole histogram)
             dist.all_reduce(counts, op=dist.ReduceOp.SUM)
             red[0] = mm[0]
             red[1] = -mm[1]

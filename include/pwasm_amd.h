@@ -194,6 +194,9 @@ int pw_msa_columns(const pw_msa_args* args, void* stream);
  * reduced with min / max, pw_msa_call writes bestChar for every column and minmax[3]. */
 int pw_msa_count(const pw_msa_args* args, void* stream);
 int pw_msa_call(const pw_msa_args* args, void* stream);
+/* pw_msa_call over columns [col_lo, col_hi) only (the zero-coverage scan too); counts_lo = the
+ * counts of column col_lo onwards ([col_hi - col_lo][6]) or NULL for args->counts. */
+int pw_msa_call_cols(const pw_msa_args* args, int32_t col_lo, int32_t col_hi, const int32_t* counts_lo, void* stream);
 
 /* GSeqAlign::refineMSA after buildMSA (GapAssem.cpp:1143-1181): the consensus string over
  * [mincol, maxcol] ('-' -> '*'; with remove_gaps = MSAColumns::removeConsGaps the gap columns
@@ -234,6 +237,15 @@ int pw_comm_destroy(void* comm);
 int pw_msa_counts_allreduce(const pw_msa_args* args, uint32_t row_base, void* comm, void* stream);
 int pw_msa_counts_reduce_scatter(const int32_t* counts, int32_t* counts_part, uint64_t cols_per_rank, void* comm,
                                  void* stream);
+/* Column-sharded bestChar, after every rank's pw_msa_count on its rows: the
+ * histograms reduce-scattered by column range (rank r: columns [r * cols_per_rank, ...) into
+ * counts_part; args->counts holds nranks * cols_per_rank columns, zero past n_cols), the bounds
+ * reduced as in pw_msa_counts_allreduce, bestChar + the zero-coverage scan of the rank's range only
+ * (pw_msa_call_cols), then the consensus ranges all-gathered in place (args->consensus holds
+ * nranks * cols_per_rank bytes) and minmax[3] reduced MIN.  Every rank then holds what an
+ * all-reduce + pw_msa_call leaves, except the full counts (its own range is in counts_part). */
+int pw_msa_call_sharded(const pw_msa_args* args, uint32_t row_base, int32_t* counts_part, uint64_t cols_per_rank,
+                        int rank, int nranks, void* comm, void* stream);
 
 /* Host per-row steps of GSeqAlign::refineMSA after the consensus (the GapAssem C++ API,
  * pwasm_gapassem.hpp, and the multi-GPU driver call these on the rows they own).

@@ -117,6 +117,10 @@ _SIGS = {
     "pw_msa_columns": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_count": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_call": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
+    "pw_msa_call_cols": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    "pw_msa_call_sharded": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_msa_refine_tiles": (ctypes.c_uint64, [ctypes.c_int32]),
     "pw_msa_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
     "pw_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),

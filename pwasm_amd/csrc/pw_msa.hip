@@ -306,8 +306,8 @@ __global__ __launch_bounds__(64 * kTileWaves) void tile_counts(const pw_msa_args
 }
 
 // bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage
-__global__ __launch_bounds__(256) void call_columns(const pw_msa_args A) {
-  for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < A.n_cols; c += (int64_t)gridDim.x * 256) {
+__global__ __launch_bounds__(256) void call_columns(const pw_msa_args A, int32_t lo, int32_t hi) {
+  for (int64_t c = lo + (int64_t)blockIdx.x * 256 + threadIdx.x; c < hi; c += (int64_t)gridDim.x * 256) {
     int v[6];
     const int32_t* src = A.counts + c * 6;
 #pragma unroll
@@ -329,8 +329,9 @@ __global__ __launch_bounds__(256) void call_columns(const pw_msa_args A) {
   }
 }
 
-__global__ __launch_bounds__(256) void zero_scan(const pw_msa_args A) {
-  const int lo = A.minmax[0], hi = A.minmax[1];
+// (columns [c_lo, c_hi) of the consensus are this call's: the whole layout, or a rank's range)
+__global__ __launch_bounds__(256) void zero_scan(const pw_msa_args A, int32_t c_lo, int32_t c_hi) {
+  const int lo = max(A.minmax[0], c_lo), hi = min(A.minmax[1], c_hi - 1);
   for (int c = lo + blockIdx.x * 256 + threadIdx.x; c <= hi; c += gridDim.x * 256)
     if (c >= 0 && c < A.n_cols && A.consensus[c] == 0) atomicMin(&A.minmax[3], c);
 }
@@ -513,13 +514,22 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
+extern "C" int pw_msa_call_cols(const pw_msa_args* a, int32_t col_lo, int32_t col_hi, const int32_t* counts_lo,
+                                void* stream) {
+  if (!msa_args_ok(a) || col_lo < 0 || col_hi > a->n_cols || col_lo > col_hi) return PW_E_ARG;
+  if (col_lo == col_hi) return PW_OK;
+  hipStream_t s = (hipStream_t)stream;
+  pw_msa_args b = *a;
+  if (counts_lo) b.counts = const_cast<int32_t*>(counts_lo) - (int64_t)col_lo * 6;  // column c at counts_lo[(c - lo) * 6]
+  const uint64_t nb = ((uint64_t)(col_hi - col_lo) + 255) / 256;
+  hipLaunchKernelGGL(pw::call_columns, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, b, col_lo, col_hi);
+  hipLaunchKernelGGL(pw::zero_scan, dim3(256), dim3(256), 0, s, b, col_lo, col_hi);
+  return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+}
+
 extern "C" int pw_msa_call(const pw_msa_args* a, void* stream) {
   if (!msa_args_ok(a)) return PW_E_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  const uint64_t nb = ((uint64_t)a->n_cols + 255) / 256;
-  hipLaunchKernelGGL(pw::call_columns, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, *a);
-  hipLaunchKernelGGL(pw::zero_scan, dim3(256), dim3(256), 0, s, *a);
-  return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+  return pw_msa_call_cols(a, 0, a->n_cols, nullptr, stream);
 }
 
 extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) {

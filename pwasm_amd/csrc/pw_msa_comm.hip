@@ -28,6 +28,7 @@ struct Rccl {
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
   decltype(&ncclGroupEnd) group_end = nullptr;
 };
@@ -44,9 +45,10 @@ const Rccl& rccl() {
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.reduce_scatter = (decltype(r.reduce_scatter))dlsym(h, "ncclReduceScatter");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
     r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
     r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
-    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.reduce_scatter &&
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_reduce && r.reduce_scatter && r.all_gather &&
            r.group_start && r.group_end;
   });
   return r;
@@ -115,4 +117,38 @@ extern "C" int pw_msa_counts_reduce_scatter(const int32_t* counts, int32_t* coun
                           (hipStream_t)stream) == ncclSuccess
              ? PW_OK
              : PW_E_HIP;
+}
+
+// Column-sharded bestChar: reduce-scatter of the row-sharded histograms by column
+// range + the bounds, bestChar and the zero-coverage scan of the rank's range, all-gather of the
+// consensus ranges (in place) + MIN of the first zero column.
+extern "C" int pw_msa_call_sharded(const pw_msa_args* a, uint32_t row_base, int32_t* counts_part,
+                                   uint64_t cols_per_rank, int rank, int nranks, void* comm, void* stream) {
+  const Rccl& r = rccl();
+  if (!r.ok) return PW_E_HIP;
+  if (!a || !a->counts || !a->consensus || !a->minmax || a->n_cols <= 0 || !comm || !counts_part || nranks < 1 ||
+      rank < 0 || rank >= nranks || cols_per_rank * (uint64_t)nranks < (uint64_t)a->n_cols)
+    return PW_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  ncclComm_t c = (ncclComm_t)comm;
+  hipLaunchKernelGGL(rebase_bad_row, dim3(1), dim3(64), 0, s, a->minmax, row_base);
+  if (hipGetLastError() != hipSuccess) return PW_E_HIP;
+  int32_t* mm = a->minmax;
+  bool ok = r.group_start() == ncclSuccess;
+  ok = ok && r.reduce_scatter(a->counts, counts_part, (size_t)cols_per_rank * 6, ncclInt32, ncclSum, c, s) == ncclSuccess;
+  ok = ok && r.all_reduce(mm, mm, 1, ncclInt32, ncclMin, c, s) == ncclSuccess;
+  ok = ok && r.all_reduce(mm + 1, mm + 1, 1, ncclInt32, ncclMax, c, s) == ncclSuccess;
+  ok = ok && r.all_reduce(mm + 2, mm + 2, 1, ncclInt32, ncclMin, c, s) == ncclSuccess;
+  ok = (r.group_end() == ncclSuccess) && ok;
+  if (!ok) return PW_E_HIP;
+  const uint64_t lo = (uint64_t)rank * cols_per_rank;
+  const int32_t c_lo = (int32_t)(lo < (uint64_t)a->n_cols ? lo : (uint64_t)a->n_cols);
+  const int32_t c_hi = (int32_t)(lo + cols_per_rank < (uint64_t)a->n_cols ? lo + cols_per_rank : (uint64_t)a->n_cols);
+  const int rc = pw_msa_call_cols(a, c_lo, c_hi, counts_part, stream);
+  if (rc != PW_OK) return rc;
+  ok = r.group_start() == ncclSuccess;
+  ok = ok && r.all_gather(a->consensus + lo, a->consensus, cols_per_rank, ncclUint8, c, s) == ncclSuccess;
+  ok = ok && r.all_reduce(mm + 3, mm + 3, 1, ncclInt32, ncclMin, c, s) == ncclSuccess;
+  ok = (r.group_end() == ncclSuccess) && ok;
+  return ok ? PW_OK : PW_E_HIP;
 }

@@ -8,13 +8,15 @@ is the multi-GPU driver of the same computation, one process per GPU:
                 694-716) and stages ITS rows (a contiguous, base-balanced block) in HBM;
   pw_msa_count  buildMSA's toMSA/addNuc/addGap scatter of those rows -> partial [n_cols x 6]
                 int32 histograms + mincol/maxcol (GapAssem.cpp:551-591, 1088-1106);
-  collectives   one all-reduce(SUM) of the histograms and MIN/MAX reductions of (mincol,
-                maxcol, first bad row): with the "nccl" backend the C-ABI's
-                pw_msa_counts_allreduce on an RCCL communicator of its own (rccl_comm), grouped
-                on the rank's stream; torch.distributed all-reduces otherwise (gloo rehearsals).
-                Integer sums are order-independent: the merged histograms are bit-identical to
-                a single-GPU count;
-  pw_msa_call   bestChar of every column (GapAssem.cpp:1048-1069), identical on every rank;
+  collectives   with the "nccl" backend (the product) the column-sharded call of the C-ABI,
+  + call        pw_msa_call_sharded on an RCCL communicator of its own (rccl_comm), on the rank's
+                stream: a reduce-scatter of the histograms by column range + MIN/MAX of (mincol,
+                maxcol, first bad row), bestChar (GapAssem.cpp:1048-1069) and the zero-coverage
+                scan of the rank's columns only, an all-gather of the consensus ranges; rank 0
+                gathers the column ranges of the histogram for the result file.  Integer sums are
+                order-independent: bit-identical to a single-GPU count.  (PW_GA_COMM=rccl-allreduce:
+                one all-reduce of the whole histogram + pw_msa_call everywhere; under gloo the
+                same through torch.distributed, for rehearsals.)
   pw_msa_refine refineMSA's consensus string and, with removeConsGaps, the closed-form
                 removeColumn/removeBase edits of the rank's own rows (GapAssem.cpp:1143-1162);
   finish_rows   the per-row tail on the host through the C-ABI: removeColumn replayed for rows
@@ -101,7 +103,9 @@ class HipEngine:
         self.torch, self.lib, self.device = torch, lib(), device
         self.stream = torch.cuda.current_stream(device)
 
-    def stage(self, lay: Layout, rows, ncols: int):
+    def stage(self, lay: Layout, rows, ncols: int, nranks: int = 1):
+        """Stage the rows; nranks > 1: the histograms and consensus padded to nranks column ranges
+        of cols_per_rank (the column-sharded call, pw_msa_call_sharded)."""
         from pwasm_amd import MsaArgs, MsaRefineArgs
         torch, dev = self.torch, self.device
         rows = list(rows)
@@ -134,9 +138,12 @@ class HipEngine:
         def e(n, dt):
             return torch.empty(max(int(n), 1), dtype=dt, device=dev)
 
+        cpr = (ncols + nranks - 1) // nranks
         d = {"seq": t(seq), "ofs": t(ofs), "row_off": t(row_off), "len": t(lens), "col0": t(col0), "cl": t(cl),
              "cr": t(cr), "slot": t(slot_base), "scr": e(3 * nslots, torch.int32),
-             "counts": e(ncols * 6, torch.int32), "cons": e(ncols, torch.uint8), "mm": e(4, torch.int32),
+             "counts": torch.zeros(max(nranks * cpr * 6, 1), dtype=torch.int32, device=dev),
+             "cons": torch.zeros(max(nranks * cpr, 1), dtype=torch.uint8, device=dev), "mm": e(4, torch.int32),
+             "cpart": e(cpr * 6, torch.int32),
              "gp": e(ncols, torch.int32), "tg": e(self.lib.pw_msa_refine_tiles(ncols), torch.int32),
              "cout": e(ncols, torch.uint8), "clen": e(1, torch.int32),
              "roffs": t(np.array([int(lay.offset[r]) for r in rows], dtype=np.int32)),
@@ -152,7 +159,7 @@ class HipEngine:
         ra.gap_prefix, ra.tile_gaps, ra.cons_out, ra.cons_len = (d[k].data_ptr() for k in ("gp", "tg", "cout", "clen"))
         ra.row_offset, ra.ofs_out, ra.offset_out, ra.numgaps_out = (d[k].data_ptr()
                                                                     for k in ("roffs", "ofso", "offo", "ngo"))
-        return dict(rows=rows, nr=nr, lens=lens, row_off=row_off, ncols=ncols, d=d, args=a, rargs=ra)
+        return dict(rows=rows, nr=nr, lens=lens, row_off=row_off, ncols=ncols, d=d, args=a, rargs=ra, cpr=cpr)
 
     def _rc(self, name, rc):
         if rc != 0:
@@ -170,6 +177,14 @@ class HipEngine:
         self._rc("pw_msa_counts_allreduce", self.lib.pw_msa_counts_allreduce(ctypes.byref(st["args"]), row_base, comm,
                                                                              self.stream.cuda_stream))
         return st["d"]["counts"], st["d"]["mm"]
+
+    def call_sharded(self, st, row_base: int, comm, rank: int, nranks: int):
+        """pw_msa_call_sharded: histograms reduce-scattered by column range over RCCL, bestChar of
+        this rank's range, the consensus all-gathered -> (consensus, minmax, this range's counts)."""
+        self._rc("pw_msa_call_sharded", self.lib.pw_msa_call_sharded(ctypes.byref(st["args"]), row_base,
+                                                                     st["d"]["cpart"].data_ptr(), st["cpr"], rank,
+                                                                     nranks, comm, self.stream.cuda_stream))
+        return st["d"]["cons"], st["d"]["mm"], st["d"]["cpart"]
 
     def call(self, st):
         """bestChar per column + first zero-coverage column (minmax[3]) from the merged counts."""
@@ -380,13 +395,26 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
     if ncols <= 0 or ncols > INT_MAX:
         return 1, ("MSAColumns op[]: bad index 0 (size=%d)\n" % ncols) if rank == 0 else "", None
     engine = engine or HipEngine()
-    st = engine.stage(lay, range(lo, hi), ncols)
+    mode = os.environ.get("PW_GA_COMM", "auto")  # auto | rccl / rccl-allreduce (also at world 1) | torch
+    use_rccl = (dist_on and isinstance(engine, HipEngine) and dist.get_backend(group) == "nccl"
+                and (mode in ("rccl", "rccl-allreduce") or (mode == "auto" and world > 1)))
+    sharded = use_rccl and mode != "rccl-allreduce"  # column-sharded call (reduce-scatter + all-gather)
+    st = engine.stage(lay, range(lo, hi), ncols, world if sharded else 1)
     counts, mm = engine.count(st)
     mm_h = [int(x) for x in mm.cpu().tolist()]
-    mode = os.environ.get("PW_GA_COMM", "auto")  # auto | rccl (also at world 1) | torch
-    use_rccl = (dist_on and isinstance(engine, HipEngine) and dist.get_backend(group) == "nccl"
-                and (mode == "rccl" or (mode == "auto" and world > 1)))
-    if use_rccl:  # the C-ABI collective (pw_msa_counts_allreduce) on this rank's stream
+    called = None
+    if sharded:  # pw_msa_call_sharded: reduce-scatter by column range, own-range bestChar, all-gather
+        cons_cols, mm, part = engine.call_sharded(st, lo, rccl_comm(group), rank, world)
+        called = (cons_cols, mm)
+        mm_h = [int(x) for x in mm.cpu().tolist()]
+        bad = mm_h[2]
+        mm_h[2] = INT_MAX
+        # the full histogram for the result file, on rank 0 only
+        parts = [torch.empty_like(part) for _ in range(world)] if rank == 0 else None
+        dist.gather(part, parts, dst=0, group=group)
+        if rank == 0:
+            counts = torch.cat(parts)[: ncols * 6]
+    elif use_rccl:  # the C-ABI all-reduce (pw_msa_counts_allreduce) on this rank's stream
         counts, mm = engine.merge(st, lo, rccl_comm(group))
         mm_h = [int(x) for x in mm.cpu().tolist()]
         bad = mm_h[2]
@@ -413,7 +441,7 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
             col = next(c for c in cols if c is not None)
         err.append("MSAColumns op[]: bad index %d (size=%d)\n" % (col, ncols))
         return 1, "".join(err) if rank == 0 else "", None
-    cons_cols, mm = engine.call(st)
+    cons_cols, mm = called if called else engine.call(st)
     zero = int(mm[3].item())
     mincol, maxcol = mm_h[0], max(mm_h[1], 0)
     if zero != INT_MAX:
@@ -449,7 +477,7 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
             if fin[r][1]:
                 return 1, "".join(err), None
     full = lay if world == 1 else Layout(layout_path, load=set(r for r in range(hdr.n) if r not in fin))
-    counts_h = counts.cpu().numpy().astype("<i4")
+    counts_h = counts.cpu().numpy().astype("<i4")[: ncols * 6]
     out = [b"PWC1", struct.pack("<6i", ncols, lay.minoffset, -1 if mincol == INT_MAX else mincol, maxcol, len(cons_s),
                                 n_removed), cons_s, counts_h.tobytes(), struct.pack("<I", hdr.n)]
     for r in range(hdr.n):

@@ -22,7 +22,7 @@ INT_MAX = 2 ** 31 - 1
 class ModelEngine:
     """CPU stand-in for HipEngine (test infrastructure only)."""
 
-    def stage(self, lay, rows, ncols):
+    def stage(self, lay, rows, ncols, nranks=1):
         return dict(lay=lay, rows=list(rows), ncols=ncols)
 
     def count(self, st):
