@@ -389,6 +389,7 @@ struct Options {
   bool single_query_gene = false;  // rlabel "" (pafreport.cpp:378-379)
   uint32_t shard = 0, nshards = 1;  // multi-GPU: only lines whose target hashes to `shard`
   bool msa = false;                 // -w: gap lists, setGap checks and the query run are kept
+  bool gpu_pack = false;            // cs strings packed on the GPU (pw_pack_cs_batch; the CLI)
 };
 
 struct RecHost {                // (trivial: lives in PodVec; pack_line sets every field)
@@ -407,6 +408,13 @@ struct RecHost {                // (trivial: lives in PodVec; pack_line sets eve
   int32_t w_msg;
   int32_t r_alnstart, t_len;
   uint32_t gap_off, n_rg, n_tg, lab_len;
+  // GPU packing (Options::gpu_pack): the cs field in Batch::cstext, and the CIGAR loop's outcome,
+  // judged once the cs totals are back (finish_gpu_pack)
+  uint64_t cs_off;
+  uint32_t cs_len;
+  int32_t cig_msg;              // CIGAR parse / op error (message index) or -1
+  int32_t cig_tpos, cig_qpos;
+  int32_t r_alnend, t_alnstart, t_alnend;
 };
 
 // Ordered log of what a batch prints: messages, records, a terminating fatal.
@@ -437,10 +445,14 @@ struct Batch {
   PodVec<uint32_t> ops;
   PodVec<uint8_t> lits;
   PodVec<int32_t> gaps;  // -w: (pos, len) pairs
+  PodVec<char> cstext;   // GPU packing: the records' cs fields back to back
+  bool gpu_packed = false;
   uint64_t text_total = 0, n_events_max = 0;
   bool fatal = false;
   void clear_out() {
     gaps.clear();
+    cstext.clear();
+    gpu_packed = false;
     hdr.clear();
     msgs.clear();
     log.clear();
@@ -479,7 +491,7 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
       break;
     }
   std::vector<uint64_t> o_desc(np + 1), o_ops(np + 1), o_lits(np + 1), o_hdr(np + 1), o_msg(np + 1), o_log(np + 1),
-      o_ev(np + 1), o_txt(np + 1), o_gap(np + 1);
+      o_ev(np + 1), o_txt(np + 1), o_gap(np + 1), o_cs(np + 1);
   for (size_t i = 0; i < np; i++) {
     const Batch& p = parts[i];
     o_desc[i + 1] = o_desc[i] + p.desc.size();
@@ -491,12 +503,14 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
     o_ev[i + 1] = o_ev[i] + p.n_events_max;
     o_txt[i + 1] = o_txt[i] + p.text_total;
     o_gap[i + 1] = o_gap[i] + p.gaps.size();
+    o_cs[i + 1] = o_cs[i] + p.cstext.size();
   }
   const size_t d0 = b.desc.size(), op0 = b.ops.size(), l0 = b.lits.size(), h0 = b.hdr.size(), m0 = b.msgs.size(),
                g0 = b.log.size();
   const uint64_t e0 = b.n_events_max;
-  const size_t gp0 = b.gaps.size();
+  const size_t gp0 = b.gaps.size(), cs0 = b.cstext.size();
   b.gaps.resize(gp0 + o_gap[np]);
+  b.cstext.resize(cs0 + o_cs[np]);
   b.desc.resize(d0 + o_desc[np]);
   b.recs.resize(d0 + o_desc[np]);
   b.ops.resize(op0 + o_ops[np]);
@@ -526,11 +540,13 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
         if (r.post_msg >= 0) r.post_msg += dm;
         if (r.w_msg >= 0) r.w_msg += dm;
         r.gap_off += (uint32_t)(gp0 + o_gap[i]);
+        r.cs_off += cs0 + o_cs[i];
         b.recs[d0 + o_desc[i] + k] = r;
       }
       if (!p.ops.empty()) memcpy(&b.ops[op0 + o_ops[i]], p.ops.data(), p.ops.size() * 4);
       if (!p.lits.empty()) memcpy(&b.lits[l0 + o_lits[i]], p.lits.data(), p.lits.size());
       if (!p.gaps.empty()) memcpy(&b.gaps[gp0 + o_gap[i]], p.gaps.data(), p.gaps.size() * 4);
+      if (!p.cstext.empty()) memcpy(&b.cstext[cs0 + o_cs[i]], p.cstext.data(), p.cstext.size());
       if (!p.hdr.empty()) memcpy(&b.hdr[h0 + o_hdr[i]], p.hdr.data(), p.hdr.size());
       for (size_t k = 0; k < p.msgs.size(); k++) b.msgs[m0 + o_msg[i] + k] = std::move(p.msgs[k]);
       for (size_t k = 0; k < p.log.size(); k++) {
@@ -543,8 +559,20 @@ void append_parts(Batch& b, std::vector<Batch>& parts, int nt) {
   b.fatal = b.fatal || parts[np - 1].fatal;
 }
 
+// The reference's message for a cs string that stops the record (pafreport.cpp:542, 620-624; D1,
+// D2): rc from pw_pack_cs, `at` = the rest of the cs string from where it stopped.
+std::string cs_error_msg(int rc, const char* s, const std::string& at) {
+  switch (rc) {
+    case PW_CS_PARSE: return strf("Error parsing cs string from line: %s (cs position: %s)\n", s, at.c_str());
+    case PW_CS_SPLICED: return strf("Error: spliced alignments not supported! at line:\n%s\n", s);
+    case PW_CS_UNHANDLED: return strf("Error: unhandled event at %s in cs, line:\n%s\n", at.c_str(), s);
+    case PW_CS_EMPTY: return strf("Error: empty indel in cs string at line:\n%s\n", s);
+    case PW_CS_BOUNDS: return strf("Error: cs string extends beyond query sequence at line:\n%s\n", s);
+    default: return strf("Error: cs string too long at line:\n%s\n", s);
+  }
+}
+
 const char* CIGAR_ERROR = "Error parsing cigar string from line: %s (cigar position: %s)\n";
-const char* CS_ERROR = "Error parsing cs string from line: %s (cs position: %s)\n";
 
 // Line classes of the pre-scan (kind) and the gene-mode dedupe verdict (dup).
 enum : uint8_t { kLineSkip = 0, kLineShort = 1, kLineSelf = 2, kLineRec = 3 };
@@ -709,6 +737,7 @@ struct Packer {
     });
     const double t_3 = prof ? now() : 0;
     append_parts(b, parts, nt);
+    b.gpu_packed = opt.gpu_pack;
     if (opt.msa) track_run(b);
     if (prof)
       fprintf(stderr, "[pack] %zu lines, %d threads: classify %.3f dedupe %.3f pack %.3f append %.3f s\n", nl, nt,
@@ -818,6 +847,13 @@ struct Packer {
     rh.pre_msg = rh.cs_msg = rh.post_msg = rh.w_msg = -1;
     rh.n_softclip = 0;
     rh.r_alnstart = r_alnstart;
+    rh.r_alnend = r_alnend;
+    rh.t_alnstart = t_alnstart;
+    rh.t_alnend = t_alnend;
+    rh.cs_off = b.cstext.size();
+    rh.cs_len = 0;
+    rh.cig_msg = -1;
+    rh.cig_tpos = rh.cig_qpos = 0;
     rh.t_len = 0;
     rh.gap_off = (uint32_t)b.gaps.size();
     rh.n_rg = rh.n_tg = rh.lab_len = 0;
@@ -862,6 +898,52 @@ struct Packer {
       rh.pre_msg = (int32_t)b.add_msg(strf(CIGAR_ERROR, s, "(null)"));
     } else if (cs == nullptr) {
       rh.pre_msg = (int32_t)b.add_msg(strf("Error: cs tag missing at line:\n%s\n", s));
+    } else if (opt.gpu_pack) {
+      // the cs field goes to the GPU packer; the CIGAR loop runs now, its verdict waits for the
+      // cs totals (finish_gpu_pack)
+      rh.cs_len = (uint32_t)(cs_end - cs);
+      b.cstext.append(cs, rh.cs_len);
+      const char* p = cigar;
+      int qpos = 0, tpos = 0;
+      std::string err;
+      while (p < cigar_end) {
+        int cl = 0;
+        if (!parse_int(p, cigar_end, cl)) {
+          err = strf(CIGAR_ERROR, s, std::string(p, cigar_end).c_str());
+          break;
+        }
+        if (p >= cigar_end) {
+          err = strf(CIGAR_ERROR, s, "");
+          break;
+        }
+        const char cop = *p;
+        bool bad = false;
+        switch (cop) {
+          case 'X':
+          case 'M':
+          case '=':
+            tpos += cl;
+            qpos += cl;
+            break;
+          case 'P':
+          case 'H': break;
+          case 'S':
+            qpos += cl;
+            rh.n_softclip++;
+            break;
+          case 'I': qpos += cl; break;
+          case 'D':
+          case 'N': tpos += cl; break;
+          default:
+            err = strf("Error: unhandled cigar_op %c (len %d) in %s\n", cop, cl, s);
+            bad = true;
+        }
+        if (bad) break;
+        ++p;
+      }
+      if (!err.empty()) rh.cig_msg = (int32_t)b.add_msg(std::move(err));
+      rh.cig_tpos = tpos;
+      rh.cig_qpos = qpos;
     } else {
       // pack cs (grow the arrays to the worst case first: one op per cs byte)
       const size_t cslen = (size_t)(cs_end - cs);
@@ -882,17 +964,7 @@ struct Packer {
       b.text_total += tot.text_bound;
       b.n_events_max += tot.n_events_max;
       if (rc != PW_CS_OK) {
-        const std::string at(cs + epos, cs_end);
-        std::string m;
-        switch (rc) {
-          case PW_CS_PARSE: m = strf(CS_ERROR, s, at.c_str()); break;
-          case PW_CS_SPLICED: m = strf("Error: spliced alignments not supported! at line:\n%s\n", s); break;
-          case PW_CS_UNHANDLED: m = strf("Error: unhandled event at %s in cs, line:\n%s\n", at.c_str(), s); break;
-          case PW_CS_EMPTY: m = strf("Error: empty indel in cs string at line:\n%s\n", s); break;
-          case PW_CS_BOUNDS: m = strf("Error: cs string extends beyond query sequence at line:\n%s\n", s); break;
-          default: m = strf("Error: cs string too long at line:\n%s\n", s); break;
-        }
-        rh.cs_msg = (int32_t)b.add_msg(std::move(m));
+        rh.cs_msg = (int32_t)b.add_msg(cs_error_msg(rc, s, std::string(cs + epos, cs_end)));
       } else {
         // CIGAR loop (pafreport.cpp:645-718): warnings and errors come after the cs loop
         const char* p = cigar;
@@ -1134,6 +1206,10 @@ struct Device {
   DevBuf<uint8_t> lits, text, work;
   DevBuf<pw_aln_result> res;
   DevBuf<pw_page> pages;
+  DevBuf<uint8_t> cs_text;  // GPU packing
+  DevBuf<uint64_t> cs_offs;
+  DevBuf<int32_t> cs_o, cs_q;
+  DevBuf<pw_cs_rec> cs_rec;
   uint32_t nq = 0;
   bool init(const QueryDb& q, bool skip_codan) {
     int n = 0;
@@ -1160,10 +1236,103 @@ struct Device {
     HIPCHK(hipStreamSynchronize(stream));
     return true;
   }
+  // GPU packing of a batch whose records carry their cs fields (Options::gpu_pack): every cs
+  // string through pw_pack_cs_batch into the device op / literal arrays (record k's ops and
+  // literal bytes start at its cs field's offset), the per-record totals back to the host, and the
+  // rest of the record's host work that needs them — descriptor (op count, tseq length, event
+  // slots, A/C/G/T flag), the cs / CIGAR verdict in the reference's order (pafreport.cpp:536-718).
+  // Records the kernel hands back (PW_PACK_HOST: not plain cs, or an op longer than a window) are
+  // packed by pw_pack_cs here, which gives the exact error, or their ops are uploaded.
+  bool gpu_pack(Batch& b, const QueryDb& q) {
+    const size_t na = b.desc.size();
+    const size_t ct = b.cstext.size();
+    std::vector<uint64_t> off(na + 1);
+    std::vector<int32_t> o(na), ql(na);
+    for (size_t k = 0; k < na; k++) {
+      off[k] = b.recs[k].cs_off;
+      o[k] = b.desc[k].offset;
+      ql[k] = b.recs[k].qlen;
+    }
+    off[na] = ct;
+    if (!cs_text.ensure(ct + 16) || !ops.ensure(ct + 16) || !lits.ensure(ct + kDevPad) || !cs_offs.ensure(na + 1) ||
+        !cs_o.ensure(na + 1) || !cs_q.ensure(na + 1) || !cs_rec.ensure(na + 1)) {
+      fprintf(stderr, "pafreport: device allocation failed\n");
+      return false;
+    }
+    if (ct) HIPCHK(hipMemcpyAsync(cs_text.p, b.cstext.data(), ct, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemsetAsync(cs_text.p + ct, 0, 16, stream));
+    HIPCHK(hipMemcpyAsync(cs_offs.p, off.data(), (na + 1) * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(cs_o.p, o.data(), na * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(cs_q.p, ql.data(), na * 4, hipMemcpyHostToDevice, stream));
+    if (pw_pack_cs_batch(cs_text.p, cs_offs.p, cs_o.p, cs_q.p, (uint32_t)na, ops.p, lits.p, cs_rec.p, stream) != PW_OK) {
+      fprintf(stderr, "pafreport: cs packing launch failed\n");
+      return false;
+    }
+    std::vector<pw_cs_rec> rec(na);
+    HIPCHK(hipMemcpyAsync(rec.data(), cs_rec.p, na * sizeof(pw_cs_rec), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    uint64_t ev = 0, txt = 0;
+    std::vector<uint32_t> hops;
+    std::vector<uint8_t> hlits;
+    for (size_t k = 0; k < na; k++) {
+      RecHost& rh = b.recs[k];
+      pw_aln_desc& d = b.desc[k];
+      d.op_begin = d.lit_begin = (uint32_t)rh.cs_off;
+      d.ev_begin = ev;
+      if (rh.pre_msg >= 0) continue;  // no cs loop (pafreport.cpp:521-524)
+      const char* s = b.buf.data() + rh.line_off;
+      const char* cs = b.cstext.data() + rh.cs_off;
+      const int qi = (int)(d.ref & PW_REF_QMASK);
+      pw_cs_totals tot;
+      int rc = PW_CS_OK;
+      int32_t epos = 0;
+      bool acgt;
+      if (rec[k].flags & PW_PACK_HOST) {
+        hops.resize((size_t)rh.cs_len + 1);
+        hlits.resize((size_t)rh.cs_len + 1);
+        rc = pack_cs_n(cs, cs + rh.cs_len, d.offset, rh.qlen, hops.data(), hops.size(), hlits.data(), hlits.size(), &tot,
+                       &epos);
+        if (rc == PW_CS_OK && tot.n_ops) HIPCHK(hipMemcpy(ops.p + rh.cs_off, hops.data(), tot.n_ops * 4, hipMemcpyHostToDevice));
+        if (rc == PW_CS_OK && tot.n_lits) HIPCHK(hipMemcpy(lits.p + rh.cs_off, hlits.data(), tot.n_lits, hipMemcpyHostToDevice));
+        acgt = rc == PW_CS_OK && q.all_acgt(qi);
+        for (uint32_t i = 0; i < tot.n_lits && acgt; i++) acgt = QueryDb::is_acgt_byte(hlits[i]);
+      } else {
+        tot.q_total = rec[k].q_total;
+        tot.t_total = rec[k].t_total;
+        tot.n_ops = rec[k].n_ops;
+        tot.n_lits = rec[k].n_lits;
+        tot.n_events_max = rec[k].n_events_max;
+        tot.text_bound = rec[k].text_bound;
+        acgt = q.all_acgt(qi) && (rec[k].flags & PW_PACK_ACGT);
+      }
+      d.n_ops = tot.n_ops;
+      d.t_len = tot.t_total;
+      if (acgt) d.ref |= PW_REF_ACGT;
+      ev += tot.n_events_max;
+      txt += tot.text_bound;
+      if (rc != PW_CS_OK) {
+        rh.cs_msg = (int32_t)b.add_msg(cs_error_msg(rc, s, std::string(cs + epos, cs + rh.cs_len)));
+      } else if (rh.cig_msg >= 0) {
+        rh.post_msg = rh.cig_msg;
+      } else {
+        const int eff_t_len = rh.t_alnend - rh.t_alnstart, tpos = rh.cig_tpos, qpos = rh.cig_qpos;
+        if (eff_t_len != tpos || tot.t_total != tpos)
+          rh.post_msg = (int32_t)b.add_msg(strf("Error: tseq alignment length mismatch (%d vs %d(%d-%d)) at line:%s\n",
+                                                tpos, eff_t_len, rh.t_alnend, rh.t_alnstart, s));
+        else if (rh.r_alnend - rh.r_alnstart != qpos)
+          rh.post_msg = (int32_t)b.add_msg(strf("Error: ref alignment length mismatch (%d vs %d-%d) at line:%s\n", qpos,
+                                                rh.r_alnend, rh.r_alnstart, s));
+      }
+    }
+    b.n_events_max = ev;
+    b.text_total = txt;
+    return true;
+  }
   // run the batch; fills results / pages on the host (and the text, unless text_h is null: the
   // CLI streams it with a TextStream instead)
-  bool run(const Batch& b, bool skip_codan, std::vector<uint8_t>* text_h, std::vector<pw_aln_result>& res_h,
-           std::vector<pw_page>& pages_h) {
+  bool run(Batch& b, const QueryDb& q, bool skip_codan, std::vector<uint8_t>* text_h,
+           std::vector<pw_aln_result>& res_h, std::vector<pw_page>& pages_h) {
+    if (b.gpu_packed && !b.desc.empty() && !gpu_pack(b, q)) return false;
     const size_t na = b.desc.size();
     res_h.resize(na);
     const uint64_t np = pw_report_page_count(b.n_events_max);
@@ -1602,6 +1771,9 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   pk.opt.verbose = verbose;
   pk.opt.single_query_gene = (qdb.ids.size() == 1 && !fullgenome);
   pk.opt.msa = fmsa.f != nullptr;
+  // cs strings are packed on the GPU unless -w needs the op stream on the host
+  // (the query run's MSA is built there) or PW_PACK_HOST=1 asks for the host packer
+  pk.opt.gpu_pack = !pk.opt.msa && !(getenv("PW_PACK_HOST") && atoi(getenv("PW_PACK_HOST")) != 0);
   // Pipeline: while the GPU runs batch k and its report is written, batch k + 1 is read and
   // packed (by pk.nt threads); nothing past a fatal batch is packed.
   ChunkReader rd(in.f);
@@ -1635,7 +1807,7 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
       nxt = std::async(std::launch::async, [&, o] { return pack_next(bb[o]); });
     }
     const double t_r0 = prof ? now() : 0;
-    bool ran = dev.run(B, skip_codan, nullptr, res_h, pages_h);
+    bool ran = dev.run(B, qdb, skip_codan, nullptr, res_h, pages_h);
     ran = ran && tstream.init() &&
           tstream.begin(dev.text.p, pages_h, pw_report_page_count(B.n_events_max));
     const double t_r1 = prof ? now() : 0;

@@ -40,18 +40,65 @@ struct PkOp {
   bool emit;      // an op word is written (':0' is dropped)
 };
 
+// A record's head, loaded one record ahead: its extent, offset / query length and the first
+// window as aligned dwords (lane l: bytes [a0 + 4l, a0 + 4l + 4); lane 0 also the dword after the
+// window, which an unaligned start needs).  Addresses past the record are clamped to its last
+// dword: the caller's text is only readable up to the last record's end (+16 bytes).
+struct PkHead {
+  uint64_t base, L;
+  int off, ql;
+  uint32_t d0, d1;
+};
+__device__ __forceinline__ void pk_head(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
+                                        const int32_t* qlen, uint32_t ri, int lane, PkHead& h) {
+  h.base = cs_off[ri];
+  h.L = cs_off[ri + 1] - h.base;
+  h.off = offset[ri];
+  h.ql = qlen[ri];
+  const uint64_t a0 = h.base & ~3ull, last = h.L ? (h.base + h.L - 1) & ~3ull : a0;
+  const uint64_t x0 = a0 + 4ull * (uint64_t)lane, x1 = a0 + 256ull;
+  h.d0 = *reinterpret_cast<const uint32_t*>(text + (x0 < last ? x0 : last));
+  h.d1 = *reinterpret_cast<const uint32_t*>(text + (x1 < last ? x1 : last));
+}
+// stage window bytes [pos, pos + 256) of the record into w (from the dwords of pk_head when pos
+// is 0, else loaded here); returns the window's shift inside the staging buffer
+__device__ __forceinline__ int pk_stage(const uint8_t* text, const PkHead& h, uint64_t pos, int lane, LDS uint8_t* wr,
+                                        bool first) {
+  const uint64_t st = h.base + pos, a0 = st & ~3ull, last = (h.base + h.L - 1) & ~3ull;
+  uint32_t d0 = h.d0, d1 = h.d1;
+  if (!first) {
+    const uint64_t x0 = a0 + 4ull * (uint64_t)lane, x1 = a0 + 256ull;
+    d0 = *reinterpret_cast<const uint32_t*>(text + (x0 < last ? x0 : last));
+    d1 = *reinterpret_cast<const uint32_t*>(text + (x1 < last ? x1 : last));
+  }
+  *reinterpret_cast<LDS uint32_t*>(wr + 4 * lane) = d0;
+  if (lane == 0) *reinterpret_cast<LDS uint32_t*>(wr + 256) = d1;
+  return (int)(st & 3ull);
+}
+
+// Persistent wavefronts: wave g takes records g, g + NW, ...; the next record's head and first
+// window are loaded before this one is decoded, so their latency hides behind the decode (the
+// per-record work is a short dependent chain: load -> classify -> scans -> stores).
 __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
                                                       const int32_t* qlen, uint32_t n, uint32_t* ops, uint8_t* lits,
                                                       pw_cs_rec* out) {
-  __shared__ uint8_t win[4][kPackWin + 4];
+  __shared__ uint8_t win[4][kPackWin + 8];   // staged window (shifted by the start's alignment)
+  __shared__ uint8_t wz[4][kPackWin + 8];    // the window from its first character, zeros past its end
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar loop)
-  // (an address-space-3 pointer: through a generic one every window read would be a flat load,
+  // (address-space-3 pointers: through a generic one every window read would be a flat load,
   // which also waits for the wave's outstanding global stores)
-  LDS uint8_t* w = (LDS uint8_t*)win[wv];
+  LDS uint8_t* wr = (LDS uint8_t*)win[wv];
+  LDS uint8_t* w = (LDS uint8_t*)wz[wv];
   const uint32_t nw = gridDim.x * 4;
-  for (uint32_t ri = blockIdx.x * 4 + (uint32_t)wv; ri < n; ri += nw) {
-    const uint64_t base = cs_off[ri], L = cs_off[ri + 1] - base;
-    const int off = offset[ri], ql = qlen[ri];
+  uint32_t ri = blockIdx.x * 4 + (uint32_t)wv;
+  if (ri >= n) return;
+  PkHead nxt;
+  pk_head(text, cs_off, offset, qlen, ri, lane, nxt);
+  for (; ri < n; ri += nw) {
+    const PkHead cur = nxt;
+    if (ri + nw < n) pk_head(text, cs_off, offset, qlen, ri + nw, lane, nxt);
+    const uint64_t base = cur.base, L = cur.L;
+    const int off = cur.off, ql = cur.ql;
     int qpos = 0, tpos = 0;
     uint32_t nops = 0, nlits = 0, nev = 0;
     uint64_t bound = 0;
@@ -60,14 +107,18 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
     while (pos < L && !bad) {
       const int wl = (int)(L - pos < (uint64_t)kPackWin ? L - pos : (uint64_t)kPackWin);
       const bool last_win = pos + (uint64_t)wl == L;
-      // stage the window (4 bytes per lane; zeros past its end)
+      // stage the window (aligned dword loads, then this lane's 4 characters re-read at the
+      // window's shift; zeros past its end)
+      const int sh = pk_stage(text, cur, pos, lane, wr, pos == 0);
+      __builtin_amdgcn_wave_barrier();
       uint32_t c4 = 0;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int i = 4 * lane + j;
-        const uint32_t c = i < wl ? text[base + pos + (uint64_t)i] : 0u;
+        const uint32_t c = i < wl ? (uint32_t)wr[sh + i] : 0u;
         c4 |= c << (8 * j);
       }
+      __builtin_amdgcn_wave_barrier();
       *reinterpret_cast<LDS uint32_t*>(w + 4 * lane) = c4;
       if (lane == 0) *reinterpret_cast<LDS uint32_t*>(w + kPackWin) = 0u;
       __builtin_amdgcn_wave_barrier();
@@ -247,9 +298,14 @@ extern "C" int pw_pack_cs_batch(const uint8_t* cs_text, const uint64_t* cs_off, 
                                 void* stream) {
   if (!cs_text || !cs_off || !offset || !qlen || !ops || !lits || !out) return PW_E_ARG;
   if (n == 0) return PW_OK;
-  // a wavefront per record (the per-record work is a short dependent chain: more waves in flight,
-  // not a longer loop per wave, hide it)
-  const uint32_t grid = (n + 3) / 4 < (1u << 20) ? (n + 3) / 4 : (1u << 20);
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
+  }
+  // persistent wavefronts, two rounds of 8 resident workgroups per CU
+  const uint32_t cap = (uint32_t)ncu * 16u;
+  const uint32_t grid = (n + 3) / 4 < cap ? (n + 3) / 4 : cap;
   hipLaunchKernelGGL(pw::pack_cs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, cs_text, cs_off, offset, qlen,
                      n, ops, lits, out);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
