@@ -9,26 +9,34 @@
 //   codon consequence predictImpact                        pafreport.cpp:801-883
 //   event line        printDiffInfo (event loop)           pafreport.cpp:893-954
 //
-// One pass (pw_report_events) is four launches on one stream:
+// One pass (pw_report_events) is these launches on one stream (pw_stop_table_build, the
+// per-query next-stop table, may run on a side stream: pw_report_events_after):
 //
-//  index_kernel     one wavefront per PAF record: wave prefix scans over the packed op stream
-//                   give every op its query / target / literal coordinates (the sequential walk
-//                   of pafreport.cpp:536-626), '*' ops are base-checked, directly consecutive '*'
-//                   ops merged into one S event (:556-560), and every event is written as a
-//                   32-byte render record (+ a 16-byte cold record) into its record's event
-//                   slots, already in OUTPUT order ('-' records fill their slots back to front =
-//                   tdiffs.Reverse(), :643).  Target contexts that need an op walk (another event
-//                   within 5 bases) are rendered here, where the op words are in LDS.
-//  render_kernel    lane-dense: one wavefront takes 64 consecutive event slots (across record
-//                   boundaries) from a work ticket, each lane renders its event's report line
-//                   into an LDS line buffer, a decoupled look-back over the chunks gives the
-//                   chunk's place in the contiguous text, and the wave writes the lines with
-//                   16-byte stores.  The forward query bytes an event reads are staged per lane
-//                   (a 64-byte LDS window around the event); the next chunk's records are
-//                   loaded while the current one renders.
-//  fixup_kernel     lines longer than the line buffer (S runs with many changed codons),
-//                   written in place.
-//  finalize_kernel  per-record results (text offset/length, event count, errors).
+//  plan_kernel,     only when a record has more than PW_BLOCK_OPS (2048) ops: such records are cut
+//  carry_kernel     into blocks of 2048 ops; one wavefront per block sums its query / target /
+//                   literal advance and event heads, so blocks can be decoded independently.
+//  index_kernel     one wavefront per PAF record (per block of a long record): DPP wave prefix
+//                   scans over the packed op stream give every op its query / target / literal
+//                   coordinates (the sequential walk of pafreport.cpp:536-626), '*' ops are
+//                   base-checked by ballot, directly consecutive '*' ops merged into one S event
+//                   (:556-560), and every event is written as a 32-byte Hot record (+ a 16-byte
+//                   Cold record for a record's first / last line) into its record's event slots,
+//                   already in OUTPUT order ('-' records fill their slots back to front =
+//                   tdiffs.Reverse(), :643).  Events whose target context needs an op walk are
+//                   flagged for tctx_kernel.
+//  tctx_kernel      a wavefront takes 256 slots, compacts the flagged ones by ballot and walks
+//                   each one's op stream through LDS windows (setTContext, :120-128): a 32-byte
+//                   pre-rendered target-context record.
+//  render_kernel    lane-dense: wavefront g takes chunks g, g + NW, ... of 64 consecutive event
+//                   slots (static stride, no work queue); each lane renders its event's report
+//                   line into an LDS line buffer from its Hot record and a 48-byte forward-query
+//                   window staged per lane (loaded one chunk ahead); a wave whose lanes all
+//                   qualify renders through the RecFast instantiation (every read in registers
+//                   or the window, no fallbacks).  A DPP scan of the line lengths places the
+//                   lines in the chunk's page and the wave writes them with 16-byte stores.
+//  fixup_kernel     lines longer than the line buffer (~0.06 %), rendered again straight to
+//                   their reserved place in the page.
+//  finalize_kernel  per-record results (text length across pages, event count, errors).
 //
 // The text is one contiguous stream of event lines in record order; record headers are
 // formatted by the host (the only floating-point value, coverage:%.2f).
@@ -154,6 +162,14 @@ struct Rec {
   uint32_t n_ops;
   bool rev;
   bool acgt;                // query and the record's literals are all A/C/G/T (register fast paths)
+  static constexpr bool kFast = false;
+};
+// A render lane whose every read is known to hit its registers or its LDS query window (the
+// render_kernel predicate fast_lane()): query bytes straight from the window, literal bytes from
+// the Hot record's 8, codons from the A/C/G/T table, and every byte-wise fallback compiled out.
+// A wavefront takes this instantiation of emit_event when all its lanes qualify.
+struct RecFast : Rec {
+  static constexpr bool kFast = true;
 };
 
 // Query byte x of the forward query, 0 outside [0, L) (the NUL / missing bytes).  The LDS
@@ -167,6 +183,7 @@ __device__ __forceinline__ uint8_t Rc(const Rec& r, int x) {
   if (o < (unsigned)r.qn) return r.qw[o];
   return rc_global(r.R, r.L, x);
 }
+__device__ __forceinline__ uint8_t Rc(const RecFast& r, int x) { return r.qw[x - r.qlo]; }
 __device__ __noinline__ uint8_t lit_global(const uint8_t* lits, uint32_t i) { return lits[i]; }
 __device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
   const uint32_t o = i - r.ls0;
@@ -174,6 +191,10 @@ __device__ __forceinline__ uint8_t litb(const Rec& r, uint32_t i) {
   const uint32_t ow = i - r.l_lo;
   if (ow < r.l_n) return r.lw[ow];
   return lit_global(r.lits, i);
+}
+__device__ __forceinline__ uint8_t litb(const RecFast& r, uint32_t i) {
+  const uint32_t o = i - r.ls0;
+  return (uint8_t)((o < 4 ? r.lit0 : r.lit1) >> (8 * (o & 3)));
 }
 __device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
   const unsigned o = (unsigned)((int)j - r.op_lo);
@@ -201,6 +222,12 @@ __device__ __forceinline__ uint8_t translate(const LDS SmallTables* t, uint8_t a
   if (is_acgt(a) && is_acgt(b) && is_acgt(c))
     return t->codon64[((a >> 1) & 3u) << 4 | ((b >> 1) & 3u) << 2 | ((c >> 1) & 3u)];
   return translate_iupac(a, b, c);
+}
+// translateCodon as the record's lane needs it (a fast lane's bytes are all A/C/G/T)
+template <class R>
+__device__ __forceinline__ uint8_t tr(const R& r, uint8_t a, uint8_t b, uint8_t c) {
+  if constexpr (R::kFast) return r.tab->codon64[((a >> 1) & 3u) << 4 | ((b >> 1) & 3u) << 2 | ((c >> 1) & 3u)];
+  else return translate(r.tab, a, b, c);
 }
 
 __device__ __forceinline__ uint32_t op_tadv(uint32_t w) {
@@ -243,13 +270,15 @@ struct EvIn {
 constexpr int kNsNone = INT_MIN;
 
 // evtbases[i] in final orientation, upper case (pafreport.cpp:563,594-596,612-614,637,895)
-__device__ __forceinline__ uint8_t ev_base(const Rec& r, const Event& e, int i) {
+template <class R>
+__device__ __forceinline__ uint8_t ev_base(const R& r, const Event& e, int i) {
   if (e.type == PW_OP_SUB) return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i))] : litb(r, e.ls + 2 * i);
   if (e.type == PW_OP_INS) return r.rev ? r.tab->comp[litb(r, e.ls + (e.n - 1 - i))] : litb(r, e.ls + i);
   return r.rev ? comp2(Rc(r, e.rloc + i)) : Rc(r, e.q_pos + i);
 }
 // evtsub[i] (S only)
-__device__ __forceinline__ uint8_t ev_sub(const Rec& r, const Event& e, int i) {
+template <class R>
+__device__ __forceinline__ uint8_t ev_sub(const R& r, const Event& e, int i) {
   return r.rev ? r.tab->comp[litb(r, e.ls + 2 * (e.n - 1 - i) + 1)] : litb(r, e.ls + 2 * i + 1);
 }
 
@@ -550,8 +579,8 @@ __device__ __forceinline__ bool tctx_fast(const TGeom& g, uint32_t typ, int n, u
 }
 
 // The tctx field, fast form: ll query bytes, the event's own target bases, rl query bytes.
-template <class S>
-__device__ __forceinline__ void emit_tctx_fast(S& k, const Rec& r, uint32_t typ, int n, int qp, uint32_t ls, int ll,
+template <class S, class R>
+__device__ __forceinline__ void emit_tctx_fast(S& k, const R& r, uint32_t typ, int n, int qp, uint32_t ls, int ll,
                                                int rl) {
   const int nm = typ == PW_OP_DEL ? 0 : (typ == PW_OP_SUB ? 1 : n);
   // aligned query start after the event; '-' records read the forward query in the other
@@ -560,8 +589,8 @@ __device__ __forceinline__ void emit_tctx_fast(S& k, const Rec& r, uint32_t typ,
   const int f1 = r.rev ? r.L - qpa - rl : qp - ll, n1 = r.rev ? rl : ll;
   const int f2 = r.rev ? r.L - qp : qpa, n2 = r.rev ? ll : rl;
   const int o1 = f1 - r.qlo, o2 = f2 - r.qlo;
-  if (r.acgt && r.qn == kQWin && o1 >= 0 && o2 >= 0 && o1 + 8 <= kQWin && o2 + 8 <= kQWin && r.ln == 8 &&
-      ls == r.ls0 && nm <= 8) {
+  if (R::kFast || (r.acgt && r.qn == kQWin && o1 >= 0 && o2 >= 0 && o1 + 8 <= kQWin && o2 + 8 <= kQWin && r.ln == 8 &&
+                    ls == r.ls0 && nm <= 8)) {
     // register images (comp2 is the identity on A/C/G/T): 8 query bytes each side, the event's
     // target bases from the literal registers, lower case
     const uint64_t a = lds8(r.qw, o1), b = lds8(r.qw, o2);
@@ -619,7 +648,8 @@ __device__ __forceinline__ void emit_tctx_walk(S& k, const Rec& r, uint32_t typ,
 }
 
 // S consequence, one codon of modseq (predictImpact, pafreport.cpp:811-826)
-__device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, uint8_t& aa, uint8_t& maa) {
+template <class R>
+__device__ __forceinline__ void sub_codon(const R& r, const Event& e, int ao, uint8_t& aa, uint8_t& maa) {
   const int p0 = e.rloc - e.r_trloc;
   uint8_t m[3], o[3];
 #pragma unroll
@@ -628,8 +658,8 @@ __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, 
     o[j] = Rc(r, e.r_trloc + pos);
     m[j] = (pos >= p0 && pos < p0 + e.n) ? ev_base(r, e, pos - p0) : o[j];
   }
-  aa = translate(r.tab, o[0], o[1], o[2]);
-  maa = translate(r.tab, m[0], m[1], m[2]);
+  aa = tr(r, o[0], o[1], o[2]);
+  maa = tr(r, m[0], m[1], m[2]);
 }
 
 // The five codons of modseq and the four reference codons after the first (predictImpact's
@@ -637,12 +667,15 @@ __device__ __forceinline__ void sub_codon(const Rec& r, const Event& e, int ao, 
 // LDS window, inside the query and all A/C/G/T (the common case; anything else -> false and
 // the byte-wise path).  m(p) = Q[r_trloc + p] (p < a), X[p - a] (a <= p < a + x),
 // Q[r_trloc + p + dl - x] (after the event).
-__device__ __forceinline__ bool indel_codons_fast(const Rec& r, const Event& e, int a, int x, int dl, uint8_t (&mm)[5],
+template <class R>
+__device__ __forceinline__ bool indel_codons_fast(const R& r, const Event& e, int a, int x, int dl, uint8_t (&mm)[5],
                                                   uint8_t (&rr)[5]) {
-  if (!r.acgt || r.qn != kQWin || x > 8 || a + x > 15) return false;
-  if (x > 0 && (r.ln != 8 || e.ls != r.ls0)) return false;  // inserted bases not in registers
+  if constexpr (!R::kFast) {
+    if (!r.acgt || r.qn != kQWin || x > 8 || a + x > 15) return false;
+    if (x > 0 && (r.ln != 8 || e.ls != r.ls0)) return false;  // inserted bases not in registers
+  }
   const int o0 = e.r_trloc - r.qlo, o1 = o0 + dl - x;
-  if (o0 < 0 || o1 < 0 || o0 + 16 > kQWin || o1 + 16 > kQWin) return false;
+  if (!R::kFast && (o0 < 0 || o1 < 0 || o0 + 16 > kQWin || o1 + 16 > kQWin)) return false;
   const u128 q0 = lds16(r.qw, o0), q1 = lds16(r.qw, o1);
   u128 xs = 0;
   if (x > 0) {
@@ -670,11 +703,13 @@ __device__ __forceinline__ uint32_t pack_even4(uint64_t v) {  // bytes 0, 2, 4, 
   return (uint32_t)(v & 0xFFu) | (uint32_t)((v >> 8) & 0xFF00u) | (uint32_t)((v >> 16) & 0xFF0000u) |
          (uint32_t)((v >> 24) & 0xFF000000u);
 }
-__device__ __forceinline__ bool sub_image(const Rec& r, const Event& e, int p0, u128& q0, u128& m, int& modseq_err) {
+template <class R>
+__device__ __forceinline__ bool sub_image(const R& r, const Event& e, int p0, u128& q0, u128& m, int& modseq_err) {
   // (codons up to byte 8 of q0 are read: all inside the query, none reaches the NUL)
-  if (!r.acgt || r.qn != kQWin || e.n > 4 || r.ln != 8 || e.ls != r.ls0 || e.r_trloc + 9 > r.L) return false;
+  if (!R::kFast && (!r.acgt || r.qn != kQWin || e.n > 4 || r.ln != 8 || e.ls != r.ls0 || e.r_trloc + 9 > r.L))
+    return false;
   const int o0 = e.r_trloc - r.qlo;
-  if (o0 < 0 || o0 + 16 > kQWin) return false;
+  if (!R::kFast && (o0 < 0 || o0 + 16 > kQWin)) return false;
   q0 = lds16(r.qw, o0);
   const uint64_t l64 = (uint64_t)r.lit1 << 32 | r.lit0;  // (target, query) pairs
   uint32_t alt = pack_even4(l64), sub = pack_even4(l64 >> 8);
@@ -696,8 +731,8 @@ __device__ __forceinline__ bool sub_image(const Rec& r, const Event& e, int p0, 
 // (D; s = rloc + len).  Codons touching the prefix / X / the first five codons are translated
 // explicitly; past that, modseq codons are query codons and the first stop is one lookup in the
 // next-stop table.
-template <class S>
-__device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e, int ns_pre) {
+template <class S, class R>
+__device__ __forceinline__ void indel_impact(S& k, const R& r, const Event& e, int ns_pre) {
   const int a = e.rloc - e.r_trloc;
   const int x = (e.type == PW_OP_INS) ? e.n : 0;
   const int dl = (e.type == PW_OP_DEL) ? e.n : 0;
@@ -707,7 +742,7 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
   int stop_i = -1;
   uint32_t aa4 = 0, maa4 = 0;
   int aa4n = 0, maa4n = 0;
-  if (a + x <= 15) {
+  if (R::kFast || a + x <= 15) {  // (a fast lane's insertion is at most 8 bases)
     // the reference scans codons i = 0,3,..,12 (while i+2 < M), stopping at the first stop;
     // here all five codons and the four reference codons are read and translated at once
     // (independent reads, no loop-carried latency) and the scan is replayed on the results
@@ -724,8 +759,8 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
       }
 #pragma unroll
       for (int c = 0; c < 5; c++) {
-        mm[c] = translate(r.tab, m[3 * c], m[3 * c + 1], m[3 * c + 2]);
-        rr[c] = c == 0 ? 0 : translate(r.tab, Rc(r, e.r_trloc + 3 * c), Rc(r, e.r_trloc + 3 * c + 1),
+        mm[c] = tr(r, m[3 * c], m[3 * c + 1], m[3 * c + 2]);
+        rr[c] = c == 0 ? 0 : tr(r, Rc(r, e.r_trloc + 3 * c), Rc(r, e.r_trloc + 3 * c + 1),
                                        Rc(r, e.r_trloc + 3 * c + 2));
       }
     }
@@ -767,14 +802,14 @@ __device__ __forceinline__ void indel_impact(S& k, const Rec& r, const Event& e,
         const int p = i + j;
         m[j] = (p < a) ? Rc(r, e.r_trloc + p) : (p < a + x ? ev_base(r, e, p - a) : Rc(r, sfx + p - a - x));
       }
-      const uint8_t mm = translate(r.tab, m[0], m[1], m[2]);
+      const uint8_t mm = tr(r, m[0], m[1], m[2]);
       if (mm == '.') {
         stop_i = i;
         break;
       }
       if (i > 0 && maa4n < 4) {
         if (i + 2 < trlen) {
-          aa4 |= (uint32_t)translate(r.tab, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1),
+          aa4 |= (uint32_t)tr(r, Rc(r, e.r_trloc + i), Rc(r, e.r_trloc + i + 1),
                                      Rc(r, e.r_trloc + i + 2))
                  << (8 * aa4n);
           aa4n++;
@@ -819,8 +854,8 @@ __device__ __forceinline__ int event_rloc(int L, bool rev, uint32_t typ, int qp,
 // Write one event's report line (printDiffInfo, pafreport.cpp:886-953) to the sink as the
 // fields become known.  Returns the evtsub index failing the modseq check
 // (pafreport.cpp:811-814), or -1; `rel` receives rloc - r_trloc for the error message.
-template <class S>
-__device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bool skip, int& rel) {
+template <class S, class R>
+__device__ __forceinline__ int emit_event(S& k, const R& r, const EvIn& in, bool skip, int& rel) {
   Event e;
   const uint32_t typ = in.typ;
   e.type = typ;
@@ -830,7 +865,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   e.rloc = event_rloc(r.L, r.rev, typ, in.qp, in.n);
   // amino acid at the event (pafreport.cpp:897-899)
   const int aap0 = e.rloc / 3;
-  const uint8_t aa = translate(r.tab, Rc(r, 3 * aap0), Rc(r, 3 * aap0 + 1), Rc(r, 3 * aap0 + 2));
+  const uint8_t aa = tr(r, Rc(r, 3 * aap0), Rc(r, 3 * aap0 + 1), Rc(r, 3 * aap0 + 2));
   e.r_trloc = aap0 > 0 ? 3 * (aap0 - 1) : 0;  // 3*(aapos-2), clipped at 0
   rel = e.rloc - e.r_trloc;
 
@@ -847,7 +882,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
       o.put('\t');
     });
   // ---- bases field ("[n]" past MAX_EVLEN, pafreport.cpp:928-941); homopolymer uniformity; tloc
-  const bool big = e.n > kMaxEv;
+  const bool big = !R::kFast && e.n > kMaxEv;
   const uint8_t b0 = ev_base(r, e, 0);
   bool same = true;
   if (big)
@@ -903,7 +938,7 @@ __device__ __forceinline__ int emit_event(S& k, const Rec& r, const EvIn& in, bo
   {
     uint32_t rw0 = 0, rw1 = 0, rw2 = 0;
     const int oc = c0 - r.qlo;
-    if (r.qn == kQWin && oc >= 0 && oc + 16 <= kQWin) {  // one image from the window
+    if (R::kFast || (r.qn == kQWin && oc >= 0 && oc + 16 <= kQWin)) {  // one image from the window
       const u128 im = lds16(r.qw, oc);
       rw0 = (uint32_t)im;
       rw1 = (uint32_t)(im >> 32);
@@ -1844,7 +1879,24 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       k.line = my_line;
       k.pos = 0;
       int rel = 0;
-      const int merr = emit_event(k, r, in, skip, rel);
+      // the fast instantiation when every active lane's reads are in its registers / window: A/C/G/T,
+      // at least 8 query bytes before the event (the window starts at or before rloc - 8, so it
+      // covers [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8 bases whose modseq tail
+      // image starts inside the window, deletions of <= 12 (the largest read, the tail image at
+      // r_trloc + deletion, ends by rloc + 25)
+      const int rlc = event_rloc(r.L, rev, typ, h.qp, n);
+      const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
+      const bool fast = r.acgt && rlc >= 8 && pre.qlo <= rlc - 8 &&
+                        (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L)
+                                          : (typ == PW_OP_INS ? (n <= 8 && rt - pre.qlo >= n) : n <= 12));
+      int merr;
+      if (__ballot(!fast) == 0) {
+        RecFast rf;
+        static_cast<Rec&>(rf) = r;
+        merr = emit_event(k, rf, in, skip, rel);
+      } else {
+        merr = emit_event(k, r, in, skip, rel);
+      }
       linelen = k.pos;
       if (merr >= 0) {  // modseq error: first failing event of the record in output order
         const uint32_t ai = rec_of_slot(A, s);

@@ -17,12 +17,15 @@ from test_shard import _with_duplicates_and_comments
 pytestmark = pytest.mark.gpu
 
 
-def _rank(rank, world, port, argv, errf, q):
+def _rank(rank, world, port, argv, errf, q, backend="gloo", env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank), PW_DIST_BACKEND="gloo")
+                      LOCAL_RANK=str(rank), PW_DIST_BACKEND=backend, **(env or {}))
     if rank == 0:
         fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
         os.dup2(fd, 2)
+        if os.environ.get("PW_TEST_STDOUT"):  # (rank 0's stdout into a file)
+            fo = os.open(os.environ["PW_TEST_STDOUT"], os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+            os.dup2(fo, 1)
     from pwasm_amd import mgpu
     import torch.distributed as dist
     rc = mgpu.main(argv)
@@ -31,7 +34,7 @@ def _rank(rank, world, port, argv, errf, q):
     q.put((rank, rc))
 
 
-def run_mgpu(world, argv, tmp_path):
+def run_mgpu(world, argv, tmp_path, backend="gloo", env=None):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -39,7 +42,7 @@ def run_mgpu(world, argv, tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     errf = str(tmp_path / "mg.err")
-    ps = [ctx.Process(target=_rank, args=(r, world, port, argv, errf, q)) for r in range(world)]
+    ps = [ctx.Process(target=_rank, args=(r, world, port, argv, errf, q, backend, env)) for r in range(world)]
     for p in ps:
         p.start()
     rcs = dict(q.get(timeout=300) for _ in range(world))
@@ -106,3 +109,34 @@ def test_mgpu_cfg3_shards_gene_mode(built, tmp_path):
     rc, err = run_mgpu(2, ["-G", "-C", "-r", fa, paf, "-o", str(out)], tmp_path)
     orc, oout, oerr = run([ORACLE, "-G", "-C", "-r", fa, paf])
     assert (rc, out.read_bytes(), err) == (orc, oout, oerr) and orc == 0
+
+
+def test_mgpu_many_batches_per_rank(built, tmp_path):
+    """Each rank's lines in several pipelined batches (PW_CHUNK_BYTES): the q~t dedupe state moves
+    from batch to batch, the output offsets span all of them."""
+    fa, paf = synth_paf(tmp_path, 0, seed=19)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 4)
+    out = tmp_path / "r.txt"
+    rc, err = run_mgpu(2, ["-r", fa, dup, "-o", str(out)], tmp_path, env={"PW_CHUNK_BYTES": "4000"})
+    orc, oout, oerr = run([ORACLE, "-r", fa, dup])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr)
+
+
+def test_mgpu_stdout(built, tmp_path):
+    """No -o: the file assembled at offsets goes to rank 0's stdout."""
+    fa, paf = synth_paf(tmp_path, 0, seed=23)
+    so = tmp_path / "stdout.txt"
+    rc, err = run_mgpu(2, ["-r", fa, paf], tmp_path, env={"PW_TEST_STDOUT": str(so)})
+    orc, oout, oerr = run([ORACLE, "-r", fa, paf])
+    assert (rc, so.read_bytes(), err) == (orc, oout, oerr)
+
+
+@pytest.mark.skipif(__import__("torch").cuda.device_count() < 2, reason="needs two GPUs (RCCL ranks)")
+def test_mgpu_rccl_two_gpus(built, tmp_path):
+    """The node configuration: one rank per GPU, collectives over RCCL ("nccl")."""
+    fa, paf = synth_paf(tmp_path, 0, seed=29)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 5)
+    out = tmp_path / "r.txt"
+    rc, err = run_mgpu(2, ["-r", fa, dup, "-o", str(out)], tmp_path, backend="nccl")
+    orc, oout, oerr = run([ORACLE, "-r", fa, dup])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr)

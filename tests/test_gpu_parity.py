@@ -49,6 +49,15 @@ def test_edge_mix(built, tmp_path, seed):
     assert out.count(b"\n") > 100
 
 
+@pytest.mark.parametrize("seed", [1, 7])
+def test_edge_mix_host_packer(built, tmp_path, seed, monkeypatch):
+    """The CLI packs cs strings on the GPU by default (pw_pack_cs_batch); PW_PACK_HOST=1 keeps the
+    host packer (the -w path uses it always): same bytes either way."""
+    monkeypatch.setenv("PW_PACK_HOST", "1")
+    fa, paf = synth_paf(tmp_path, 0, seed=seed)
+    same(["-r", fa, paf])
+
+
 @pytest.mark.parametrize("flags", [[], ["-C"], ["-N"], ["-G"], ["-F"], ["-G", "-C"], ["-F", "-C"]])
 def test_modes(built, tmp_path, flags):
     fa, paf = synth_paf(tmp_path, 0, seed=11)
