@@ -370,7 +370,9 @@ void pw_batch_free(pw_batch* b);
 /* `pafreport -w`: the multi-FASTA MSA of the batch's last query run (refMSA->writeMSA,
  * pafreport.cpp:382-421, 447-450; GapAssem.cpp:645-753, 1006-1046) from its gap lists — the
  * query's gap profile is the elementwise max of the alignments' query gaps and target-only
- * bases are left-packed in it.  Needs flags bit4. */
+ * bases are left-packed in it.  Needs flags bit4, and gene mode: in full-genome
+ * mode (-F, or auto for a FASTA over 120000 bytes) it returns PW_E_ARG, as the reference refuses
+ * -w there ("can only generate MSA for -G mode", pafreport.cpp:263-268). */
 int pw_batch_write_msa(const pw_batch* b, const char* path);
 
 /* ---------------------------------------------------------------- multi-GPU
