@@ -1029,7 +1029,7 @@ __device__ __forceinline__ int emit_event(S& k, const R& r, const EvIn& in, bool
 //   ctr      u32 [1] long-line count, [2] overflow flags; u64 at byte 16: arena bytes used
 //   rec_mod  per record: modseq error key (first failing line in output order)
 //   hot/cold per event slot (Hot, Cold); tx: pre-rendered target contexts
-//   sflag    per slot: 1 = tctx_kernel renders its target context (zeroed per pass)
+//   sflag    per slot: 1 = tctx_kernel renders its target context (index_kernel writes every slot's)
 //   fix      long-line list
 struct Fixup {
   uint32_t s, pad;
@@ -1456,6 +1456,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           hh.l0 = hl0[k];
           hh.l1 = hl1[k];
           W.hot[s] = hh;
+          W.sflag[s] = fast ? (uint8_t)0 : (uint8_t)1;  // (every slot's flag is written: no memset)
           if (kidx == 0 || lastc || n >= kNBig) {  // only the first / last line and saturated lengths read it
             Cold cd;
             cd.ai = ai;
@@ -1471,7 +1472,6 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       // an S run, a long insertion) are rendered by tctx_kernel: flag the slot and leave the
       // walk's start (head op, its query / target position, record geometry) in its tx record
       if (slow) {
-        W.sflag[s] = 1;
         v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
         dtx[0] = (v4u){d.op_begin, sb + (uint32_t)(64 * k + lane), n_ops, (uint32_t)qs[k]};
         dtx[1] = (v4u){(uint32_t)ts[k], (uint32_t)T, (uint32_t)d.offset, 0u};
@@ -1491,11 +1491,17 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     const uint32_t f0 = ev < nmax ? ev : nmax, f1 = B.ev1 < nmax ? B.ev1 : nmax;
     if (f1 > f0) {
       const uint64_t a0 = rev ? evb + nmax - f1 : evb + f0, a1 = rev ? evb + nmax - f0 : evb + f1;
-      for (uint64_t s = a0 + lane; s < a1; s += kWave) W.hot[s].fn = kNoEv;
+      for (uint64_t s = a0 + lane; s < a1; s += kWave) {
+        W.hot[s].fn = kNoEv;
+        W.sflag[s] = 0;
+      }
     }
     if (B.sb1 == n_ops && B.tot < nmax) {
       const uint64_t a0 = rev ? evb : evb + B.tot, a1 = rev ? evb + nmax - B.tot : evb + nmax;
-      for (uint64_t s = a0 + lane; s < a1; s += kWave) W.hot[s].fn = kNoEv;
+      for (uint64_t s = a0 + lane; s < a1; s += kWave) {
+        W.hot[s].fn = kNoEv;
+        W.sflag[s] = 0;
+      }
     }
     if (lane == 0) {
       if (B.k == 0) {
@@ -1517,6 +1523,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     }
     return;
   }
+  if (!layout_ok && pre.ev_next >= evb && pre.ev_next <= A.n_ev_slots)  // (contract violation: no events)
+    for (uint64_t s = evb + lane; s < pre.ev_next; s += kWave) {
+      W.hot[s].fn = kNoEv;
+      W.sflag[s] = 0;
+    }
   const bool ev_over = ev > nmax;
   if (ev_over) {  // host event bound violated (cannot happen: every head is a counted op)
     err = PW_REC_OVERFLOW;
@@ -1524,7 +1535,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   }
   // empty slots: merged '*' runs, or everything after a failure
   const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;  // (none if !layout_ok)
-  for (uint64_t s = h0 + lane; s < h1; s += kWave) W.hot[s].fn = kNoEv;
+  for (uint64_t s = h0 + lane; s < h1; s += kWave) {
+    W.hot[s].fn = kNoEv;
+    W.sflag[s] = 0;
+  }
   // the last created event was flagged when written unless the last segment had no event head
   // (or the event bound was violated): then flag it now, after this wave's store of its record
   if (lane == 0 && ev > 0 && err == PW_REC_OK && (ev_last_seg == 0 || ev_over)) {
@@ -1610,7 +1624,10 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
   // the padding slots of the last chunk are empty
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
   if (blockIdx.x == 0)
-    for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) W.hot[s].fn = kNoEv;
+    for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) {
+      W.hot[s].fn = kNoEv;
+      W.sflag[s] = 0;
+    }
 }
 
 // ------------------------------------------------------------------ long records: plan + carries
@@ -2173,6 +2190,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
 }
 
 // ------------------------------------------------------------------ fixup_kernel
+__device__ __forceinline__ void finalize_record(const pw_report_args& A, const Work& W, uint32_t ai);
 // Lines longer than the LDS line buffer, one per thread, rewritten in place (their bytes were
 // reserved).  The thread stages the same windows as render_kernel (query bytes around the event,
 // the tx record) plus 32 literal bytes in LDS, so only the line itself goes to global memory.
@@ -2191,6 +2209,9 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   __syncthreads();
   LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x];
   const bool skip = A.skip_codan != 0;
+  // the per-record results first (finalize_kernel's work: one launch less per pass; they do not
+  // depend on the long lines' bytes)
+  for (uint32_t ai = blockIdx.x * 256 + threadIdx.x; ai < A.n_alns; ai += gridDim.x * 256) finalize_record(A, W, ai);
   if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
   // a wave takes 64 chunks at a time and spreads their long lines over its lanes (line j of the
   // group -> lane j % 64): the chunk of line j is the last one whose prefix is <= j
@@ -2291,9 +2312,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
 }
 
 // ------------------------------------------------------------------ finalize_kernel
-__global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W) {
-  const uint32_t ai = blockIdx.x * 256 + threadIdx.x;
-  if (ai >= A.n_alns) return;
+__device__ __forceinline__ void finalize_record(const pw_report_args& A, const Work& W, uint32_t ai) {
   const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;
   pw_aln_result r = A.results[ai];
   if (W.ctr[2]) {
@@ -2336,6 +2355,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W)
     }
   }
   A.results[ai] = r;
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W) {
+  const uint32_t ai = blockIdx.x * 256 + threadIdx.x;
+  if (ai < A.n_alns) finalize_record(A, W, ai);
 }
 
 // ------------------------------------------------------------------ next-stop table
@@ -2457,7 +2481,6 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   pw::work_layout(static_cast<uint8_t*>(args->workspace), args->n_ev_slots, args->n_alns, &W);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;  // counters
-  if (W.n_chunks && hipMemsetAsync(W.sflag, 0, W.n_chunks * pw::kWave, st) != hipSuccess) return PW_E_HIP;
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
   const bool planned = args->max_rec_ops == 0 || args->max_rec_ops > (uint32_t)pw::kBlkOps;
@@ -2480,9 +2503,10 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     // (render is the first kernel that reads next_stop)
     if (next_stop_ready && hipStreamWaitEvent(st, (hipEvent_t)next_stop_ready, 0) != hipSuccess) return PW_E_HIP;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);
+    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);  // (+ finalize)
+  } else {
+    hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);
   }
-  hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
