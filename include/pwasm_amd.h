@@ -171,7 +171,8 @@ typedef struct pw_msa_args {
   const int32_t* clip_l;    /* [n_rows] oriented left clip */
   const int32_t* clip_r;    /* [n_rows] oriented right clip */
   const int64_t* slot_base; /* [n_rows + 1] from pw_msa_slots */
-  int32_t* scratch;         /* [3 * n_slots] (chunk sums, checkpoints, slot -> row) */
+  int32_t* scratch;         /* [pw_msa_scratch_words(n_slots, n_rows)] (chunk sums, checkpoints,
+                               slot -> row, per-chunk gap lists, per-row counted extents) */
   int32_t* counts;          /* [n_cols][6] A,C,G,T,N,- (GAlnColumn::counts order) */
   uint8_t* consensus;       /* [n_cols] bestChar() per column ('-' for gap), 0 = no coverage */
   int32_t* minmax;          /* [4]: mincol, maxcol, first out-of-range row, first zero column */
@@ -182,6 +183,8 @@ typedef struct pw_msa_args {
 
 /* Host helper: fills slot_base[n_rows + 1], returns n_slots. */
 uint64_t pw_msa_slots(const int32_t* row_len_host, uint32_t n_rows, int64_t* slot_base_host);
+/* int32 words of pw_msa_args.scratch for a layout of n_slots slots and n_rows rows. */
+uint64_t pw_msa_scratch_words(uint64_t n_slots, uint32_t n_rows);
 
 /* Replaces GSeqAlign::buildMSA -> GASeq::toMSA -> GAlnColumn::addNuc/addGap and
  * GAlnColumn::bestChar (GapAssem.cpp:551-591, 1048-1069, 1088-1106; GapAssem.h:295-337).

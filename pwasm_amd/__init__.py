@@ -114,6 +114,7 @@ _SIGS = {
     "pw_stop_table_build": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "pw_msa_slots": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "pw_msa_scratch_words": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint32]),
     "pw_msa_columns": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_count": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
     "pw_msa_call": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.c_void_p]),
@@ -198,6 +199,8 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(f"pwasm_amd: native library missing ({LIB_PATH}); run `make` / __graft_entry__.build()")
         L = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("PWASM_LIB") and not hasattr(L, name):
+                continue  # (an older experiment build: tools/exp_build.py)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

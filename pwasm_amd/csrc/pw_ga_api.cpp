@@ -914,7 +914,7 @@ void GSeqAlign::buildMSA() {
     D->cl.alloc(n_stage);
     D->cr.alloc(n_stage);
     D->slot.alloc(n_stage + 1);
-    D->scr.alloc(3 * nslots);
+    D->scr.alloc(pw_msa_scratch_words(nslots, n_stage));
     D->counts.alloc(ncols * 6);
     D->cons.alloc(ncols);
     D->mm.alloc(4);

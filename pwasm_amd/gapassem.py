@@ -140,7 +140,7 @@ class HipEngine:
 
         cpr = (ncols + nranks - 1) // nranks
         d = {"seq": t(seq), "ofs": t(ofs), "row_off": t(row_off), "len": t(lens), "col0": t(col0), "cl": t(cl),
-             "cr": t(cr), "slot": t(slot_base), "scr": e(3 * nslots, torch.int32),
+             "cr": t(cr), "slot": t(slot_base), "scr": e(self._scratch_words(nslots, nr), torch.int32),
              "counts": torch.zeros(max(nranks * cpr * 6, 1), dtype=torch.int32, device=dev),
              "cons": torch.zeros(max(nranks * cpr, 1), dtype=torch.uint8, device=dev), "mm": e(4, torch.int32),
              "cpart": e(cpr * 6, torch.int32),
@@ -160,6 +160,10 @@ class HipEngine:
         ra.row_offset, ra.ofs_out, ra.offset_out, ra.numgaps_out = (d[k].data_ptr()
                                                                     for k in ("roffs", "ofso", "offo", "ngo"))
         return dict(rows=rows, nr=nr, lens=lens, row_off=row_off, ncols=ncols, d=d, args=a, rargs=ra, cpr=cpr)
+
+    def _scratch_words(self, nslots: int, nr: int) -> int:
+        f = getattr(self.lib, "pw_msa_scratch_words", None)
+        return int(f(nslots, nr)) if f is not None else 3 * nslots  # (older experiment builds)
 
     def _rc(self, name, rc):
         if rc != 0:

@@ -5,7 +5,9 @@ RCCL refuses two ranks on one GPU; on a node every rank has its own GPU and the 
 node-wide per-genome table must equal one computed from the PAF and the oracle's report."""
 import collections
 import os
+import queue
 import socket
+import time
 
 import pytest
 import torch.multiprocessing as mp
@@ -18,6 +20,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _rank(rank, world, port, argv, errf, q, backend="gloo", env=None):
+    import faulthandler
+    tb = open(f"{errf}.rank{rank}.tb", "w")
+    faulthandler.dump_traceback_later(100, exit=True, file=tb)  # a hung rank names where it hangs
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), PW_DIST_BACKEND=backend, **(env or {}))
     if rank == 0:
@@ -45,7 +50,21 @@ def run_mgpu(world, argv, tmp_path, backend="gloo", env=None):
     ps = [ctx.Process(target=_rank, args=(r, world, port, argv, errf, q, backend, env)) for r in range(world)]
     for p in ps:
         p.start()
-    rcs = dict(q.get(timeout=300) for _ in range(world))
+    rcs = {}
+    deadline = time.time() + 150
+    while len(rcs) < world:  # (fail as soon as a rank dies or hangs, with its traceback)
+        try:
+            r, rc = q.get(timeout=5)
+            rcs[r] = rc
+            continue
+        except queue.Empty:
+            pass
+        dead = [p.exitcode for p in ps if p.exitcode not in (None, 0)]
+        if dead or time.time() > deadline:
+            for p in ps:
+                p.kill()
+            tbs = "".join(open(f"{errf}.rank{r}.tb").read() for r in range(world) if os.path.exists(f"{errf}.rank{r}.tb"))
+            raise AssertionError(f"ranks exit {dead or 'hung'}; stderr: {open(errf, 'rb').read()[-2000:]!r}\n{tbs}")
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -173,12 +173,19 @@ FX_PAR = [
 ]
 
 
+def rev_src(rev):
+    return subprocess.run(["git", "show", f"{rev}:pwasm_amd/csrc/pw_report.hip"], cwd=REPO, check=True,
+                          capture_output=True, text=True).stdout
+
+
 def variants():
     """name -> source text; edit this table per experiment (splice(), patched())"""
     cur, head = open(SRC).read(), head_src()
     return {
         "head": head,
         "cur": cur,
+        "base3": lambda: rev_src("8ee5aa5"),  # round 3 before the render fast lanes
+        "fast3": lambda: rev_src("1c76643"),  # + RecFast
         "fx_lds": lambda: patched(cur, FX_LDS),
         "fx_par": lambda: patched(cur, FX_PAR),
         "r_grid6": lambda: patched(cur, [("if (rg > (uint64_t)ncu * pw::kRenderOcc) rg = (uint64_t)ncu * pw::kRenderOcc;",
