@@ -5,21 +5,25 @@
 //   GAlnColumn::addGap/Nuc  GapAssem.h:295-337     6 counters A,C,G,T,N,- (+ layers)
 //   GAlnColumn::bestChar    GapAssem.cpp:1048-1069 stable qsort + N/- tie rule
 //   GSeqAlign::buildMSA     GapAssem.cpp:1088-1106
-// The reference scatters row by row (one NucOri allocation per base).  Here ofs is read once and
-// seq once per pass, column tile by column tile:
+// The reference scatters row by row (one NucOri allocation per base).  Here ofs and seq are each
+// read once per pass from HBM:
 //   K0 slot_rows:      row of every chunk slot (no per-chunk binary search later)
-//   K1 row_chunk_sums: per 256-base chunk of a row, sum of (1 + max(ofs,0)) and the chunk's list
-//                      of positive gaps (<= 8 entries, 32 B per 256 bases)
-//   K2 row_prefix:     per row, exclusive scan of the chunk sums -> layout column at which each
-//                      chunk's first gap run starts (checkpoints), row end column, bounds check,
-//                      the row's counted column extent, mincol / maxcol
-//   K3 tile_counts:    one 1024-thread workgroup per 2048-column tile; its 16 waves walk the
-//                      chunks of every row that overlaps the tile, place each base's bin code in
-//                      a per-wave LDS column strip (columns from the checkpoint + gap list, no
-//                      scan), then count the strip into packed register counters; no LDS atomic
-//                      per base.  The tile writes its counts coalesced.
-//                      (pw_msa_count stops here: with rows sharded over GPUs the partial
-//                      counts are summed by an all-reduce before the call)
+//   K1 row_chunk_sums: per 256-base chunk of a row (16 lanes, 16 bases each), sum of
+//                      (1 + max(ofs,0)) and the chunk's gap runs in layout order as
+//                      (column offset in the chunk, length) — 32 B per chunk instead of 512 B of ofs
+//   K2 row_prefix:     per row, exclusive scan of the chunk sums -> checkpoints (layout column at
+//                      which each chunk's first gap run starts), row end column, bounds check, the
+//                      counted extent, mincol / maxcol, and for every 2048-column tile that starts
+//                      inside the row its first chunk and first base (the tile start table)
+//   K3 tile_counts:    one 8-wave workgroup per 2048-column tile; lane l of a wave owns the tile's
+//                      columns [32l, 32l + 32) for every row the wave takes.  Per row: a 2 KB window
+//                      of the row's bases is staged in LDS (loaded a row ahead), the tile's gap-column
+//                      bitmap is built from the runs of the <= 9 chunks that reach the tile, and each
+//                      lane expands its bases into its columns 4 at a time (the bitmap's popcounts
+//                      give the source offset, a v_perm inserts the gap characters) and adds them to
+//                      32 packed 5-bit register counters — no scatter, no atomic per base.
+//                      (pw_msa_count stops here: with rows sharded over GPUs the partial counts are
+//                      summed by an all-reduce before the call)
 //   K4 call_columns:   bestChar of every column (pw_msa_call)
 //   K5 zero_scan:      first zero-coverage column in [mincol, maxcol] (ErrZeroCov, :1121-1131).
 // Column-closed form of bestChar: max count wins, ties resolved A<C<G<T; a tie between only N
@@ -38,7 +42,7 @@
 // for ofs >= 0 (the walk of :766-771 sees raw ofs values; negative input gaps are refused).
 //   K6 gap_tiles / K7 gap_scan: G per column (tile counts + in-tile scan) and the consensus
 //                      string ('-' -> '*', or gap columns dropped)
-//   K8 row_edit:       ofs' of every base (chunked like K3)
+//   K8 row_edit:       ofs' of every base (one wave per chunk, columns from the checkpoints)
 //   K9 row_finish:     offset', numgaps', then removeClipGaps on ofs' (i <= clipL and
 //                      i >= seqlen - clipR) unless keep_clip_gaps (refineClipping first, host)
 #include <hip/hip_runtime.h>
@@ -50,9 +54,11 @@
 
 namespace pw {
 
+#define LDS __attribute__((address_space(3)))
 constexpr int kChunk = 256;   // bases per checkpoint chunk
-constexpr int kTileW = 2048;  // columns per workgroup
+constexpr int kTileW = 2048;  // columns per refine tile
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 // GAlnColumn::addNuc / addGap bin (GapAssem.h:295-337): toupper(c) A,C,G,T -> 0..3, '-' / '*' ->
@@ -67,6 +73,13 @@ __device__ __forceinline__ int bin_of(uint32_t c) {
   return b;
 }
 
+// a value the compiler must treat as per-lane (a load through it stays a vector load kept in
+// VGPRs instead of a scalar load whose lgkmcnt wait would also hold every LDS wait after it)
+__device__ __forceinline__ int64_t vary(int64_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // K0: the row of every slot (slot_row), one workgroup per row, coalesced
 __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row) {
   if (blockIdx.x == 0 && threadIdx.x < 4)  // minmax sentinels (no host copy on the stream)
@@ -75,111 +88,102 @@ __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* s
     for (int64_t k = A.slot_base[r] + threadIdx.x; k < A.slot_base[r + 1]; k += 256) slot_row[k] = (int32_t)r;
 }
 
-// K1: per 256-base chunk of a row, sum of (1 + max(ofs, 0)) and the chunk's gap list: the
-// (base index in chunk, gap) of every ofs > 0 (~1 % of bases in an assembly layout), at most
-// kGapCap per chunk, unordered, 0 = unused, kGapOverflow in entry 0 when a chunk has more (K3
-// then re-reads that chunk's ofs).  K3 reads these 32 bytes per chunk instead of 512 bytes of
-// ofs, so the layout's ofs is read once per pass.  A wavefront takes 8 consecutive slots at a
-// time, 8 lanes per slot, 32 bases per lane (four 16-byte loads when the row starts 8-base
-// aligned); the next group's loads are issued before this group is reduced.
-constexpr int kGapCap = 8;
-constexpr uint32_t kGapOverflow = 0xFFFFFFFFu;
+// K1: per 256-base chunk, sum of (1 + max(ofs, 0)) and its gap runs.  A run is the gap before a
+// base with ofs > 0 (~1 % of bases in an assembly layout): entry = (column offset of the run in
+// the chunk, from the chunk's checkpoint) << 16 | length, in layout order, at most kRunCap per
+// chunk, 0 = unused; kRunOverflow in entry 0 when a chunk has more runs or its columns pass 16 bits
+// (K2 / K3 then read that chunk's ofs).  A wavefront takes 4 consecutive slots at a time, 16 lanes
+// per slot, 16 bases per lane (two 16-byte loads when the row starts 8-base aligned); the next
+// group's loads are issued before this group is reduced.
+constexpr int kRunCap = 8;
+constexpr uint32_t kRunOverflow = 0xFFFFFFFFu;
 struct SumPre {
-  v4i q[4];
+  v4u q0, q1;
   uint64_t roff;
   int len, i0;
-  int s;        // (element path) the sum
-  uint32_t pm;  // (element path) bit t: base i0 + t has ofs > 0
-  bool vec;
+  bool vec, live;
 };
 __device__ __forceinline__ void sums_load(const pw_msa_args& A, const int32_t* slot_row, uint64_t g, int lane, SumPre& p) {
-  const uint64_t c = g * 8 + (uint64_t)(lane >> 3);
-  p.len = 0;
-  p.vec = false;
-  p.s = 0;
-  p.pm = 0;
-  if (c >= A.n_slots) return;
-  const uint32_t r = (uint32_t)slot_row[c];
-  const int64_t k = (int64_t)c - A.slot_base[r];
+  const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
+  p.live = c < A.n_slots;
+  const uint64_t cc = p.live ? c : A.n_slots - 1;
+  const uint32_t r = (uint32_t)slot_row[cc];
+  const int64_t k = (int64_t)cc - A.slot_base[r];
   p.len = A.row_len[r];
-  p.i0 = (int)(k * kChunk) + 32 * (lane & 7);
   p.roff = A.row_off[r];
-  p.vec = (p.roff & 7) == 0 && p.i0 + 32 <= p.len;
-  if (p.vec) {
-    const v4i* src = reinterpret_cast<const v4i*>(A.ofs + p.roff + p.i0);
-#pragma unroll
-    for (int w = 0; w < 4; w++) p.q[w] = src[w];
-  } else {
-    for (int i = p.i0; i < p.i0 + 32 && i < p.len; i++) {  // row tail / unaligned row
-      const int gg = A.ofs[p.roff + i];
-      p.s += 1 + (gg > 0 ? gg : 0);
-      p.pm |= gg > 0 ? 1u << (i - p.i0) : 0u;
-    }
-  }
+  p.i0 = (int)(k * kChunk) + 16 * (lane & 15);
+  p.vec = (p.roff & 7) == 0 && p.i0 + 16 <= p.len;
+  // (unconditional loads: a row tail or unaligned row reads the scratch instead and takes the
+  // element path when consumed)
+  const v4u* src = p.vec ? reinterpret_cast<const v4u*>(A.ofs + p.roff + p.i0) : reinterpret_cast<const v4u*>(A.scratch);
+  p.q0 = src[0];
+  p.q1 = src[1];
+}
+__device__ __forceinline__ uint32_t row16_scan_incl(uint32_t v) {  // inclusive prefix within each 16-lane row
+  v += dpp_or_zero<0x111>(v);
+  v += dpp_or_zero<0x112>(v);
+  v += dpp_or_zero<0x114>(v);
+  v += dpp_or_zero<0x118>(v);
+  return v;
 }
 __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const int32_t* slot_row,
-                                                      uint32_t* glist) {
-  const int lane = threadIdx.x & 63, sub = lane & 7;
-  const uint64_t ng = (A.n_slots + 7) / 8;
+                                                      uint32_t* runs) {
+  const int lane = threadIdx.x & 63, sub = lane & 15;
+  const uint64_t ng = (A.n_slots + 3) / 4;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ng) return;
   SumPre cur;
-  if (g < ng) sums_load(A, slot_row, g, lane, cur);
+  sums_load(A, slot_row, g, lane, cur);
   for (; g < ng; g += nw) {
     SumPre nxt;
-    if (g + nw < ng) sums_load(A, slot_row, g + nw, lane, nxt);
-    int s = cur.s;
-    uint32_t pm = cur.pm;
+    sums_load(A, slot_row, g + nw < ng ? g + nw : g, lane, nxt);
+    asm volatile("" : "+v"(cur.q0), "+v"(cur.q1));
+    uint32_t w[8];  // 16 int16 gaps, two per dword
     if (cur.vec) {
-      s = 32;
+      w[0] = cur.q0.x, w[1] = cur.q0.y, w[2] = cur.q0.z, w[3] = cur.q0.w;
+      w[4] = cur.q1.x, w[5] = cur.q1.y, w[6] = cur.q1.z, w[7] = cur.q1.w;
+    } else {  // row tail / unaligned row
 #pragma unroll
-      for (int w = 0; w < 16; w++) {
-        const uint32_t d = (uint32_t)cur.q[w >> 2][w & 3];
-        const int lo = max((int)(int16_t)(d & 0xFFFFu), 0), hi = max((int)(int16_t)(d >> 16), 0);
-        s += lo + hi;
-        pm |= (uint32_t)min(lo, 1) << (2 * w) | (uint32_t)min(hi, 1) << (2 * w + 1);
-      }
+      for (int d = 0; d < 8; d++) w[d] = 0;
+      for (int i = 0; i < 16 && cur.i0 + i < cur.len; i++)
+        w[i >> 1] |= (uint32_t)(uint16_t)A.ofs[cur.roff + cur.i0 + i] << (16 * (i & 1));
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    // gap-list slots: exclusive prefix of the 8 lanes' counts
+    const int nv = cur.live ? min(max(cur.len - cur.i0, 0), 16) : 0;  // bases of this lane
+    int s = 0;
+    uint32_t pm = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+      const int lo = max((int)(int16_t)(w[d] & 0xFFFFu), 0), hi = max((int)(int16_t)(w[d] >> 16), 0);
+      s += lo + hi;
+      pm |= (uint32_t)min(lo, 1) << (2 * d) | (uint32_t)min(hi, 1) << (2 * d + 1);
+    }
+    if (!cur.live) s = 0, pm = 0;
     const int n = __popc(pm);
-    int incl = n;
-#pragma unroll
-    for (int d = 1; d < 8; d <<= 1) {
-      const int t = __shfl_up(incl, d, 64);
-      if (sub >= d) incl += t;
-    }
-    const int total = __shfl(incl, lane | 7, 64);
-    const uint64_t c = g * 8 + (uint64_t)(lane >> 3);
-    if (c < A.n_slots) {
-      if (sub == 0) chunk_sum[c] = s;
-      uint32_t* gl = glist + c * kGapCap;
-      if (total > kGapCap) {
-        if (sub == 0) gl[0] = kGapOverflow;
+    const uint32_t is = row16_scan_incl((uint32_t)s), in = row16_scan_incl((uint32_t)n), iv = row16_scan_incl((uint32_t)nv);
+    const int ts = __shfl((int)is, lane | 15, 64), tn = __shfl((int)in, lane | 15, 64), tv = __shfl((int)iv, lane | 15, 64);
+    const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
+    if (cur.live) {
+      if (sub == 0) chunk_sum[c] = tv + ts;
+      uint32_t* rl = runs + c * kRunCap;
+      if (tn > kRunCap || tv + ts > 0xFFFF) {
+        if (sub == 0) rl[0] = kRunOverflow;
       } else {
-        if (sub >= total) gl[sub] = 0u;
-        int slot = incl - n;
-        const uint32_t base = (uint32_t)(32 * sub);
-        while (pm) {  // (~0.3 per lane)
+        if (sub < kRunCap && sub >= tn) rl[sub] = 0u;
+        int slot = (int)in - n;
+        int col = 16 * sub + ((int)is - s);  // column offset of this lane's first base's gap run
+        int prev = 0;                        // base index (in the lane) the column offset refers to
+        while (pm) {                         // (~0.15 runs per lane)
           const int t = __builtin_ctz(pm);
           pm &= pm - 1;
-          uint32_t gg;
-          if (cur.vec) {  // from the registers: dword t / 2 of the 16 (a select tree, no reload)
-            const int d = t >> 1;
-            uint32_t w4[4];
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-              const v4i& v = cur.q[w];
-              w4[w] = (uint32_t)((d & 2) ? ((d & 1) ? v.w : v.z) : ((d & 1) ? v.y : v.x));
-            }
-            const uint32_t dw = (d & 8) ? ((d & 4) ? w4[3] : w4[2]) : ((d & 4) ? w4[1] : w4[0]);
-            gg = (t & 1) ? dw >> 16 : dw & 0xFFFFu;
-          } else {
-            gg = (uint32_t)(uint16_t)A.ofs[cur.roff + cur.i0 + t];
-          }
-          gl[slot++] = (base + (uint32_t)t) << 16 | gg;
+          const int d = t >> 1;
+          const uint32_t dw = (d & 4) ? ((d & 2) ? ((d & 1) ? w[7] : w[6]) : ((d & 1) ? w[5] : w[4]))
+                                      : ((d & 2) ? ((d & 1) ? w[3] : w[2]) : ((d & 1) ? w[1] : w[0]));
+          const uint32_t gg = (t & 1) ? dw >> 16 : dw & 0xFFFFu;
+          col += t - prev;
+          prev = t;
+          rl[slot++] = (uint32_t)col << 16 | gg;
+          col += (int)gg;
         }
       }
     }
@@ -190,11 +194,16 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
 // K2: one 1024-thread workgroup per row: chunk checkpoints (column where chunk k's first gap run
 // starts) = col0 + exclusive scan of the chunk sums, row extent, bounds check
 // (MSAColumns::operator[], GapAssem.h:366-370).  Thread t owns a contiguous run of chunks.
-// Also K3's row record rinfo[8r..8r+7] = {ext_lo, ext_hi, first column, end column + 1, length,
-// chunks, first slot (2 words)}, where [ext_lo, ext_hi] = [first column of the gap run before
-// base lo, column of base hi - 1] is the counted extent of the unclipped bases [lo, hi) (empty:
-// ext_lo > ext_hi), and mincol / maxcol (minmax[0] / [1]: GSeqAlign's minoffset/length
-// bookkeeping over the bases toMSA counts): waves 0 / 1 scan the chunk holding lo / hi - 1.
+// K3's row record rinfo[8r..8r+7] = {ext_lo, ext_hi, first column, end column + 1, length,
+// chunks | (no tile table) << 31, first slot (2 words)}, where [ext_lo, ext_hi] = [first column of
+// the gap run before base lo, column of base hi - 1] is the counted extent of the unclipped bases
+// [lo, hi) (empty: ext_lo > ext_hi), and mincol / maxcol (minmax[0] / [1]: GSeqAlign's
+// minoffset/length bookkeeping over the bases toMSA counts): waves 0 / 1 scan the chunk holding
+// lo / hi - 1.  The tile start table: for every tile t whose first column c0 lies in the row
+// (first column < c0 < end column), tstart[first slot + t - floor(first column / kCntW)] =
+// {chunk holding c0, first base at or after c0} (the row has room for it in its slots unless its
+// gaps inflate it more than 8-fold: then the row is flagged and K3 searches).
+constexpr int kCntW = 2048;  // K3 tile width
 __device__ __forceinline__ int chunk_cols_upto(const pw_msa_args& A, uint64_t roff, int i0, int i_end, int lane) {
   // sum over bases [i0, i_end) of 1 + max(ofs, 0) (i_end - i0 <= kChunk), wave-uniform result
   int s = 0;
@@ -207,11 +216,40 @@ __device__ __forceinline__ int chunk_cols_upto(const pw_msa_args& A, uint64_t ro
   for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
   return s;
 }
+// first base of chunk k (row-relative index) whose column is >= column x of the chunk (x from its
+// checkpoint, 0 <= x < its column span): from the runs, or (overflowed chunk) by walking its ofs
+__device__ __forceinline__ int first_base_at(const pw_msa_args& A, const uint32_t* rl, uint64_t roff, int k, int len,
+                                             int x) {
+  if (rl[0] != kRunOverflow) {
+    int G = 0;
+#pragma unroll 1
+    for (int e = 0; e < kRunCap; e++) {
+      const uint32_t v = rl[e];
+      if (v == 0) break;
+      const int co = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
+      if (x < co) break;
+      if (x < co + gg) return k * kChunk + co - G;  // inside the run: the base after it
+      G += gg;
+    }
+    return k * kChunk + x - G;
+  }
+  int col = 0;
+  const int i1 = min(k * kChunk + kChunk, len);
+#pragma unroll 1
+  for (int i = k * kChunk; i < i1; i++) {
+    col += max((int)A.ofs[roff + i], 0);
+    if (col >= x) return i;
+    col++;
+  }
+  return i1;
+}
 constexpr int kRowInfo = 8;  // int32 words per row record
+constexpr uint32_t kNoTable = 0x80000000u;
 __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const int32_t* chunk_sum, int32_t* ckpt,
-                                                   int32_t* rinfo) {
+                                                   int32_t* rinfo, const uint32_t* runs, int32_t* tstart) {
   __shared__ int wsum[16];
   __shared__ int ck_s[2];
+  __shared__ uint32_t notab;
   const int64_t* chunk_base = A.slot_base;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
@@ -221,6 +259,10 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
     const int len = A.row_len[r];
     const int lo = max(A.clip_l[r], 0), hi = min(len - A.clip_r[r], len);  // counted bases [lo, hi)
     const int64_t klo = b + lo / kChunk, khi = b + (hi - 1) / kChunk;
+    const uint64_t roff = A.row_off[r];
+    const int rs = A.col0[r];
+    const int t_first = rs >> 11;  // floor(rs / kCntW)
+    if (t == 0) notab = 0;
     int mine = 0;
     for (int64_t k = k0; k < k1; k++) mine += chunk_sum[k];
     int incl = mine;
@@ -231,33 +273,48 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
     }
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int base = A.col0[r];
+    int base = rs;
     for (int w = 0; w < wv; w++) base += wsum[w];
     int run = base + incl - mine;
     int32_t* ri = rinfo + (int64_t)kRowInfo * r;
-    if (t == 0) {
-      int end = A.col0[r];
-      for (int w = 0; w < 16; w++) end += wsum[w];
-      ri[2] = A.col0[r];
-      ri[3] = end;
-      ri[4] = len;
-      ri[5] = (int)(e - 1 - b);
-      ri[6] = (int)(uint32_t)(uint64_t)b;
-      ri[7] = (int)(uint32_t)((uint64_t)b >> 32);
-    }
     for (int64_t k = k0; k < k1; k++) {
       if (k == klo) ck_s[0] = run;
       if (k == khi) ck_s[1] = run;
       ckpt[k] = run;
-      run += chunk_sum[k];
+      const int cs = chunk_sum[k];
+      // tiles whose first column lies in this chunk's columns [run, run + cs) and after rs
+      if (cs > 0) {
+        const int lo_c = max(run == rs ? run + 1 : run, 0), hi_c = run + cs - 1;
+        for (int tt = (lo_c + kCntW - 1) >> 11; lo_c <= hi_c && tt <= (hi_c >> 11); tt++) {
+          const int64_t idx = (int64_t)tt - t_first;
+          if (idx > n - 1) {
+            atomicOr(&notab, 1u);
+            break;
+          }
+          const int kk = (int)(k - b);
+          const int ib = first_base_at(A, runs + (uint64_t)k * kRunCap, roff, kk, len, tt * kCntW - run);
+          tstart[2 * (b + idx)] = kk;
+          tstart[2 * (b + idx) + 1] = ib;
+        }
+      }
+      run += cs;
     }
     if (t == 1023) {  // the row's last slot (chunk sum 0) now holds its end column + 1
       const int last = run - 1;
-      if (len > 0 && (A.col0[r] < 0 || last >= A.n_cols)) atomicMin(&A.minmax[2], (int)r);
+      if (len > 0 && (rs < 0 || last >= A.n_cols)) atomicMin(&A.minmax[2], (int)r);
     }
     __syncthreads();
+    if (t == 0) {
+      int end = rs;
+      for (int w = 0; w < 16; w++) end += wsum[w];
+      ri[2] = rs;
+      ri[3] = end;
+      ri[4] = len;
+      ri[5] = (int)((uint32_t)(e - 1 - b) | (notab ? kNoTable : 0u));
+      ri[6] = (int)(uint32_t)(uint64_t)b;
+      ri[7] = (int)(uint32_t)((uint64_t)b >> 32);
+    }
     if (wv < 2) {
-      const uint64_t roff = A.row_off[r];
       if (hi <= lo) {
         if (lane == 0) ri[wv] = wv == 0 ? 1 : 0;
       } else if (wv == 0) {  // gap-run start of base lo
@@ -280,103 +337,184 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
   }
 }
 
-// K3: counts for one 2048-column tile, with no LDS atomic per base.  16 waves share the rows
-// overlapping the tile (row r -> wave r % 16; the next row's K2 record is prefetched).  For one
-// row a wave fetches, in one round trip, a batch of up to kBatch chunks starting 2 before the
-// chunk its mean column density predicts for the tile's first counted column (checkpoints into
-// one VGPR, gap lists into two, 4 bases per lane per chunk into registers), finds the true first
-// chunk with a ballot over the checkpoints, and walks the chunks: each lane's 4 consecutive
-// bases get their columns from the chunk's checkpoint (K2) plus its gap list (K1): an entry
-// (i, g) moves every base from i on by g columns — the closed form of toMSA,
-// GapAssem.cpp:568-590.  A batch holding a chunk whose list overflowed, or a row not 4-base
-// aligned, takes a general loop that re-reads ofs and scans instead.  Each base writes its bin code (GAlnColumn::addNuc, bin_codes4: in
-// registers, 4 bases at a time) into the wave's 2 KB column strip, one byte per column.  The strip's reset value is
-// the gap code: the columns of the row's counted extent that receive no base are exactly its
-// gap runs (GAlnColumn::addGap); columns outside the extent (K2's ext) are set to "none" in the
-// tiles where the extent starts or ends.  Then each lane reads the 32 columns it owns (two
-// 16-byte LDS reads), adds them to 32 packed register counters (six 10-bit fields in a u64: one
-// shift-add per column) and resets the strip.  The counters move to the workgroup's LDS table
-// every 1023 rows and at the end (packed u64 adds when the layout has at most 1023 rows); the
-// tile is then written coalesced.  mincol / maxcol come from K2.
-constexpr int kCntW = 2048;
-constexpr int kCntWaves = 16;
-constexpr uint32_t kCodeGap = 50u, kCodeNone = 60u;  // bit offsets: A,C,G,T,N,- at 0,10,..,50
-constexpr int kPackRows = 1023;                       // 10-bit fields
-// LDS index of column c in the tile table: conflict-free both for the flush (lanes l own
-// columns 16l + m) and for the read-out (consecutive columns)
-__device__ __forceinline__ int cnt_swz(int c) { return (c & 15) * (kCntW / 16) + (((c >> 4) + 2 * (c & 15)) & (kCntW / 16 - 1)); }
-__device__ __forceinline__ uint32_t seq4(const pw_msa_args& A, uint64_t roff, bool vec, int i, int len) {
-  if (vec && i + 3 < len) return *reinterpret_cast<const uint32_t*>(A.seq + roff + i);
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (i + j < len) s |= (uint32_t)A.seq[roff + i + j] << (8 * j);
-  return s;
-}
-// lane's columns: m < 16 -> 16 * lane + m, m >= 16 -> 1024 + 16 * lane + m - 16
-__device__ __forceinline__ int acc_col(int lane, int m) { return (m < 16 ? 0 : kCntW / 2) + 16 * lane + (m & 15); }
-__device__ __forceinline__ void cnt_flush(uint64_t (&acc)[32], uint32_t* tab, bool packed, int lane) {
-  if (packed) {
-    unsigned long long* pk = reinterpret_cast<unsigned long long*>(tab);
-#pragma unroll
-    for (int m = 0; m < 32; m++) {
-      atomicAdd(&pk[cnt_swz(acc_col(lane, m))], (unsigned long long)(acc[m] & ((1ull << 60) - 1)));
-      acc[m] = 0;
-    }
-  } else {
-#pragma unroll
-    for (int m = 0; m < 32; m++) {
-      const int x = cnt_swz(acc_col(lane, m));
-#pragma unroll
-      for (int f = 0; f < 6; f++) atomicAdd(&tab[f * kCntW + x], (uint32_t)(acc[m] >> (10 * f)) & 1023u);
-      acc[m] = 0;
-    }
-  }
-}
-// the bin codes (10 x GAlnColumn::addNuc/addGap bin, as bin_of) of 4 bases in a dword, in
-// registers: h = (c >> 1) & 7 picks, per byte, the only characters that can have each bin
-// (A/a 0, C/c 1, T/t 2, G/g 3, '*' 5, '-' 6; 4 and 7 none) and v_perm looks up the code, the
-// expected character and its case mask; a byte that is not its h's character is N (40)
-__device__ __forceinline__ uint32_t bin_codes4(uint32_t s4) {
+// K3: counts for one 2048-column tile, no atomic per base.  The 8 waves share the rows
+// overlapping the tile (row r -> wave r % 8).  Lane l owns the tile's columns [32l, 32l + 32).
+// Per row, three dependent loads are pipelined over the wave's rows: the row's slot range, first
+// column and offset (3 rows ahead); its record and tile-start entry (2 rows ahead); then its
+// batch (a row ahead): the checkpoints and runs of the <= 9 chunks that reach the tile (a chunk
+// spans >= 256 columns) and a 2176-byte window of its bases from the tile's first base (buffer
+// loads: past the row's padded end they read 0).  For the row itself:
+//   * the gap-column bitmap of the tile (one dword per lane) starts as the columns outside the
+//     row's [first, end) columns, then every run of the batch ORs its columns in: the columns
+//     left clear are exactly the row's base columns, in base order (the closed form of toMSA,
+//     GapAssem.cpp:568-590);
+//   * the base in lane l's first clear column is first + 32l - (set bits before lane l) — a
+//     wave scan of the popcounts — so for each group of 4 columns the lane reads 4 bytes of the
+//     window from there (two LDS dwords + alignbyte), and v_perm puts a '-' into each set column
+//     and the next base into each clear one;
+//   * bin codes for the 4 characters (GAlnColumn::addNuc / addGap, bin_codes5) shift a 1 into
+//     the column's packed counter: six 5-bit fields A,C,G,T,N,- in a u32 (a "none" code for the
+//     columns outside the row's counted extent lands in bits 30-31 and is discarded);
+//   * the counters move to the workgroup's LDS table every 31 rows of the wave and at the end;
+//     the table is written out coalesced.
+// A row whose tile start is not in the table, or whose batch holds an overflowed chunk, builds
+// the same bitmap from ofs (a wave scan per chunk) and loads its window after that.
+constexpr int kCntWaves = 8;
+constexpr int kWin = 2176;     // bytes of the per-wave base window
+
+constexpr int kFlushRows = 31; // 5-bit packed counters
+constexpr uint32_t kCodeNone = 30u;
+struct TileLds {
+  uint32_t tab[6 * kCntW];                 // [field][swizzled column]
+  uint32_t win[kCntWaves][kWin / 4];       // per-wave base windows
+  uint32_t bmap[kCntWaves][64];            // per-wave gap-column bitmaps
+  uint32_t sel[16];                        // v_perm selectors: 4-bit gap mask -> byte picks
+};
+// LDS slot of column c: rotated by its 32-column block, so the 64 lanes' adds of one counter
+// index (columns 32l + m) fall into distinct banks
+__device__ __forceinline__ int cnt_swz(int c) { return (c & ~31) | ((c + (c >> 5)) & 31); }
+// the bin shifts (5 x GAlnColumn::addNuc/addGap bin, as bin_of) of 4 characters in a dword:
+// h = (c >> 1) & 7 picks, per byte, the only characters that can have each bin (A/a 0, C/c 1,
+// T/t 2, G/g 3, '*' 5, '-' 6; 4 and 7 none) and v_perm looks up the code, the expected
+// character and its case mask; a byte that is not its h's character is N (20)
+__device__ __forceinline__ uint32_t bin_codes5(uint32_t s4) {
   const uint32_t h = (s4 >> 1) & 0x07070707u;
-  const uint32_t code = __builtin_amdgcn_perm(0x28323228u, 0x141E0A00u, h);  // 0 10 30 20 | 40 50 50 40
+  const uint32_t code = __builtin_amdgcn_perm(0x14191914u, 0x0A0F0500u, h);  // 0 5 15 10 | 20 25 25 20
   const uint32_t ex = __builtin_amdgcn_perm(0x002D2A00u, 0x47544341u, h);    // A C T G | - * - -
   const uint32_t mk = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xDFDFDFDFu, h);    // letters: either case
   const uint32_t x = (s4 & mk) ^ ex;                                         // 0 byte: the character
   const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // 0x80: not it
   const uint32_t m = (nz << 1) - (nz >> 7);                                  // 0xFF per such byte
-  return (m & 0x28282828u) | (~m & code);
+  return (m & 0x14141414u) | (~m & code);
 }
-// one chunk: the columns of this lane's 4 bases (relative to the tile) from the chunk's start
-// column and gap list (entries gl(x), x < kGapCap; 0 = unused), or from ofs and a scan
-template <bool kAny, class GL>
-__device__ __forceinline__ void place_chunk(const pw_msa_args& A, uint64_t roff, bool fast, GL gl, uint32_t s4,
-                                            int colr, int cnr, int kb, int len, int ar, int zr, int lane,
-                                            uint8_t* myb) {
-  const int i0 = kb + 4 * lane;
-  int p[4];
-  if (!kAny || fast) {
-    // gb: entries at or before this lane's first base; i1..i3: entries inside its quad (lane qe)
-    int gb = 0, i1 = 0, i2 = 0, i3 = 0;
+// bits of columns [32 lane, 32 lane + 32) that are < lo or >= hi (tile-relative)
+__device__ __forceinline__ uint32_t outside_mask(int lane, int lo, int hi) {
+  const int a = min(max(lo - 32 * lane, 0), 32), b = min(max(hi - 32 * lane, 0), 32);
+  const uint32_t below = a >= 32 ? 0xFFFFFFFFu : ((1u << a) - 1u);
+  const uint32_t above = b >= 32 ? 0u : ~((1u << b) - 1u);
+  return below | above;
+}
+// Per-row values loaded ahead are spread over the lanes of one VGPR (a lane per dword, read
+// back with readlane): vector loads, so their waits are vmcnt waits in issue order, not lgkmcnt
+// waits that every LDS wait of the row body would share.
+//   RowA (3 rows ahead), lanes 0-6: slot_base[r] (2), slot_base[r + 1] (2), row_off (2), col0
+//   RowB (2 rows ahead), lanes 0-7: the row record; lanes 8-9: its tile-start entry
+struct RowA {
+  int64_t sb, sbn;
+  uint64_t roff;
+  int rs;
+};
+__device__ __forceinline__ uint32_t load_a(const pw_msa_args& A, uint32_t r, int lane) {
+  const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(A.col0 + rr);
+  if (lane < 4) p = reinterpret_cast<const uint32_t*>(A.slot_base + rr) + lane;
+  else if (lane < 6) p = reinterpret_cast<const uint32_t*>(A.row_off + rr) + (lane - 4);
+  return *p;
+}
+__device__ __forceinline__ RowA get_a(uint32_t v) {
+  RowA a;
+  a.sb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 0) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 1) << 32);
+  a.sbn = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 2) |
+                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 3) << 32);
+  a.roff = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 4) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 5) << 32;
+  a.rs = __builtin_amdgcn_readlane((int)v, 6);
+  return a;
+}
+__device__ __forceinline__ uint32_t load_b(const pw_msa_args& A, const int32_t* rinfo, const int32_t* tstart, uint32_t r,
+                                           const RowA& a, int c0, int lane) {
+  const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
+  int64_t idx = (int64_t)(c0 >> 11) - (int64_t)(a.rs >> 11);
+  idx = idx < 0 ? 0 : (idx > a.sbn - a.sb - 1 ? a.sbn - a.sb - 1 : idx);
+  const int32_t* p = lane < 8 ? rinfo + kRowInfo * rr + lane : tstart + 2 * (a.sb + idx) + (lane & 1);
+  return (uint32_t)*p;
+}
+__device__ __forceinline__ uint32_t rd(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// the tile's first chunk and first base for this row (kt = -1: not in the table, search)
+__device__ __forceinline__ void tile_start(const RowA& a, uint32_t b, int c0, int& kt, int& ib) {
+  if (c0 <= a.rs) {
+    kt = 0;
+    ib = 0;
+  } else if (rd(b, 5) & kNoTable) {
+    kt = -1;
+    ib = 0;
+  } else {
+    kt = (int)rd(b, 8);
+    ib = (int)rd(b, 9);
+  }
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const pw_msa_args& A, uint64_t roff, int len) {
+  // base 16-byte aligned at or before the row; the range ends at the row's readable end
+  const uint64_t b0 = roff & ~(uint64_t)15;
+  const uint32_t nrec = (uint32_t)(roff - b0) + (((uint32_t)max(len, 0) + 3u) & ~3u);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(A.seq + b0), (short)0, (int)nrec, 0x00020000);
+}
+__device__ __forceinline__ void load_win(const pw_msa_args& A, uint64_t roff, int len, int ib, int lane, v4u& w0, v4u& w1,
+                                         v4u& w2) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(A, roff, len);
+  const uint32_t o = (uint32_t)(((roff + (uint64_t)ib) & ~(uint64_t)15) - (roff & ~(uint64_t)15));
+  w0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16u * (uint32_t)lane, 0, 0);
+  w1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 1024u + 16u * (uint32_t)lane, 0, 0);
+  w2 = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 2048u + 16u * (uint32_t)(lane & 7), 0, 0);
+}
+struct RowC {  // 1 row ahead
+  int ckv;
+  uint32_t gv0, gv1;
+  v4u w0, w1, w2;
+};
+__device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint32_t* runs, const RowA& a,
+                                       uint32_t b, int c0, int lane, RowC& c) {
+  int kt, ib;
+  tile_start(a, b, c0, kt, ib);
+  const int nch = (int)(rd(b, 5) & ~kNoTable);
+  const int len = (int)rd(b, 4);
+  kt = min(max(kt, 0), nch);  // (a row that does not reach the tile reads a stale entry: clamped)
+  const int64_t sb = a.sb;
+  c.ckv = ckpt[sb + min(kt + lane, nch)];
+  c.gv0 = runs[(sb + min(kt + (lane >> 3), nch)) * kRunCap + (lane & 7)];
+  c.gv1 = runs[(sb + min(kt + 8, nch)) * kRunCap + (lane & 7)];
+  load_win(A, a.roff, len, ib, lane, c.w0, c.w1, c.w2);
+}
+__device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(v2u& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void cnt_flush(uint32_t (&acc)[32], LDS uint32_t* tab, int lane) {
 #pragma unroll
-    for (int x = 0; x < kGapCap; x++) {
-      const uint32_t v = gl(x);
-      if (v == 0) break;
-      const int idx = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
-      gb += 4 * lane >= idx ? gg : 0;
-      const int qe = idx >> 2, je = idx & 3;
-      if (je != 0) {
-        const int add = lane == qe ? gg : 0;
-        if (je <= 1) i1 += add;
-        if (je <= 2) i2 += add;
-        i3 += add;
-      }
+  for (int m = 0; m < 32; m++) {
+    const int x = cnt_swz(32 * lane + m);
+#pragma unroll
+    for (int f = 0; f < 6; f++) {
+      atomicAdd((uint32_t*)&tab[f * kCntW + x], (acc[m] >> (5 * f)) & 31u);
     }
-    p[0] = colr + 4 * lane + gb;
-    p[1] = p[0] + 1 + i1;
-    p[2] = p[0] + 2 + i2;
-    p[3] = p[0] + 3 + i3;
-  } else {  // overflowed gap list / unaligned row: ofs and a wave scan
+    acc[m] = 0;
+  }
+}
+// the gap bitmap of a row in this tile from ofs (rows without a tile-start entry, or with an
+// overflowed chunk in the batch): ORs the gap runs of chunks kt.. into bm, returns the first
+// base at or after column c0 (kt = -1: found by a search of the checkpoints first)
+__device__ int slow_bitmap(const pw_msa_args& A, const int32_t* ckpt, int64_t sb, int nch, uint64_t roff, int len, int c0,
+                           int c1, int kt, int lane, LDS uint32_t* bm) {
+  if (kt < 0) {  // last chunk whose checkpoint is <= c0
+    int lo = 0, hi = nch - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (ckpt[sb + mid] <= c0) lo = mid;
+      else hi = mid - 1;
+    }
+    kt = lo;
+  }
+  int ib = INT_MAX;
+  for (int k = kt; k < nch; k++) {
+    int col = ckpt[sb + k];
+    if (col >= c1) break;
+    const int i0 = k * kChunk + 4 * lane;
     int gp[4], tot = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -385,186 +523,167 @@ __device__ __forceinline__ void place_chunk(const pw_msa_args& A, uint64_t roff,
       tot += ok ? 1 + gp[j] : 0;
     }
     const int incl = wave_scan_incl(tot);
-    int run = colr + incl - tot;
+    int run = col + incl - tot;
+    int first = INT_MAX;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      run += (i0 + j < len) ? 1 + gp[j] : 0;
-      p[j] = run - 1;
+      if (i0 + j >= len) break;
+      const int g0 = run, bc = run + gp[j];  // gap run [g0, bc), base column bc
+      for (int x = max(g0, c0); x < bc && x < c1; x++) atomicOr((uint32_t*)&bm[(x - c0) >> 5], 1u << ((x - c0) & 31));
+      if (bc >= c0 && first == INT_MAX) first = i0 + j;
+      run = bc + 1;
     }
-  }
-  const bool all = kb + kChunk <= len && colr >= ar && cnr - 1 <= zr;  // (wave-uniform)
-  const uint32_t code4 = bin_codes4(s4);
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    if (all || (i0 + j < len && p[j] >= ar && p[j] <= zr)) myb[p[j]] = (uint8_t)(code4 >> (8 * j));
+    for (int d = 32; d >= 1; d >>= 1) first = min(first, __shfl_xor(first, d, 64));
+    ib = min(ib, first);
   }
+  return ib == INT_MAX ? len : ib;
 }
-constexpr int kBatch = 14;  // chunks fetched per round trip (a 2048-column tile spans ~8-9)
-__global__ __launch_bounds__(64 * kCntWaves) void tile_counts(const pw_msa_args A, const int32_t* __restrict__ ckpt,
-                                                              const uint32_t* __restrict__ glist,
-                                                              const int32_t* __restrict__ rinfo) {
-  __shared__ uint32_t strip[kCntWaves * kCntW / 4];
-  __shared__ uint32_t tab[6 * kCntW];  // u32 counters [field][swz col], or packed u64 [swz col]
+__global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_args A, const int32_t* __restrict__ ckpt,
+                                                              const uint32_t* __restrict__ runs,
+                                                              const int32_t* __restrict__ rinfo,
+                                                              const int32_t* __restrict__ tstart) {
+  __shared__ __attribute__((aligned(16))) TileLds L;
+  LDS TileLds* lp = (LDS TileLds*)&L;
   const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * kCntW;
   const int c1 = min(c0 + kCntW, A.n_cols);
-  const bool packed = A.n_rows <= (uint32_t)kPackRows;
-  for (int i = tid; i < 6 * kCntW; i += 64 * kCntWaves) tab[i] = 0;
-  for (int i = tid; i < kCntWaves * kCntW / 4; i += 64 * kCntWaves) strip[i] = kCodeGap * 0x01010101u;
+  for (int i = tid; i < 6 * kCntW; i += 64 * kCntWaves) lp->tab[i] = 0;
+  if (tid < 16) {  // byte p: a gap column -> 4 (a '-' of src0), else the next source byte
+    uint32_t s = 0;
+    int k = 0;
+    for (int p = 0; p < 4; p++) {
+      s |= (uint32_t)(((tid >> p) & 1) ? 4 : k) << (8 * p);
+      k += ((tid >> p) & 1) ? 0 : 1;
+    }
+    lp->sel[tid] = s;
+  }
   __syncthreads();
-  uint32_t* my = strip + wv * (kCntW / 4);
-  uint8_t* myb = reinterpret_cast<uint8_t*>(my);  // myb[c - c0]: column c
-  uint64_t acc[32];
+  LDS uint32_t* win = lp->win[wv];
+  LDS uint32_t* bm = lp->bmap[wv];
+  LDS uint32_t* tab = lp->tab;
+  uint32_t acc[32];
 #pragma unroll
   for (int m = 0; m < 32; m++) acc[m] = 0;
   int nrow = 0;
-  const uint4* ri4 = reinterpret_cast<const uint4*>(rinfo);
-  uint4 nx0 = make_uint4(0, 0, 0, 0), nx1 = nx0;  // the next row's record (prefetched)
-  uint64_t nroff = 0;
-  if ((uint32_t)wv < A.n_rows) {
-    nx0 = ri4[2 * wv];
-    nx1 = ri4[2 * wv + 1];
-    nroff = A.row_off[wv];
-  }
-  for (uint32_t r = wv;; r += kCntWaves) {
-    const bool end = r >= A.n_rows;
-    if (end || nrow == kPackRows) {  // the counters' one flush site: every kPackRows rows, and the end
-      if (nrow) cnt_flush(acc, tab, packed, lane);
-      nrow = 0;
-      if (end) break;
-    }
-    const int elo = __builtin_amdgcn_readfirstlane((int)nx0.x), ehi = __builtin_amdgcn_readfirstlane((int)nx0.y);
-    const int rs = __builtin_amdgcn_readfirstlane((int)nx0.z), re = __builtin_amdgcn_readfirstlane((int)nx0.w);
-    const int len = __builtin_amdgcn_readfirstlane((int)nx1.x), nch = __builtin_amdgcn_readfirstlane((int)nx1.y);
-    const int64_t b = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nx1.z) |
-                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)nx1.w) << 32);
-    const uint64_t roff = nroff;
-    if (r + kCntWaves < A.n_rows) {
-      nx0 = ri4[2 * (r + kCntWaves)];
-      nx1 = ri4[2 * (r + kCntWaves) + 1];
-      nroff = A.row_off[r + kCntWaves];
-    }
-    const int a = max(elo, c0), z = min(ehi, c1 - 1);  // counted columns of this row here
-    if (a > z) continue;
-    const int ar = a - c0, zr = z - c0;
-    if (a > c0 || z < c1 - 1) {  // the extent starts or ends in this tile
-      for (int x = lane; x < kCntW / 4; x += 64) {
-        uint32_t w = 0;
+  const uint32_t W = kCntWaves;
+  uint32_t r = wv;
+  if (r < A.n_rows) {
+    // prologue: rows r (A, B, C), r + W (A, B), r + 2W (A)
+    uint32_t av1 = load_a(A, r, lane), av2 = load_a(A, r + W, lane), av3 = load_a(A, r + 2 * W, lane);
+    RowA a1 = get_a(av1);
+    uint32_t bv1 = load_b(A, rinfo, tstart, r, a1, c0, lane);
+    RowA a2 = get_a(av2);
+    uint32_t bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane);
+    RowC cc;
+    load_c(A, ckpt, runs, a1, bv1, c0, lane, cc);
+    for (;; r += W) {
+      // the next rows' loads (each waits only for what the previous iteration issued), then this
+      // row, whose batch was issued a row earlier
+      RowC cn;
+      load_c(A, ckpt, runs, a2, bv2, c0, lane, cn);
+      const RowA a3 = get_a(av3);
+      const uint32_t bv3 = load_b(A, rinfo, tstart, r + 2 * W, a3, c0, lane);
+      const uint32_t av4 = load_a(A, r + 3 * W, lane);
+      pin(cc.w0);
+      pin(cc.w1);
+      pin(cc.w2);
+      pin(cc.ckv);
+      pin(cc.gv0);
+      pin(cc.gv1);
+      const int elo = (int)rd(bv1, 0), ehi = (int)rd(bv1, 1);
+      const int a = max(elo, c0), z = min(ehi, c1 - 1);  // counted columns of this row here
+      if (a <= z) {
+        nrow++;
+        const int rs = (int)rd(bv1, 2), re = (int)rd(bv1, 3);
+        const int len = (int)rd(bv1, 4);
+        const int nch = (int)(rd(bv1, 5) & ~kNoTable);
+        const int64_t sb = a1.sb;
+        const uint64_t roff = a1.roff;
+        int kt, ib;
+        tile_start(a1, bv1, c0, kt, ib);
+        // gap bitmap: the columns outside [rs, re), then the runs of the batch's chunks
+        bm[lane] = outside_mask(lane, rs - c0, re - c0);
+        const bool cv0 = kt >= 0 && kt + (lane >> 3) < nch, cv1 = kt >= 0 && kt + 8 < nch && lane < 8;
+        const bool ovf = kt < 0 || __ballot((lane & 7) == 0 && ((cv0 && cc.gv0 == kRunOverflow) ||
+                                                                (cv1 && cc.gv1 == kRunOverflow))) != 0;
+        wave_sync();
+        if (!ovf) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int c = c0 + 4 * x + q;
-          w |= ((c < a || c > z) ? kCodeNone : kCodeGap) << (8 * q);
-        }
-        my[x] = w;
-      }
-    }
-    const bool vec = (roff & 3) == 0;
-    // first chunk reaching column a (the last with start column <= a), guessed from the row's mean
-    // column density; a batch starts 2 chunks before the guess
-    const double dens = (double)nch / (double)(re - rs);  // chunks per column
-    int ks = a > rs ? (int)((double)(a - rs) * dens) - 2 : 0;
-    ks = min(max(ks, 0), nch - 1);
-    bool exact = false;  // ks is the first chunk
-    for (;;) {
-      const int nb = min(min(kBatch, (int)((double)(z - a + 1) * dens) + (exact ? 2 : 4)), nch - ks);
-      // one round trip: checkpoints [ks, ks + nb], gap lists and seq of chunks [ks, ks + nb)
-      const int ckv = lane <= nb ? ckpt[b + ks + lane] : INT_MAX;
-      const uint32_t* glb = glist + (uint64_t)(b + ks) * kGapCap;
-      const uint32_t gv0 = lane < kGapCap * nb ? glb[lane] : 0u;
-      const uint32_t gv1 = 64 + lane < kGapCap * nb ? glb[64 + lane] : 0u;
-      uint32_t sq[kBatch];
-#pragma unroll
-      for (int j = 0; j < kBatch; j++) sq[j] = j < nb ? seq4(A, roff, vec, (ks + j) * kChunk + 4 * lane, len) : 0u;
-      int j0 = 0;
-      if (!exact) {
-        const uint64_t m = __ballot(lane < nb && ckv <= a);
-        if (m == 0 || (m >> (nb - 1)) != 0) {
-          // guess off by more than the margin (or the batch ends before a): step from the guess
-          int k = ks;
-          while (k > 0 && ckpt[b + k] > a) k--;
-          while (k + 1 < nch && ckpt[b + k + 1] <= a) k++;
-          if (k + 1 < nch || ckpt[b + k] <= a) {
-            ks = k;
-            exact = true;
-            continue;
+          for (int h = 0; h < 2; h++) {
+            const uint32_t v = h == 0 ? (cv0 ? cc.gv0 : 0u) : (cv1 ? cc.gv1 : 0u);
+            const int ck = h == 0 ? __shfl(cc.ckv, lane >> 3, 64) : __builtin_amdgcn_readlane(cc.ckv, 8);
+            if (v != 0u) {
+              const int s = max(ck + (int)(v >> 16) - c0, 0), e = min(ck + (int)(v >> 16) + (int)(v & 0xFFFFu) - c0, kCntW);
+              for (int x = s; x < e; x = (x | 31) + 1) {
+                const int xe = min(e, (x | 31) + 1);
+                const uint32_t m = (xe - x >= 32 ? 0xFFFFFFFFu : ((1u << (xe - x)) - 1u)) << (x & 31);
+                atomicOr((uint32_t*)&bm[x >> 5], m);
+              }
+            }
           }
+          // the window (loaded a row ahead)
+          LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+          w4[lane] = cc.w0;
+          w4[64 + lane] = cc.w1;
+          if (lane < 8) w4[128 + lane] = cc.w2;
+        } else {
+          ib = slow_bitmap(A, ckpt, sb, nch, roff, len, c0, c1, kt, lane, bm);
+          v4u w0, w1, w2;
+          load_win(A, roff, len, ib, lane, w0, w1, w2);
+          LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+          w4[lane] = w0;
+          w4[64 + lane] = w1;
+          if (lane < 8) w4[128 + lane] = w2;
         }
-        j0 = 63 - __builtin_clzll(m);
-      }
-      bool done = false;
-      // a chunk whose gap list overflowed, or an unaligned row: the whole batch takes the general
-      // loop (per chunk: gap list or ofs), else the unrolled gap-list loop over the registers
-      const bool slow = !vec || __ballot((lane & 7) == 0 && (gv0 == kGapOverflow || gv1 == kGapOverflow)) != 0;
-      if (!slow) {
+        wave_sync();
+        const uint32_t bmv = bm[lane];
+        const int pc = __popc(bmv);
+        const int excl = wave_scan_incl(pc) - pc;
+        // byte offset in the window of the base in this lane's first clear column
+        const int so = (int)((uint32_t)(roff + (uint64_t)ib) & 15u) + 32 * lane - excl;
+        const bool edge = a > c0 || z < c1 - 1;
+        const uint32_t om = edge ? outside_mask(lane, a - c0, z - c0 + 1) : 0u;
+        const LDS uint8_t* wb = reinterpret_cast<const LDS uint8_t*>(win);
 #pragma unroll
-        for (int j = 0; j < kBatch; j++) {
-          if (j < j0) continue;
-          if (j >= nb) break;
-          const int colr = __builtin_amdgcn_readlane(ckv, j) - c0;
-          if (colr > zr) {
-            done = true;
-            break;
+        for (int q = 0; q < 8; q++) {
+          const uint32_t nb = (bmv >> (4 * q)) & 15u;
+          const int src = so + 4 * q - (q == 0 ? 0 : __popc(bmv & ((1u << (4 * q)) - 1u)));
+          const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
+          const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
+          const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);
+          uint32_t codes = bin_codes5(e4);
+          if (edge) {
+            const uint32_t on = (om >> (4 * q)) & 15u;
+            const uint32_t bmask = ((on * 0x00204081u) & 0x01010101u) * 0xFFu;  // 4 bits -> 4 bytes
+            codes = (codes & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
           }
-          const int cnr = __builtin_amdgcn_readlane(ckv, j + 1) - c0;
-          auto gl = [&](int x) -> uint32_t {
-            const int q = kGapCap * j + x;
-            return (uint32_t)__builtin_amdgcn_readlane((int)(q < 64 ? gv0 : gv1), q & 63);
-          };
-          place_chunk<false>(A, roff, true, gl, sq[j], colr, cnr, (ks + j) * kChunk, len, ar, zr, lane, myb);
+#pragma unroll
+          for (int j = 0; j < 4; j++) acc[4 * q + j] += 1u << ((codes >> (8 * j)) & 31u);
         }
-      } else {
-#pragma unroll 1
-        for (int j = j0; j < nb; j++) {
-          const int colr = __builtin_amdgcn_readlane(ckv, j) - c0;
-          if (colr > zr) {
-            done = true;
-            break;
-          }
-          const int cnr = __builtin_amdgcn_readlane(ckv, j + 1) - c0;
-          auto gl = [&](int x) -> uint32_t {
-            const int q = kGapCap * j + x;
-            const int lo = __builtin_amdgcn_readlane((int)gv0, q & 63), hi = __builtin_amdgcn_readlane((int)gv1, q & 63);
-            return (uint32_t)(q < 64 ? lo : hi);
-          };
-          const bool fast = vec && gl(0) != kGapOverflow;
-          const uint32_t s4 = seq4(A, roff, vec, (ks + j) * kChunk + 4 * lane, len);
-          place_chunk<true>(A, roff, fast, gl, s4, colr, cnr, (ks + j) * kChunk, len, ar, zr, lane, myb);
-        }
+        wave_sync();
       }
-      ks += nb;
-      if (done || ks >= nch || __builtin_amdgcn_readlane(ckv, nb) > z) break;
-      exact = true;  // the next batch starts right after this one
+      a1 = a2;
+      a2 = a3;
+      av3 = av4;
+      bv1 = bv2;
+      bv2 = bv3;
+      cc = cn;
+      const bool last = r + W >= A.n_rows;
+      if (last || nrow == kFlushRows) {  // (the counters' one flush site)
+        cnt_flush(acc, tab, lane);
+        nrow = 0;
+      }
+      if (last) break;
     }
-    // the strip is read back by other lanes of this wave (LDS is in order within a wave)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint4* w4 = reinterpret_cast<uint4*>(my);
-    const uint4 wa = w4[lane], wb = w4[64 + lane];
-    const uint32_t wd[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-    for (int m = 0; m < 32; m++) acc[m] += 1ull << ((wd[m >> 2] >> (8 * (m & 3))) & 0xFFu);
-    const uint32_t g4 = kCodeGap * 0x01010101u;
-    w4[lane] = make_uint4(g4, g4, g4, g4);
-    w4[64 + lane] = make_uint4(g4, g4, g4, g4);
-    nrow++;
   }
   __syncthreads();
-  // the tile's counters: [col][6] rows in memory, one column per thread at a time
-  for (int c = tid; c < c1 - c0; c += 64 * kCntWaves) {
-    const int x = cnt_swz(c);
-    uint32_t v[6];
-    if (packed) {
-      const uint64_t pv = reinterpret_cast<const unsigned long long*>(tab)[x];
-#pragma unroll
-      for (int f = 0; f < 6; f++) v[f] = (uint32_t)(pv >> (10 * f)) & 1023u;
-    } else {
-#pragma unroll
-      for (int f = 0; f < 6; f++) v[f] = tab[f * kCntW + x];
-    }
-    int32_t* dst = A.counts + ((int64_t)c0 + c) * 6;
-#pragma unroll
-    for (int f = 0; f < 6; f++) dst[f] = (int32_t)v[f];
+  // the tile's counters: [col][6] rows in memory, coalesced
+  const int cw = c1 - c0;
+  int32_t* dst = A.counts + (int64_t)c0 * 6;
+  for (int i = tid; i < cw * 6; i += 64 * kCntWaves) {
+    const int c = i / 6, f = i - 6 * c;
+    dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];
   }
 }
 
@@ -744,7 +863,9 @@ __global__ __launch_bounds__(64) void row_finish(const pw_msa_args A, pw_msa_ref
 }
 
 // scratch word of the row records (16-byte aligned: K3 reads them as uint4)
-inline uint64_t rinfo_word(uint64_t n_slots) { return ((3 + (uint64_t)kGapCap) * n_slots + 3) & ~(uint64_t)3; }
+// scratch words: chunk sums | checkpoints | slot -> row | runs (kRunCap per slot) | tile starts (2 per slot) | row records
+inline uint64_t tstart_word(uint64_t n_slots) { return (3 + (uint64_t)kRunCap) * n_slots; }
+inline uint64_t rinfo_word(uint64_t n_slots) { return (tstart_word(n_slots) + 2 * n_slots + 3) & ~(uint64_t)3; }
 
 }  // namespace pw
 
@@ -771,20 +892,22 @@ static bool msa_args_ok(const pw_msa_args* a) {
 extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   if (!msa_args_ok(a)) return PW_E_ARG;
   hipStream_t s = (hipStream_t)stream;
-  // scratch: chunk sums | checkpoints | slot -> row | gap lists (kGapCap per slot) | row extents
+  // scratch: chunk sums | checkpoints | slot -> row | gap runs (kRunCap per slot) | tile starts |
+  // row records
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
   int32_t* slot_row = a->scratch + 2 * a->n_slots;
-  uint32_t* glist = reinterpret_cast<uint32_t*>(a->scratch + 3 * a->n_slots);
+  uint32_t* runs = reinterpret_cast<uint32_t*>(a->scratch + 3 * a->n_slots);
+  int32_t* tstart = a->scratch + pw::tstart_word(a->n_slots);
   int32_t* rinfo = a->scratch + pw::rinfo_word(a->n_slots);
   hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row);
-  const uint64_t nb1 = ((a->n_slots + 7) / 8 + 3) / 4;  // 8 slots per wave, 4 waves per workgroup
-  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 4096 ? nb1 : 4096)), dim3(256), 0, s, *a,
-                     chunk_sum, slot_row, glist);
+  const uint64_t nb1 = ((a->n_slots + 3) / 4 + 3) / 4;  // 4 slots per wave, 4 waves per workgroup
+  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 8192 ? nb1 : 8192)), dim3(256), 0, s, *a,
+                     chunk_sum, slot_row, runs);
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(1024), 0, s, *a, chunk_sum, ckpt,
-                     rinfo);
+                     rinfo, runs, tstart);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kCntW - 1) / pw::kCntW);
-  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kCntWaves), 0, s, *a, ckpt, glist, rinfo);
+  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kCntWaves), 0, s, *a, ckpt, runs, rinfo, tstart);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 

@@ -10,6 +10,5 @@ tail -3 gpurun_out/pytest_ga_$TAG.log
 timeout -k 10 300 python3 bench.py --config 5 > gpurun_out/bench5_$TAG.json 2> gpurun_out/bench5_$TAG.err || { echo "bench5 failed: $?"; tail -20 gpurun_out/bench5_$TAG.err; exit 1; }
 cat gpurun_out/bench5_$TAG.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_c5/trace -o run --output-format csv -- python3 bench.py --config 5 --steps 10 --warmup 2 --no-parity --no-cpu-baseline > gpurun_out/prof_${TAG}_c5/bench_trace.json 2> gpurun_out/prof_${TAG}_c5.err || { echo "trace5 failed"; exit 1; }
-f=$(find gpurun_out/prof_${TAG}_c5/trace -name "*kernel_stats.csv" | head -1)
-grep "pw::" "$f" | awk -F, '{printf "   %-24s %8.1f us\n", substr($1,2,24), $4/1000}'
+python3 tools/kstats.py gpurun_out/prof_${TAG}_c5/trace/run_kernel_stats.csv
 echo ga done
