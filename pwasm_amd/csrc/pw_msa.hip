@@ -49,6 +49,8 @@
 #include <limits.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pwasm_amd.h"
 #include "pw_wave.h"
 
@@ -80,12 +82,23 @@ __device__ __forceinline__ int64_t vary(int64_t v) {
   return v;
 }
 
-// K0: the row of every slot (slot_row), one workgroup per row, coalesced
-__global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row) {
+// K0: the row of every slot (slot_row) and K1's chunk descriptor (sdesc: the chunk's first ofs
+// element | its base count << 48 | 16-byte aligned << 63), one workgroup per row, coalesced
+constexpr uint64_t kDescVec = 1ull << 63;
+__global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row, uint64_t* sdesc) {
   if (blockIdx.x == 0 && threadIdx.x < 4)  // minmax sentinels (no host copy on the stream)
     A.minmax[threadIdx.x] = threadIdx.x == 1 ? -1 : INT_MAX;
-  for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x)
-    for (int64_t k = A.slot_base[r] + threadIdx.x; k < A.slot_base[r + 1]; k += 256) slot_row[k] = (int32_t)r;
+  for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
+    const int64_t b = A.slot_base[r], e = A.slot_base[r + 1];
+    const uint64_t roff = A.row_off[r];
+    const int len = A.row_len[r];
+    for (int64_t k = b + threadIdx.x; k < e; k += 256) {
+      slot_row[k] = (int32_t)r;
+      const int i0 = (int)(k - b) * kChunk;
+      const uint64_t nv = (uint64_t)min(max(len - i0, 0), kChunk);
+      sdesc[k] = ((roff + (uint64_t)i0) & ((1ull << 48) - 1)) | nv << 48 | ((roff & 7) == 0 ? kDescVec : 0ull);
+    }
+  }
 }
 
 // K1: per 256-base chunk, sum of (1 + max(ofs, 0)) and its gap runs.  A run is the gap before a
@@ -95,27 +108,27 @@ __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* s
 // (K2 / K3 then read that chunk's ofs).  A wavefront takes 4 consecutive slots at a time, 16 lanes
 // per slot, 16 bases per lane (two 16-byte loads when the row starts 8-base aligned); the next
 // group's loads are issued before this group is reduced.
-constexpr int kRunCap = 8;
+constexpr int kRunCap = 16;  // (one per lane of the chunk's 16; > 16 runs in 256 bases: ~1e-7 at 1 % gaps)
 constexpr uint32_t kRunOverflow = 0xFFFFFFFFu;
+// K1's inputs per lane: the slot's descriptor two groups ahead, its 16 gaps one group ahead
 struct SumPre {
   v4u q0, q1;
-  uint64_t roff;
-  int len, i0;
-  bool vec, live;
+  uint64_t off;  // first ofs element of this lane's 16
+  int nv;        // bases of this lane (0..16)
+  bool vec;
 };
-__device__ __forceinline__ void sums_load(const pw_msa_args& A, const int32_t* slot_row, uint64_t g, int lane, SumPre& p) {
+__device__ __forceinline__ uint64_t sums_desc(const pw_msa_args& A, const uint64_t* sdesc, uint64_t g, int lane) {
   const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
-  p.live = c < A.n_slots;
-  const uint64_t cc = p.live ? c : A.n_slots - 1;
-  const uint32_t r = (uint32_t)slot_row[cc];
-  const int64_t k = (int64_t)cc - A.slot_base[r];
-  p.len = A.row_len[r];
-  p.roff = A.row_off[r];
-  p.i0 = (int)(k * kChunk) + 16 * (lane & 15);
-  p.vec = (p.roff & 7) == 0 && p.i0 + 16 <= p.len;
+  return c < A.n_slots ? sdesc[c] : sdesc[A.n_slots - 1] & ((1ull << 48) - 1);  // (past the end: no bases)
+}
+__device__ __forceinline__ void sums_load(const pw_msa_args& A, uint64_t d, int lane, SumPre& p) {
+  const int sub = lane & 15;
+  p.off = (d & ((1ull << 48) - 1)) + 16ull * (uint64_t)sub;
+  p.nv = min(max((int)((d >> 48) & 0x1FFu) - 16 * sub, 0), 16);
+  p.vec = (d & kDescVec) && p.nv == 16;
   // (unconditional loads: a row tail or unaligned row reads the scratch instead and takes the
   // element path when consumed)
-  const v4u* src = p.vec ? reinterpret_cast<const v4u*>(A.ofs + p.roff + p.i0) : reinterpret_cast<const v4u*>(A.scratch);
+  const v4u* src = p.vec ? reinterpret_cast<const v4u*>(A.ofs + p.off) : reinterpret_cast<const v4u*>(A.scratch);
   p.q0 = src[0];
   p.q1 = src[1];
 }
@@ -126,18 +139,21 @@ __device__ __forceinline__ uint32_t row16_scan_incl(uint32_t v) {  // inclusive 
   v += dpp_or_zero<0x118>(v);
   return v;
 }
-__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const int32_t* slot_row,
+__global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const uint64_t* sdesc,
                                                       uint32_t* runs) {
   const int lane = threadIdx.x & 63, sub = lane & 15;
   const uint64_t ng = (A.n_slots + 3) / 4;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= ng) return;
+  uint64_t dn = sums_desc(A, sdesc, g + nw, lane);
   SumPre cur;
-  sums_load(A, slot_row, g, lane, cur);
+  sums_load(A, sums_desc(A, sdesc, g, lane), lane, cur);
   for (; g < ng; g += nw) {
     SumPre nxt;
-    sums_load(A, slot_row, g + nw < ng ? g + nw : g, lane, nxt);
+    asm volatile("" : "+v"(dn));
+    sums_load(A, dn, lane, nxt);
+    dn = sums_desc(A, sdesc, g + 2 * nw, lane);
     asm volatile("" : "+v"(cur.q0), "+v"(cur.q1));
     uint32_t w[8];  // 16 int16 gaps, two per dword
     if (cur.vec) {
@@ -146,10 +162,9 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
     } else {  // row tail / unaligned row
 #pragma unroll
       for (int d = 0; d < 8; d++) w[d] = 0;
-      for (int i = 0; i < 16 && cur.i0 + i < cur.len; i++)
-        w[i >> 1] |= (uint32_t)(uint16_t)A.ofs[cur.roff + cur.i0 + i] << (16 * (i & 1));
+      for (int i = 0; i < cur.nv; i++) w[i >> 1] |= (uint32_t)(uint16_t)A.ofs[cur.off + i] << (16 * (i & 1));
     }
-    const int nv = cur.live ? min(max(cur.len - cur.i0, 0), 16) : 0;  // bases of this lane
+    const int nv = cur.nv;
     int s = 0;
     uint32_t pm = 0;
 #pragma unroll
@@ -158,18 +173,17 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
       s += lo + hi;
       pm |= (uint32_t)min(lo, 1) << (2 * d) | (uint32_t)min(hi, 1) << (2 * d + 1);
     }
-    if (!cur.live) s = 0, pm = 0;
     const int n = __popc(pm);
     const uint32_t is = row16_scan_incl((uint32_t)s), in = row16_scan_incl((uint32_t)n), iv = row16_scan_incl((uint32_t)nv);
     const int ts = __shfl((int)is, lane | 15, 64), tn = __shfl((int)in, lane | 15, 64), tv = __shfl((int)iv, lane | 15, 64);
     const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
-    if (cur.live) {
+    if (c < A.n_slots) {
       if (sub == 0) chunk_sum[c] = tv + ts;
       uint32_t* rl = runs + c * kRunCap;
       if (tn > kRunCap || tv + ts > 0xFFFF) {
         if (sub == 0) rl[0] = kRunOverflow;
       } else {
-        if (sub < kRunCap && sub >= tn) rl[sub] = 0u;
+        if (sub >= tn) rl[sub] = 0u;
         int slot = (int)in - n;
         int col = 16 * sub + ((int)is - s);  // column offset of this lane's first base's gap run
         int prev = 0;                        // base index (in the lane) the column offset refers to
@@ -204,51 +218,92 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
 // {chunk holding c0, first base at or after c0} (the row has room for it in its slots unless its
 // gaps inflate it more than 8-fold: then the row is flagged and K3 searches).
 constexpr int kCntW = 2048;  // K3 tile width
-__device__ __forceinline__ int chunk_cols_upto(const pw_msa_args& A, uint64_t roff, int i0, int i_end, int lane) {
-  // sum over bases [i0, i_end) of 1 + max(ofs, 0) (i_end - i0 <= kChunk), wave-uniform result
-  int s = 0;
+// A chunk's runs, all kRunCap entries loaded at once (one round trip, no dependent loads)
+struct Runs {
+  uint32_t v[kRunCap];
+};
+__device__ __forceinline__ Runs load_runs(const uint32_t* rl) {  // (rl 16-byte aligned)
+  Runs R;
+  const v4u* p = reinterpret_cast<const v4u*>(rl);
 #pragma unroll
-  for (int j = 0; j < kChunk / 64; j++) {
-    const int i = i0 + j * 64 + lane;
-    if (i < i_end) s += 1 + max((int)A.ofs[roff + i], 0);
+  for (int e = 0; e < kRunCap / 4; e++) {
+    const v4u v = p[e];
+    R.v[4 * e] = v.x, R.v[4 * e + 1] = v.y, R.v[4 * e + 2] = v.z, R.v[4 * e + 3] = v.w;
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
-  return s;
+  return R;
 }
 // first base of chunk k (row-relative index) whose column is >= column x of the chunk (x from its
 // checkpoint, 0 <= x < its column span): from the runs, or (overflowed chunk) by walking its ofs
-__device__ __forceinline__ int first_base_at(const pw_msa_args& A, const uint32_t* rl, uint64_t roff, int k, int len,
-                                             int x) {
-  if (rl[0] != kRunOverflow) {
-    int G = 0;
-#pragma unroll 1
+__device__ __forceinline__ int first_base_at(const pw_msa_args& A, const Runs& R, uint64_t roff, int k, int len, int x) {
+  if (R.v[0] != kRunOverflow) {
+    int G = 0, ib = -1;
+#pragma unroll
     for (int e = 0; e < kRunCap; e++) {
-      const uint32_t v = rl[e];
-      if (v == 0) break;
+      const uint32_t v = R.v[e];
       const int co = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
-      if (x < co) break;
-      if (x < co + gg) return k * kChunk + co - G;  // inside the run: the base after it
-      G += gg;
+      if (ib < 0 && v != 0 && x >= co) {
+        if (x < co + gg) ib = co - G;  // inside the run: the base after it
+        else G += gg;
+      } else if (ib < 0) {
+        ib = x - G;  // (a run at or after x, or none left: x is a base column)
+      }
     }
-    return k * kChunk + x - G;
+    return k * kChunk + (ib < 0 ? x - G : ib);
   }
   int col = 0;
   const int i1 = min(k * kChunk + kChunk, len);
 #pragma unroll 1
-  for (int i = k * kChunk; i < i1; i++) {
-    col += max((int)A.ofs[roff + i], 0);
-    if (col >= x) return i;
-    col++;
+  for (int i8 = k * kChunk; i8 < i1; i8 += 16) {  // (16 loads issued together per step)
+    int16_t g[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) g[j] = A.ofs[roff + (uint64_t)min(i8 + j, i1 - 1)];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      if (i8 + j >= i1) break;
+      col += max((int)g[j], 0);
+      if (col >= x) return i8 + j;
+      col++;
+    }
   }
   return i1;
 }
+// column offset (from the chunk's checkpoint) of base i of chunk k (i chunk-relative): its gap
+// run's first column (run_start) or the base's own column
+__device__ __forceinline__ int base_col(const pw_msa_args& A, const Runs& R, uint64_t roff, int k, int i, bool run_start) {
+  if (R.v[0] != kRunOverflow) {
+    int G = 0;
+    bool done = false;
+#pragma unroll
+    for (int e = 0; e < kRunCap; e++) {
+      const uint32_t v = R.v[e];
+      const int co = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
+      const int idx = co - G;  // the base this run precedes
+      if (!done && v != 0 && (run_start ? idx < i : idx <= i)) G += gg;
+      else done = true;
+    }
+    return i + G;
+  }
+  int col = 0;
+  const uint64_t o = roff + (uint64_t)k * kChunk;
+#pragma unroll 1
+  for (int b8 = 0; b8 <= i; b8 += 16) {  // (16 loads issued together per step; reads stay inside the chunk)
+    int16_t g[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) g[j] = A.ofs[o + (uint64_t)min(b8 + j, i)];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      if (b8 + j < i) col += 1 + max((int)g[j], 0);
+      else if (b8 + j == i && !run_start) col += max((int)g[j], 0);
+    }
+  }
+  return col;
+}
 constexpr int kRowInfo = 8;  // int32 words per row record
 constexpr uint32_t kNoTable = 0x80000000u;
+constexpr int kPfxUnroll = 4;  // chunk sums a thread keeps in registers (rows of <= 4096 chunks)
 __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const int32_t* chunk_sum, int32_t* ckpt,
                                                    int32_t* rinfo, const uint32_t* runs, int32_t* tstart) {
   __shared__ int wsum[16];
-  __shared__ int ck_s[2];
   __shared__ uint32_t notab;
   const int64_t* chunk_base = A.slot_base;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -263,50 +318,70 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
     const int rs = A.col0[r];
     const int t_first = rs >> 11;  // floor(rs / kCntW)
     if (t == 0) notab = 0;
-    int mine = 0;
-    for (int64_t k = k0; k < k1; k++) mine += chunk_sum[k];
-    int incl = mine;
+    // the thread's chunk sums: the first kPfxUnroll kept in registers (loads issued together)
+    int cs[kPfxUnroll];
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += v;
-    }
+    for (int u = 0; u < kPfxUnroll; u++) cs[u] = k0 + u < k1 ? chunk_sum[k0 + u] : 0;
+    int mine = 0;
+#pragma unroll
+    for (int u = 0; u < kPfxUnroll; u++) mine += cs[u];
+    for (int64_t k = k0 + kPfxUnroll; k < k1; k++) mine += chunk_sum[k];
+    const int incl = wave_scan_incl(mine);
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int base = rs;
-    for (int w = 0; w < wv; w++) base += wsum[w];
+    int base = rs, end = rs;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+      const int v = wsum[w];
+      base += w < wv ? v : 0;
+      end += v;
+    }
     int run = base + incl - mine;
     int32_t* ri = rinfo + (int64_t)kRowInfo * r;
-    for (int64_t k = k0; k < k1; k++) {
-      if (k == klo) ck_s[0] = run;
-      if (k == khi) ck_s[1] = run;
+    auto chunk = [&](int64_t k, int c) {
       ckpt[k] = run;
-      const int cs = chunk_sum[k];
-      // tiles whose first column lies in this chunk's columns [run, run + cs) and after rs
-      if (cs > 0) {
-        const int lo_c = max(run == rs ? run + 1 : run, 0), hi_c = run + cs - 1;
-        for (int tt = (lo_c + kCntW - 1) >> 11; lo_c <= hi_c && tt <= (hi_c >> 11); tt++) {
-          const int64_t idx = (int64_t)tt - t_first;
-          if (idx > n - 1) {
-            atomicOr(&notab, 1u);
-            break;
+      const int kk = (int)(k - b);
+      // tiles whose first column lies in this chunk's columns [run, run + c) and after rs, and the
+      // counted extent's ends; both need the chunk's runs
+      const int lo_c = max(run == rs ? run + 1 : run, 0), hi_c = run + c - 1;
+      const bool tiles = c > 0 && lo_c <= hi_c && ((lo_c + kCntW - 1) >> 11) <= (hi_c >> 11);
+      const bool ends = hi > lo && (k == klo || k == khi);
+      if (tiles || ends) {
+        const Runs R = load_runs(runs + (uint64_t)k * kRunCap);
+        if (tiles)
+          for (int tt = (lo_c + kCntW - 1) >> 11; tt <= (hi_c >> 11); tt++) {
+            const int64_t idx = (int64_t)tt - t_first;
+            if (idx > n - 1) {
+              atomicOr(&notab, 1u);
+              break;
+            }
+            tstart[2 * (b + idx)] = kk;
+            tstart[2 * (b + idx) + 1] = first_base_at(A, R, roff, kk, len, tt * kCntW - run);
           }
-          const int kk = (int)(k - b);
-          const int ib = first_base_at(A, runs + (uint64_t)k * kRunCap, roff, kk, len, tt * kCntW - run);
-          tstart[2 * (b + idx)] = kk;
-          tstart[2 * (b + idx) + 1] = ib;
+        if (ends && k == klo) {  // gap-run start of base lo
+          const int x = run + base_col(A, R, roff, kk, lo - kk * kChunk, true);
+          ri[0] = x;
+          if (A.clip_l[r] >= 0) atomicMin(&A.minmax[0], x);
+        }
+        if (ends && k == khi) {  // column of base hi - 1
+          const int x = run + base_col(A, R, roff, kk, hi - 1 - kk * kChunk, false);
+          ri[1] = x;
+          if (A.clip_r[r] >= 0) atomicMax(&A.minmax[1], x);
         }
       }
-      run += cs;
-    }
-    if (t == 1023) {  // the row's last slot (chunk sum 0) now holds its end column + 1
-      const int last = run - 1;
-      if (len > 0 && (rs < 0 || last >= A.n_cols)) atomicMin(&A.minmax[2], (int)r);
+      run += c;
+    };
+#pragma unroll
+    for (int u = 0; u < kPfxUnroll; u++)
+      if (k0 + u < k1) chunk(k0 + u, cs[u]);
+    for (int64_t k = k0 + kPfxUnroll; k < k1; k++) chunk(k, chunk_sum[k]);
+    if (t == 1023 && len > 0 && (rs < 0 || end - 1 >= A.n_cols)) atomicMin(&A.minmax[2], (int)r);  // (end - 1: last column)
+    if (t == 0 && hi <= lo) {  // empty counted extent
+      ri[0] = 1;
+      ri[1] = 0;
     }
     __syncthreads();
     if (t == 0) {
-      int end = rs;
-      for (int w = 0; w < 16; w++) end += wsum[w];
       ri[2] = rs;
       ri[3] = end;
       ri[4] = len;
@@ -314,26 +389,7 @@ __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const in
       ri[6] = (int)(uint32_t)(uint64_t)b;
       ri[7] = (int)(uint32_t)((uint64_t)b >> 32);
     }
-    if (wv < 2) {
-      if (hi <= lo) {
-        if (lane == 0) ri[wv] = wv == 0 ? 1 : 0;
-      } else if (wv == 0) {  // gap-run start of base lo
-        const int i0 = (lo / kChunk) * kChunk;
-        const int x = ck_s[0] + chunk_cols_upto(A, roff, i0, lo, lane);
-        if (lane == 0) {
-          ri[0] = x;
-          if (A.clip_l[r] >= 0) atomicMin(&A.minmax[0], x);
-        }
-      } else {  // column of base hi - 1
-        const int i0 = ((hi - 1) / kChunk) * kChunk;
-        const int x = ck_s[1] + chunk_cols_upto(A, roff, i0, hi, lane) - 1;
-        if (lane == 0) {
-          ri[1] = x;
-          if (A.clip_r[r] >= 0) atomicMax(&A.minmax[1], x);
-        }
-      }
-    }
-    __syncthreads();
+    __syncthreads();  // (wsum / notab are reused by the next row)
   }
 }
 
@@ -370,9 +426,10 @@ struct TileLds {
   uint32_t bmap[kCntWaves][64];            // per-wave gap-column bitmaps
   uint32_t sel[16];                        // v_perm selectors: 4-bit gap mask -> byte picks
 };
-// LDS slot of column c: rotated by its 32-column block, so the 64 lanes' adds of one counter
-// index (columns 32l + m) fall into distinct banks
-__device__ __forceinline__ int cnt_swz(int c) { return (c & ~31) | ((c + (c >> 5)) & 31); }
+// LDS slot of column c: rotated by (32-column block & 3), so the adds of one counter index of
+// the 32 lanes of an LDS access group (lane 4a + b: column 32(4a + b) + 4((q + a) & 7) + j) fall
+// into distinct banks (4((q + a) & 7) + b + j)
+__device__ __forceinline__ int cnt_swz(int c) { return (c & ~31) | ((c + ((c >> 5) & 3)) & 31); }
 // the bin shifts (5 x GAlnColumn::addNuc/addGap bin, as bin_of) of 4 characters in a dword:
 // h = (c >> 1) & 7 picks, per byte, the only characters that can have each bin (A/a 0, C/c 1,
 // T/t 2, G/g 3, '*' 5, '-' 6; 4 and 7 none) and v_perm looks up the code, the expected
@@ -460,7 +517,7 @@ __device__ __forceinline__ void load_win(const pw_msa_args& A, uint64_t roff, in
 }
 struct RowC {  // 1 row ahead
   int ckv;
-  uint32_t gv0, gv1;
+  uint32_t gv[3];  // runs of chunks kt + (lane >> 4) + 4h, entry lane & 15 (h = 2: lanes 0-15)
   v4u w0, w1, w2;
 };
 __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint32_t* runs, const RowA& a,
@@ -472,8 +529,8 @@ __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt
   kt = min(max(kt, 0), nch);  // (a row that does not reach the tile reads a stale entry: clamped)
   const int64_t sb = a.sb;
   c.ckv = ckpt[sb + min(kt + lane, nch)];
-  c.gv0 = runs[(sb + min(kt + (lane >> 3), nch)) * kRunCap + (lane & 7)];
-  c.gv1 = runs[(sb + min(kt + 8, nch)) * kRunCap + (lane & 7)];
+#pragma unroll
+  for (int h = 0; h < 3; h++) c.gv[h] = runs[(sb + min(kt + (lane >> 4) + 4 * h, nch)) * kRunCap + (lane & 15)];
   load_win(A, a.roff, len, ib, lane, c.w0, c.w1, c.w2);
 }
 __device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
@@ -486,9 +543,10 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ __forceinline__ void cnt_flush(uint32_t (&acc)[32], LDS uint32_t* tab, int lane) {
+  const int rot = (lane >> 2) & 7;
 #pragma unroll
   for (int m = 0; m < 32; m++) {
-    const int x = cnt_swz(32 * lane + m);
+    const int x = cnt_swz(32 * lane + 4 * (((m >> 2) + rot) & 7) + (m & 3));  // (see the column groups in K3)
 #pragma unroll
     for (int f = 0; f < 6; f++) {
       atomicAdd((uint32_t*)&tab[f * kCntW + x], (acc[m] >> (5 * f)) & 31u);
@@ -516,10 +574,13 @@ __device__ int slow_bitmap(const pw_msa_args& A, const int32_t* ckpt, int64_t sb
     if (col >= c1) break;
     const int i0 = k * kChunk + 4 * lane;
     int gp[4], tot = 0;
+    int16_t raw[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) raw[j] = A.ofs[roff + (uint64_t)min(i0 + j, len - 1)];  // (unconditional: one round trip)
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const bool ok = i0 + j < len;
-      gp[j] = ok ? max((int)A.ofs[roff + i0 + j], 0) : 0;
+      gp[j] = ok ? max((int)raw[j], 0) : 0;
       tot += ok ? 1 + gp[j] : 0;
     }
     const int incl = wave_scan_incl(tot);
@@ -545,7 +606,7 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
                                                               const int32_t* __restrict__ tstart) {
   __shared__ __attribute__((aligned(16))) TileLds L;
   LDS TileLds* lp = (LDS TileLds*)&L;
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tid = threadIdx.x, lane0 = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c0 = blockIdx.x * kCntW;
   const int c1 = min(c0 + kCntW, A.n_cols);
   for (int i = tid; i < 6 * kCntW; i += 64 * kCntWaves) lp->tab[i] = 0;
@@ -570,27 +631,39 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
   uint32_t r = wv;
   if (r < A.n_rows) {
     // prologue: rows r (A, B, C), r + W (A, B), r + 2W (A)
-    uint32_t av1 = load_a(A, r, lane), av2 = load_a(A, r + W, lane), av3 = load_a(A, r + 2 * W, lane);
+    uint32_t av1 = load_a(A, r, lane0), av2 = load_a(A, r + W, lane0), av3 = load_a(A, r + 2 * W, lane0);
     RowA a1 = get_a(av1);
-    uint32_t bv1 = load_b(A, rinfo, tstart, r, a1, c0, lane);
+    uint32_t bv1 = load_b(A, rinfo, tstart, r, a1, c0, lane0);
     RowA a2 = get_a(av2);
-    uint32_t bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane);
+    uint32_t bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane0);
     RowC cc;
-    load_c(A, ckpt, runs, a1, bv1, c0, lane, cc);
+    load_c(A, ckpt, runs, a1, bv1, c0, lane0, cc);
     for (;; r += W) {
+      // (lane-derived values are recomputed per row from a lane index the compiler cannot hoist:
+      // left alone it keeps 64-bit per-lane pointers live across the loop and spills them)
+      int lane = lane0;
+      asm volatile("" : "+v"(lane));
       // the next rows' loads (each waits only for what the previous iteration issued), then this
       // row, whose batch was issued a row earlier
+      // this row's window into LDS first (its registers are then free for the next row's)
+      pin(cc.w0);
+      pin(cc.w1);
+      pin(cc.w2);
+      {
+        LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+        w4[lane] = cc.w0;
+        w4[64 + lane] = cc.w1;
+        if (lane < 8) w4[128 + lane] = cc.w2;
+      }
       RowC cn;
       load_c(A, ckpt, runs, a2, bv2, c0, lane, cn);
       const RowA a3 = get_a(av3);
       const uint32_t bv3 = load_b(A, rinfo, tstart, r + 2 * W, a3, c0, lane);
       const uint32_t av4 = load_a(A, r + 3 * W, lane);
-      pin(cc.w0);
-      pin(cc.w1);
-      pin(cc.w2);
       pin(cc.ckv);
-      pin(cc.gv0);
-      pin(cc.gv1);
+      pin(cc.gv[0]);
+      pin(cc.gv[1]);
+      pin(cc.gv[2]);
       const int elo = (int)rd(bv1, 0), ehi = (int)rd(bv1, 1);
       const int a = max(elo, c0), z = min(ehi, c1 - 1);  // counted columns of this row here
       if (a <= z) {
@@ -604,15 +677,20 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         tile_start(a1, bv1, c0, kt, ib);
         // gap bitmap: the columns outside [rs, re), then the runs of the batch's chunks
         bm[lane] = outside_mask(lane, rs - c0, re - c0);
-        const bool cv0 = kt >= 0 && kt + (lane >> 3) < nch, cv1 = kt >= 0 && kt + 8 < nch && lane < 8;
-        const bool ovf = kt < 0 || __ballot((lane & 7) == 0 && ((cv0 && cc.gv0 == kRunOverflow) ||
-                                                                (cv1 && cc.gv1 == kRunOverflow))) != 0;
+        // the batch's chunks kt .. kt + 8 (chunk kt holds c0; each later one spans >= 256 columns)
+        bool cv[3], ovl = false;
+#pragma unroll
+        for (int h = 0; h < 3; h++) {
+          cv[h] = kt >= 0 && kt + (lane >> 4) + 4 * h < nch && (h < 2 || lane < 16);
+          ovl = ovl || (cv[h] && (lane & 15) == 0 && cc.gv[h] == kRunOverflow);
+        }
+        const bool ovf = kt < 0 || __ballot(ovl) != 0;
         wave_sync();
         if (!ovf) {
 #pragma unroll
-          for (int h = 0; h < 2; h++) {
-            const uint32_t v = h == 0 ? (cv0 ? cc.gv0 : 0u) : (cv1 ? cc.gv1 : 0u);
-            const int ck = h == 0 ? __shfl(cc.ckv, lane >> 3, 64) : __builtin_amdgcn_readlane(cc.ckv, 8);
+          for (int h = 0; h < 3; h++) {
+            const uint32_t v = cv[h] ? cc.gv[h] : 0u;
+            const int ck = __shfl(cc.ckv, (lane >> 4) + 4 * h, 64);
             if (v != 0u) {
               const int s = max(ck + (int)(v >> 16) - c0, 0), e = min(ck + (int)(v >> 16) + (int)(v & 0xFFFFu) - c0, kCntW);
               for (int x = s; x < e; x = (x | 31) + 1) {
@@ -622,11 +700,6 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
               }
             }
           }
-          // the window (loaded a row ahead)
-          LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
-          w4[lane] = cc.w0;
-          w4[64 + lane] = cc.w1;
-          if (lane < 8) w4[128 + lane] = cc.w2;
         } else {
           ib = slow_bitmap(A, ckpt, sb, nch, roff, len, c0, c1, kt, lane, bm);
           v4u w0, w1, w2;
@@ -642,25 +715,44 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         const int excl = wave_scan_incl(pc) - pc;
         // byte offset in the window of the base in this lane's first clear column
         const int so = (int)((uint32_t)(roff + (uint64_t)ib) & 15u) + 32 * lane - excl;
-        const bool edge = a > c0 || z < c1 - 1;
-        const uint32_t om = edge ? outside_mask(lane, a - c0, z - c0 + 1) : 0u;
         const LDS uint8_t* wb = reinterpret_cast<const LDS uint8_t*>(win);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const uint32_t nb = (bmv >> (4 * q)) & 15u;
-          const int src = so + 4 * q - (q == 0 ? 0 : __popc(bmv & ((1u << (4 * q)) - 1u)));
-          const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
-          const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
-          const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);
-          uint32_t codes = bin_codes5(e4);
-          if (edge) {
-            const uint32_t on = (om >> (4 * q)) & 15u;
-            const uint32_t bmask = ((on * 0x00204081u) & 0x01010101u) * 0xFFu;  // 4 bits -> 4 bytes
-            codes = (codes & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
+        // step q: this lane's column group g = (q + rot) & 7 (columns 32 lane + 4g ..): the 32 lanes
+        // of an LDS access group then read 32 distinct banks of the window (lane 4a + b at dword
+        // 8(4a + b) + g: bank 8b + g), with acc[4q + j] holding column 32 lane + 4 g + j.  In the
+        // bitmap rotated right by 4 rot, group g is nibble q; its source offset is
+        // so + 4g - popc(bits below 4g) = base0 + 4q - popc(rotated bits below 4q), less 32 - pc
+        // once g has wrapped around (q >= 8 - rot).
+        const int rot = (lane >> 2) & 7;
+        const uint32_t rb = rot ? __builtin_amdgcn_alignbit(bmv, bmv, 4u * (uint32_t)rot) : bmv;
+        const int base0 = so + 4 * rot - __popc(__builtin_amdgcn_ubfe(bmv, 0, 4u * (uint32_t)rot));
+        const int wrapc = 32 - pc, qwrap = 8 - rot;
+        auto groups = [&](auto edge_c) {
+          constexpr bool kEdge = decltype(edge_c)::value;
+          uint32_t rom = 0;
+          if constexpr (kEdge) {
+            const uint32_t om = outside_mask(lane, a - c0, z - c0 + 1);
+            rom = rot ? __builtin_amdgcn_alignbit(om, om, 4u * (uint32_t)rot) : om;
           }
 #pragma unroll
-          for (int j = 0; j < 4; j++) acc[4 * q + j] += 1u << ((codes >> (8 * j)) & 31u);
-        }
+          for (int q = 0; q < 8; q++) {
+            const uint32_t nb = (rb >> (4 * q)) & 15u;
+            const int src = base0 + 4 * q - (q == 0 ? 0 : __popc(rb & ((1u << (4 * q)) - 1u))) - (q >= qwrap ? wrapc : 0);
+            const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
+            const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
+            const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);
+            uint32_t codes = bin_codes5(e4);
+            if constexpr (kEdge) {
+              const uint32_t on = (rom >> (4 * q)) & 15u;
+              const uint32_t b1 = (on * 0x00204081u) & 0x01010101u;  // 4 bits -> 4 bytes
+              const uint32_t bmask = (b1 << 8) - b1;
+              codes = (codes & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[4 * q + j] += 1u << ((codes >> (8 * j)) & 31u);
+          }
+        };
+        if (a > c0 || z < c1 - 1) groups(std::true_type{});  // the row's counted extent starts / ends here
+        else groups(std::false_type{});
         wave_sync();
       }
       a1 = a2;
@@ -864,7 +956,8 @@ __global__ __launch_bounds__(64) void row_finish(const pw_msa_args A, pw_msa_ref
 
 // scratch word of the row records (16-byte aligned: K3 reads them as uint4)
 // scratch words: chunk sums | checkpoints | slot -> row | runs (kRunCap per slot) | tile starts (2 per slot) | row records
-inline uint64_t tstart_word(uint64_t n_slots) { return (3 + (uint64_t)kRunCap) * n_slots; }
+inline uint64_t runs_word(uint64_t n_slots) { return (3 * n_slots + 3) & ~(uint64_t)3; }  // (16-byte aligned)
+inline uint64_t tstart_word(uint64_t n_slots) { return runs_word(n_slots) + (uint64_t)kRunCap * n_slots; }
 inline uint64_t rinfo_word(uint64_t n_slots) { return (tstart_word(n_slots) + 2 * n_slots + 3) & ~(uint64_t)3; }
 
 }  // namespace pw
@@ -897,13 +990,15 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
   int32_t* slot_row = a->scratch + 2 * a->n_slots;
-  uint32_t* runs = reinterpret_cast<uint32_t*>(a->scratch + 3 * a->n_slots);
+  uint32_t* runs = reinterpret_cast<uint32_t*>(a->scratch + pw::runs_word(a->n_slots));
   int32_t* tstart = a->scratch + pw::tstart_word(a->n_slots);
   int32_t* rinfo = a->scratch + pw::rinfo_word(a->n_slots);
-  hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row);
+  uint64_t* sdesc = reinterpret_cast<uint64_t*>(tstart);  // (K1's input; K2 then writes the tile starts there)
+  hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row, sdesc);
   const uint64_t nb1 = ((a->n_slots + 3) / 4 + 3) / 4;  // 4 slots per wave, 4 waves per workgroup
-  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 8192 ? nb1 : 8192)), dim3(256), 0, s, *a,
-                     chunk_sum, slot_row, runs);
+  // (persistent: ~2 rounds of resident waves, each streaming many groups)
+  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 2048 ? nb1 : 2048)), dim3(256), 0, s, *a,
+                     chunk_sum, sdesc, runs);
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(1024), 0, s, *a, chunk_sum, ckpt,
                      rinfo, runs, tstart);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kCntW - 1) / pw::kCntW);
