@@ -2,19 +2,30 @@
 //
 // Reference: the cs loop of PAFAlignment::PAFAlignment (pafreport.cpp:536-626), restated on the
 // host by pw_pack_cs (pw_host.cpp).  This kernel packs a whole batch of cs strings at once into
-// the same op words and literal bytes, one 64-lane wavefront per record:
-//   * the string is read in windows of 256 characters (4 per lane, staged in LDS);
+// the same op words and literal bytes, one 64-lane wavefront per record at a time (persistent
+// waves, the next record's head loaded ahead), 256 characters per window, 4 per lane:
+//   * a lane's 4 characters come straight from two aligned dword loads and one alignbyte (no LDS
+//     staging pass); the window is also stored in LDS once, for the next two lanes' characters
+//     (an op's digits) — that is the only LDS traffic;
 //   * in a well-formed cs string every op starts at one of ':', '*', '+', '-' and no other
 //     character is one of them (digits follow ':', letters the others), so the op starts of a
-//     window are a ballot; an op runs to the next op start (the last one of a window that does
-//     not reach the string end is carried into the next window);
-//   * each lane decodes the (at most two) ops starting in its 4 characters; wave scans of the
-//     query / target / literal advances and of the emitted-op counts place every op word and
-//     literal byte and give the positions of the reference's bounds checks.
-// Anything else — a character outside [0-9A-Za-z:*+-], a ':' run of more than 9 digits, a '*'
-// not followed by exactly two characters, an empty indel or one holding a digit, '~' / '=', a
-// bounds violation, one op longer than a window — flags the record PW_PACK_HOST: the caller packs it with pw_pack_cs, which produces
-// the reference's exact error (such records are rare and end the report at their line anyway).
+//     window are a ballot, and an op runs to the next op start (the last one of a window that
+//     does not reach the string end is carried into the next window); a lane holds at most two
+//     op starts (every op has at least two characters);
+//   * per op: the 8 characters after its start are a register image (two alignbytes of this and
+//     the next two lanes' characters): a ':' run of 1-9 digits is checked and converted in SIMD
+//     (two 4-digit halves, then the 9th); per character: its governing op (its own lane's, or the last start
+//     below it: a DPP max-scan) says whether it is a literal ('*' pair, '-' bases) or must be a
+//     letter ('+' / '-' content);
+//   * DPP wave scans of the query / target / literal advances and of the packed op / event /
+//     substitution counts place every op word and literal byte (byte stores, one per literal
+//     character, from the lane that holds it) and give the positions of the reference's bounds
+//     checks; the record totals are the scans' last lanes (no LDS reductions).
+// Anything else — a character outside [0-9A-Za-z:*+-], a ':' run of 0 or more than 9 digits, a
+// '*' not followed by exactly two characters, an empty indel or one holding a digit, '~' / '=', a
+// bounds violation, one op longer than a window — flags the record PW_PACK_HOST: the caller packs
+// it with pw_pack_cs, which produces the reference's exact error (such records are rare and end
+// the report at their line anyway).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,254 +36,259 @@ namespace pw {
 
 #define LDS __attribute__((address_space(3)))
 constexpr int kPackWin = 256;  // characters per window (4 per lane)
-constexpr uint64_t kPkBoundSub = 190, kPkBoundIndel = 140;  // = the host packer's text bounds
+constexpr uint32_t kPkBoundSub = 190, kPkBoundIndel = 140;  // = the host packer's text bounds
 
-__device__ __forceinline__ bool pk_digit(uint32_t c) { return c - '0' < 10u; }
-__device__ __forceinline__ bool pk_alpha(uint32_t c) { return (c | 0x20u) - 'a' < 26u; }
-__device__ __forceinline__ bool pk_opc(uint32_t c) { return c == ':' || c == '*' || c == '+' || c == '-'; }
-__device__ __forceinline__ uint32_t pk_up(uint32_t c) { return c - 'a' < 26u ? c - 32u : c; }
-__device__ __forceinline__ bool pk_acgt(uint32_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
-
-struct PkOp {
-  uint32_t type;  // 0 ':', 1 '*', 2 '-' (INS), 3 '+' (DEL); PW_OP_* order
-  int n;          // ':' value / indel length
-  int s, e;       // content [s, e) in the window
-  bool emit;      // an op word is written (':0' is dropped)
-};
+// per byte of a dword: 0x80 where the byte is (not) in a class
+__device__ __forceinline__ uint32_t bytes_eq(uint32_t x, uint32_t c) {  // 0x80 where byte == c
+  const uint32_t t = x ^ (c * 0x01010101u);
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t bytes_digit(uint32_t x) {  // 0x80 where '0'..'9'
+  const uint32_t t = x ^ 0x30303030u;                          // digits -> 0..9
+  return ~(((t & 0x7F7F7F7Fu) + 0x76767676u) | t) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t bytes_alpha(uint32_t x) {  // 0x80 where A-Z / a-z
+  // per byte u = 0x80 + (c & 0xDF) - 'A' (every byte >= 0x80 before the subtraction: no borrow)
+  const uint32_t u = ((x & 0xDFDFDFDFu) | 0x80808080u) - 0x41414141u;
+  const uint32_t t = u ^ 0x80808080u;  // (c & 0xDF) - 'A' where that is >= 0, else a byte >= 0x80
+  const uint32_t lt26 = ~(((t & 0x7F7F7F7Fu) + 0x66666666u) | t) & 0x80808080u;  // 0 <= t < 26
+  return lt26 & ~(x & 0x80808080u);  // (bytes >= 0x80 are not letters)
+}
+__device__ __forceinline__ uint32_t msb_bits(uint32_t m) {  // 0x80 per byte -> bits 0..3
+  return (m >> 7 & 1u) | (m >> 14 & 2u) | (m >> 21 & 4u) | (m >> 28 & 8u);
+}
+// value of a run of 4 decimal digits held as byte values 0..9, most significant in byte 0
+__device__ __forceinline__ uint32_t dec4(uint32_t x) {
+  const uint32_t y = (x * 10u + (x >> 8)) & 0x00FF00FFu;
+  return (y * 100u + (y >> 16)) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t up_bytes(uint32_t x) {  // a-z -> A-Z per byte (letters only)
+  return x & ~(bytes_alpha(x) >> 2);                         // 0x80 >> 2 = 0x20: clear the case bit
+}
+__device__ __forceinline__ uint32_t dpp_max_incl(uint32_t v) {  // inclusive prefix max (v >= 0)
+  v = max(v, dpp_or_zero<0x111>(v));
+  v = max(v, dpp_or_zero<0x112>(v));
+  v = max(v, dpp_or_zero<0x114>(v));
+  v = max(v, dpp_or_zero<0x118>(v));
+  v = max(v, dpp_or_zero<0x142, 0xA>(v));
+  v = max(v, dpp_or_zero<0x143, 0xC>(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane l gets lane l-1's value (lane 0: 0)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
 
 // A record's head, loaded one record ahead: its extent, offset / query length and the first
-// window as aligned dwords (lane l: bytes [a0 + 4l, a0 + 4l + 4); lane 0 also the dword after the
-// window, which an unaligned start needs).  Addresses past the record are clamped to its last
-// dword: the caller's text is only readable up to the last record's end (+16 bytes).
+// window's two aligned dwords per lane.  Addresses past the record are clamped to its last dword
+// (the caller's text is only readable up to the last record's end + 16 bytes).
 struct PkHead {
   uint64_t base, L;
   int off, ql;
   uint32_t d0, d1;
 };
+__device__ __forceinline__ void pk_words(const uint8_t* text, uint64_t st, uint64_t last, int lane, uint32_t& d0,
+                                         uint32_t& d1) {
+  const uint64_t a0 = (st & ~3ull) + 4ull * (uint64_t)lane;
+  d0 = *reinterpret_cast<const uint32_t*>(text + (a0 < last ? a0 : last));
+  d1 = *reinterpret_cast<const uint32_t*>(text + (a0 + 4 < last ? a0 + 4 : last));
+}
 __device__ __forceinline__ void pk_head(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
                                         const int32_t* qlen, uint32_t ri, int lane, PkHead& h) {
   h.base = cs_off[ri];
   h.L = cs_off[ri + 1] - h.base;
   h.off = offset[ri];
   h.ql = qlen[ri];
-  const uint64_t a0 = h.base & ~3ull, last = h.L ? (h.base + h.L - 1) & ~3ull : a0;
-  const uint64_t x0 = a0 + 4ull * (uint64_t)lane, x1 = a0 + 256ull;
-  h.d0 = *reinterpret_cast<const uint32_t*>(text + (x0 < last ? x0 : last));
-  h.d1 = *reinterpret_cast<const uint32_t*>(text + (x1 < last ? x1 : last));
-}
-// stage window bytes [pos, pos + 256) of the record into w (from the dwords of pk_head when pos
-// is 0, else loaded here); returns the window's shift inside the staging buffer
-__device__ __forceinline__ int pk_stage(const uint8_t* text, const PkHead& h, uint64_t pos, int lane, LDS uint8_t* wr,
-                                        bool first) {
-  const uint64_t st = h.base + pos, a0 = st & ~3ull, last = (h.base + h.L - 1) & ~3ull;
-  uint32_t d0 = h.d0, d1 = h.d1;
-  if (!first) {
-    const uint64_t x0 = a0 + 4ull * (uint64_t)lane, x1 = a0 + 256ull;
-    d0 = *reinterpret_cast<const uint32_t*>(text + (x0 < last ? x0 : last));
-    d1 = *reinterpret_cast<const uint32_t*>(text + (x1 < last ? x1 : last));
-  }
-  *reinterpret_cast<LDS uint32_t*>(wr + 4 * lane) = d0;
-  if (lane == 0) *reinterpret_cast<LDS uint32_t*>(wr + 256) = d1;
-  return (int)(st & 3ull);
+  const uint64_t last = h.L ? (h.base + h.L - 1) & ~3ull : h.base & ~3ull;
+  pk_words(text, h.base, last, lane, h.d0, h.d1);
 }
 
-// Persistent wavefronts: wave g takes records g, g + NW, ...; the next record's head and first
-// window are loaded before this one is decoded, so their latency hides behind the decode (the
-// per-record work is a short dependent chain: load -> classify -> scans -> stores).
 __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
                                                       const int32_t* qlen, uint32_t n, uint32_t* ops, uint8_t* lits,
                                                       pw_cs_rec* out) {
-  __shared__ uint8_t win[4][kPackWin + 8];   // staged window (shifted by the start's alignment)
-  __shared__ uint8_t wz[4][kPackWin + 8];    // the window from its first character, zeros past its end
+  __shared__ uint32_t win[4][kPackWin / 4 + 4];  // the window's characters, zeros past its end (lanes read 3 dwords on)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar loop)
-  // (address-space-3 pointers: through a generic one every window read would be a flat load,
-  // which also waits for the wave's outstanding global stores)
-  LDS uint8_t* wr = (LDS uint8_t*)win[wv];
-  LDS uint8_t* w = (LDS uint8_t*)wz[wv];
+  LDS uint32_t* w = (LDS uint32_t*)win[wv];
   const uint32_t nw = gridDim.x * 4;
   uint32_t ri = blockIdx.x * 4 + (uint32_t)wv;
   if (ri >= n) return;
   PkHead nxt;
   pk_head(text, cs_off, offset, qlen, ri, lane, nxt);
+  if (lane < 4) w[64 + lane] = 0u;
   for (; ri < n; ri += nw) {
     const PkHead cur = nxt;
-    if (ri + nw < n) pk_head(text, cs_off, offset, qlen, ri + nw, lane, nxt);
+    pk_head(text, cs_off, offset, qlen, ri + nw < n ? ri + nw : ri, lane, nxt);
     const uint64_t base = cur.base, L = cur.L;
+    const uint64_t last = L ? (base + L - 1) & ~3ull : base & ~3ull;
     const int off = cur.off, ql = cur.ql;
     int qpos = 0, tpos = 0;
     uint32_t nops = 0, nlits = 0, nev = 0;
     uint64_t bound = 0;
     bool bad = false, acgt = true;
     uint64_t pos = 0;
-    while (pos < L && !bad) {
+    while (pos < L) {
       const int wl = (int)(L - pos < (uint64_t)kPackWin ? L - pos : (uint64_t)kPackWin);
       const bool last_win = pos + (uint64_t)wl == L;
-      // stage the window (aligned dword loads, then this lane's 4 characters re-read at the
-      // window's shift; zeros past its end)
-      const int sh = pk_stage(text, cur, pos, lane, wr, pos == 0);
+      // this lane's 4 characters (zeros past the window)
+      uint32_t d0 = cur.d0, d1 = cur.d1;
+      if (pos) pk_words(text, base + pos, last, lane, d0, d1);
+      const uint32_t sh = (uint32_t)((base + pos) & 3ull);
+      uint32_t c4 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      const int have = min(max(wl - 4 * lane, 0), 4);  // characters of this lane in the window
+      c4 = have >= 4 ? c4 : (c4 & ((1u << (8 * have)) - 1u));
+      w[lane] = c4;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      uint32_t c4 = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int i = 4 * lane + j;
-        const uint32_t c = i < wl ? (uint32_t)wr[sh + i] : 0u;
-        c4 |= c << (8 * j);
-      }
-      __builtin_amdgcn_wave_barrier();
-      *reinterpret_cast<LDS uint32_t*>(w + 4 * lane) = c4;
-      if (lane == 0) *reinterpret_cast<LDS uint32_t*>(w + kPackWin) = 0u;
-      __builtin_amdgcn_wave_barrier();
-      // character classes; op starts
-      bool lbad = false;
-      uint32_t smask = 0;  // op starts among this lane's 4 characters (bit j)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int i = 4 * lane + j;
-        const uint32_t c = (c4 >> (8 * j)) & 0xFFu;
-        if (i < wl) {
-          if (pk_opc(c)) smask |= 1u << j;
-          else if (!pk_digit(c) && !pk_alpha(c)) lbad = true;
-        }
-      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t n1 = w[lane + 1], n2 = w[lane + 2], n3 = w[lane + 3];  // the next 12 characters
+      // classes (per byte 0x80), restricted to the lane's characters
+      const uint32_t vmask = have >= 4 ? 0x80808080u : ((0x80808080u << (8 * have)) ^ 0x80808080u) & 0x80808080u;
+      const uint32_t m_col = bytes_eq(c4, ':'), m_sub = bytes_eq(c4, '*'), m_ins = bytes_eq(c4, '-'),
+                     m_del = bytes_eq(c4, '+');
+      const uint32_t m_op = (m_col | m_sub | m_ins | m_del) & vmask;
+      const uint32_t m_dig = bytes_digit(c4), m_alp = bytes_alpha(c4);
+      bool lbad = (vmask & ~(m_op | m_dig | m_alp)) != 0;
+      const uint32_t smask = msb_bits(m_op);  // op starts among this lane's characters (bit j)
       // every window starts at an op start (the string's first character, or an op carried over)
-      if (!((uint32_t)__shfl((int)smask, 0, 64) & 1u)) {
-        bad = true;
-        break;
-      }
-      // the window's last op start (it runs past the window unless the string ends here)
+      const bool starts = (__builtin_amdgcn_readfirstlane(smask) & 1u) != 0;
       const uint64_t any = __ballot(smask != 0);
-      const int ll = 63 - __builtin_clzll(any);
-      const uint32_t lmask = (uint32_t)__shfl((int)smask, ll, 64);
-      const int last_start = 4 * ll + (31 - __builtin_clz(lmask));
+      const int ll = 63 - __builtin_clzll(any | 1ull);
+      const uint32_t lmask = (uint32_t)__builtin_amdgcn_readlane((int)smask, ll);
+      const int last_start = 4 * ll + (31 - __builtin_clz(lmask | 1u));
       const int lim = last_win ? wl : last_start;  // ops starting before lim are decoded now
-      if (!last_win && last_start == 0) {
-        bad = true;  // one op fills the window
-        break;
-      }
-      // decode this lane's ops (one per op start among its 4 characters, in registers: j is a
-      // constant after unrolling).  An op ends at the next op start: the next set bit of this
-      // lane's starts, else the first start of the next lane that has one, else the window end.
-      const uint64_t nxt_l = lane == 63 ? 0ull : any & ~((2ull << lane) - 1ull);  // op-start lanes above
-      const int nl = nxt_l ? __builtin_ctzll(nxt_l) : 64;
+      // the first op start after this lane's characters (an op ends there)
+      const uint64_t above = lane == 63 ? 0ull : any & ~((2ull << lane) - 1ull);
+      const int nl = above ? __builtin_ctzll(above) : 64;
       const uint32_t nl_mask = (uint32_t)__shfl((int)smask, nl < 64 ? nl : 0, 64);
       const int next_start = nl < 64 ? 4 * nl + __builtin_ctz(nl_mask) : wl;
-      PkOp op[4];
-      bool has[4];
-      int la_q = 0, la_t = 0, la_l = 0, la_e = 0, la_v = 0;
-      uint64_t la_b = 0;
+      // this lane's op starts before lim: at most two
+      const int lim_l = min(max(lim - 4 * lane, 0), 4);
+      const uint32_t sm = smask & ((1u << lim_l) - 1u);
+      const int ns = __popc(sm);
+      lbad = lbad || ns > 2;
+      int q_a = 0, t_a = 0;                  // query / target advance of this lane's ops
+      uint32_t cnt = 0;                      // ops emitted | events << 10 | substitutions << 20
+      uint32_t opw[2] = {0u, 0u};
+      int qb[2] = {0, 0}, qn[2] = {0, 0};    // bounds checks: query advance before the op, its length
+      int kind[2] = {-1, -1};                // 0 ':' 1 '*' 2 '-' 3 '+' (PW_OP_* order), -1 none
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        const uint32_t rest = t == 0 ? sm : (sm & (sm - 1u));
+        if (!rest) continue;
+        const int j = __builtin_ctz(rest);
+        const uint32_t after = smask & ~((2u << j) - 1u);  // this lane's next start (a carried op's too)
+        const int s = 4 * lane + j, e = after ? 4 * lane + __builtin_ctz(after) : next_start;
+        const int len = e - s - 1;
+        const uint32_t c = (c4 >> (8 * j)) & 0xFFu;
+        // the 8 characters after the op start (zeros past the window)
+        const uint32_t k1 = (uint32_t)j + 1u;
+        const uint32_t lo = k1 < 4 ? __builtin_amdgcn_alignbyte(n1, c4, k1) : n1;
+        const uint32_t hi = k1 < 4 ? __builtin_amdgcn_alignbyte(n2, n1, k1) : n2;
+        const uint32_t c9 = (k1 < 4 ? __builtin_amdgcn_alignbyte(n3, n2, k1) : n3) & 0xFFu;  // the 9th
+        const int ty = c == ':' ? PW_OP_MATCH : (c == '*' ? PW_OP_SUB : (c == '-' ? PW_OP_INS : PW_OP_DEL));
+        kind[t] = ty;
+        qb[t] = q_a;
+        if (ty == PW_OP_MATCH) {
+          // 1..9 digits: checked and converted in SIMD (8 as two 4-digit halves, then the 9th)
+          const uint64_t d = (uint64_t)(lo ^ 0x30303030u) | (uint64_t)(hi ^ 0x30303030u) << 32;
+          const uint32_t dg_lo = bytes_digit(lo), dg_hi = bytes_digit(hi);
+          const uint64_t need = len >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull & ((1ull << (8 * len)) - 1ull));
+          const uint64_t have_d = (uint64_t)dg_lo | (uint64_t)dg_hi << 32;
+          if (len < 1 || len > 9 || (need & ~have_d) || (len == 9 && c9 - '0' > 9u)) lbad = true;
+          const int ln = min(max(len, 1), 8);
+          const uint64_t al = (d & (ln >= 8 ? ~0ull : ((1ull << (8 * ln)) - 1ull))) << (8 * (8 - ln));  // right-aligned
+          const uint32_t v8 = dec4((uint32_t)al) * 10000u + dec4((uint32_t)(al >> 32));
+          const uint32_t v = len == 9 ? v8 * 10u + (c9 - '0') : v8;
+          qn[t] = (int)v;
+          q_a += (int)v;
+          t_a += (int)v;
+          if (v > 0) {
+            opw[t] = PW_OP(PW_OP_MATCH, v);
+            cnt += 1u;
+          }
+        } else if (ty == PW_OP_SUB) {
+          if (len != 2) lbad = true;  // (any two characters, as the host packer takes them)
+          qn[t] = 0;
+          q_a += 1;
+          t_a += 1;
+          opw[t] = PW_OP(PW_OP_SUB, 1u);
+          cnt += 1u | 1u << 10 | 1u << 20;
+        } else {
+          if (len < 1) lbad = true;
+          qn[t] = ty == PW_OP_DEL ? len : 0;
+          if (ty == PW_OP_INS) t_a += len;
+          else q_a += len;
+          opw[t] = PW_OP((uint32_t)ty, (uint32_t)max(len, 0));
+          cnt += 1u | 1u << 10;
+        }
+      }
+      // per character: its governing op (this lane's last start at or before it, else the last
+      // one below the lane) -> literal ('*' pair, '-' bases) or letter required ('+' / '-')
+      const int klast = kind[ns >= 2 ? 1 : 0];
+      const uint32_t key_own = sm ? ((uint32_t)(4 * lane + 31 - __builtin_clz(sm)) << 2 | (uint32_t)(klast & 3)) + 1u : 0u;
+      const uint32_t key_below = wave_shr1(dpp_max_incl(key_own));
+      uint32_t litm = 0;  // literal characters of this lane (bit j)
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const int s = 4 * lane + j;
-        has[j] = ((smask >> j) & 1u) && s < lim;
-        PkOp& o = op[j];
-        o.type = PW_OP_MATCH;
-        o.n = 0;
-        o.s = s + 1;
-        o.emit = false;
-        const uint32_t later = (smask >> (j + 1)) << (j + 1);  // this lane's starts after j
-        const int e = later ? 4 * lane + __builtin_ctz(later) : next_start;
-        o.e = e;
-        if (has[j]) {
-          const uint32_t c = (c4 >> (8 * j)) & 0xFFu;
-          const int len = e - s - 1;
-          o.n = len;
-          o.emit = true;
-          if (c == ':') {
-            o.type = PW_OP_MATCH;
-            if (len < 1 || len > 9) lbad = true;
-            int v = 0;
-            for (int k = s + 1; k < e && k < s + 10; k++) {
-              const uint32_t d = w[k];
-              if (!pk_digit(d)) lbad = true;
-              v = v * 10 + (int)(d - '0');
-            }
-            o.n = v;
-            o.emit = v > 0;
-            la_q += v;
-            la_t += v;
-          } else if (c == '*') {
-            o.type = PW_OP_SUB;
-            if (len != 2) lbad = true;  // (any two characters, as the host packer takes them)
-            o.n = 1;
-            la_q += 1;
-            la_t += 1;
-            la_l += 2;
-            la_v += 1;
-            la_b += kPkBoundSub;
-          } else {
-            o.type = c == '-' ? PW_OP_INS : PW_OP_DEL;
-            if (len < 1) lbad = true;
-            for (int k = s + 1; k < e; k++)  // (the host's is_alpha run ends at a digit: UNHANDLED)
-              if (!pk_alpha(w[k])) lbad = true;
-            if (c == '-') {
-              la_t += len;
-              la_l += len;
-            } else {
-              la_q += len;
-            }
-            la_v += 1;
-            la_b += kPkBoundIndel;
-          }
-          la_e += o.emit ? 1 : 0;
-        }
-      }
-      if (__ballot(lbad)) {
-        bad = true;
-        break;
-      }
-      // exclusive prefixes over the lanes (ops are in lane order)
-      const int iq = wave_scan_incl(la_q), it = wave_scan_incl(la_t), il = wave_scan_incl(la_l),
-                ie = wave_scan_incl(la_e);
-      int q = qpos + iq - la_q;
-      uint32_t lp = nlits + (uint32_t)(il - la_l), op_i = nops + (uint32_t)(ie - la_e);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (!has[k]) continue;
-        const PkOp& o = op[k];
-        const int qp = off + q;
-        if (o.type == PW_OP_MATCH) {
-          if (qp < 0 || (int64_t)qp + o.n > ql) lbad = true;
-          q += o.n;
-        } else if (o.type == PW_OP_SUB) {
-          if (qp < 0 || qp > ql) lbad = true;
-          const uint32_t a = pk_up(w[o.s]), b = pk_up(w[o.s + 1]);
-          lits[base + lp] = (uint8_t)a;
-          lits[base + lp + 1] = (uint8_t)b;
-          acgt = acgt && pk_acgt(a) && pk_acgt(b);
-          lp += 2;
-          q += 1;
-        } else if (o.type == PW_OP_INS) {
-          for (int x = o.s; x < o.e; x++) {
-            const uint32_t a = pk_up(w[x]);
-            lits[base + lp++] = (uint8_t)a;
-            acgt = acgt && pk_acgt(a);
-          }
+        const int i = 4 * lane + j;
+        if (i >= lim || ((sm >> j) & 1u)) continue;
+        const uint32_t own = sm & ((1u << j) - 1u);
+        int g, ty;
+        if (own) {
+          const int jj = 31 - __builtin_clz(own);
+          g = 4 * lane + jj;
+          ty = (jj == __builtin_ctz(sm)) ? kind[0] : kind[1];
         } else {
-          if (qp < 0 || (int64_t)qp + o.n > ql) lbad = true;
-          q += o.n;
+          g = key_below ? (int)((key_below - 1u) >> 2) : -1;
+          ty = key_below ? (int)((key_below - 1u) & 3u) : -1;
         }
-        if (o.emit) ops[base + op_i++] = PW_OP(o.type, (uint32_t)o.n);
+        const bool letter = ((m_alp >> (8 * j + 7)) & 1u) != 0;
+        if ((ty == PW_OP_INS || ty == PW_OP_DEL) && !letter) lbad = true;
+        if (ty == PW_OP_INS || (ty == PW_OP_SUB && i - g - 1 < 2)) litm |= 1u << j;
       }
-      if (__ballot(lbad)) {
-        bad = true;
+      // exclusive prefixes over the lanes (ops and characters are in lane order)
+      const uint32_t nlit = (uint32_t)__popc(litm);
+      const int iq = wave_scan_incl(q_a), it = wave_scan_incl(t_a);
+      const uint32_t il = wave_scan_incl(nlit), ic = wave_scan_incl(cnt);
+      // bounds checks (pafreport.cpp:542-626 as restated by pw_pack_cs)
+      const int q0 = qpos + iq - q_a;
+#pragma unroll
+      for (int t = 0; t < 2; t++) {
+        if (kind[t] < 0) continue;
+        const int qp = off + q0 + qb[t];
+        if (kind[t] == PW_OP_SUB) {
+          if (qp < 0 || qp > ql) lbad = true;
+        } else if (kind[t] != PW_OP_INS) {
+          if (qp < 0 || (int64_t)qp + qn[t] > ql) lbad = true;
+        }
+      }
+      if (__ballot(lbad) || !starts || (!last_win && last_start == 0)) {
+        bad = true;  // (one op filling a window also lands here)
         break;
+      }
+      // op words and literal bytes at their places
+      uint32_t op_i = nops + ((ic - cnt) & 0x3FFu);
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+        if (opw[t]) ops[base + op_i++] = opw[t];
+      const uint32_t lp0 = nlits + il - nlit;
+      const uint32_t u4 = up_bytes(c4);
+      uint32_t lp = lp0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (!((litm >> j) & 1u)) continue;
+        const uint32_t a = (u4 >> (8 * j)) & 0xFFu;
+        lits[base + lp++] = (uint8_t)a;
+        acgt = acgt && (a == 'A' || a == 'C' || a == 'G' || a == 'T');
       }
       // ':' values up to 999,999,999: sums stay in range for queries below 2^31
       qpos += wave_last(iq);
       tpos += wave_last(it);
-      nlits += (uint32_t)wave_last(il);
-      nops += (uint32_t)wave_last(ie);
-      {
-        uint32_t v = (uint32_t)la_v;
-        uint64_t bb = la_b;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-          v += (uint32_t)__shfl_xor((int)v, d, 64);
-          bb += (uint64_t)__shfl_xor((long long)bb, d, 64);
-        }
-        nev += v;
-        bound += bb;
-      }
+      nlits += wave_last(il);
+      const uint32_t ctot = wave_last(ic);
+      nops += ctot & 0x3FFu;
+      nev += (ctot >> 10) & 0x3FFu;
+      const uint32_t nsub = ctot >> 20;
+      bound += (uint64_t)kPkBoundIndel * ((ctot >> 10 & 0x3FFu) - nsub) + (uint64_t)kPkBoundSub * nsub;
       pos += (uint64_t)lim;
       __builtin_amdgcn_wave_barrier();
     }
