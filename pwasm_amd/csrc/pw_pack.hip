@@ -78,13 +78,13 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane l gets lane
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// A record's head, loaded one record ahead: its extent, offset / query length and the first
-// window's two aligned dwords per lane.  Addresses past the record are clamped to its last dword
-// (the caller's text is only readable up to the last record's end + 16 bytes).
+// A record's head in two prefetch stages (vector loads, so each wait is a vmcnt wait in issue
+// order): its extent, offset and query length two records ahead, then its first window's two
+// aligned dwords per lane one record ahead.  Addresses past the record are clamped to its last
+// dword (the caller's text is only readable up to the last record's end + 16 bytes).
 struct PkHead {
-  uint64_t base, L;
+  uint64_t base, end;
   int off, ql;
-  uint32_t d0, d1;
 };
 __device__ __forceinline__ void pk_words(const uint8_t* text, uint64_t st, uint64_t last, int lane, uint32_t& d0,
                                          uint32_t& d1) {
@@ -92,15 +92,18 @@ __device__ __forceinline__ void pk_words(const uint8_t* text, uint64_t st, uint6
   d0 = *reinterpret_cast<const uint32_t*>(text + (a0 < last ? a0 : last));
   d1 = *reinterpret_cast<const uint32_t*>(text + (a0 + 4 < last ? a0 + 4 : last));
 }
-__device__ __forceinline__ void pk_head(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
-                                        const int32_t* qlen, uint32_t ri, int lane, PkHead& h) {
+__device__ __forceinline__ uint64_t pk_last(const PkHead& h) {  // the record's last dword
+  return h.end > h.base ? (h.end - 1) & ~3ull : h.base & ~3ull;
+}
+__device__ __forceinline__ void pk_head(const uint64_t* cs_off, const int32_t* offset, const int32_t* qlen, uint32_t ri,
+                                        PkHead& h) {
   h.base = cs_off[ri];
-  h.L = cs_off[ri + 1] - h.base;
+  h.end = cs_off[ri + 1];
   h.off = offset[ri];
   h.ql = qlen[ri];
-  const uint64_t last = h.L ? (h.base + h.L - 1) & ~3ull : h.base & ~3ull;
-  pk_words(text, h.base, last, lane, h.d0, h.d1);
 }
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(PkHead& h) { asm volatile("" : "+v"(h.base), "+v"(h.end), "+v"(h.off), "+v"(h.ql)); }
 
 __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
                                                       const int32_t* qlen, uint32_t n, uint32_t* ops, uint8_t* lits,
@@ -111,26 +114,42 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
   const uint32_t nw = gridDim.x * 4;
   uint32_t ri = blockIdx.x * 4 + (uint32_t)wv;
   if (ri >= n) return;
-  PkHead nxt;
-  pk_head(text, cs_off, offset, qlen, ri, lane, nxt);
+  const uint32_t nl1 = n - 1;
+  PkHead h1, h2;
+  pk_head(cs_off, offset, qlen, ri, h1);
+  pk_head(cs_off, offset, qlen, ri + nw < n ? ri + nw : nl1, h2);
+  uint32_t d0n, d1n;
+  pk_words(text, h1.base, pk_last(h1), lane, d0n, d1n);
   if (lane < 4) w[64 + lane] = 0u;
   for (; ri < n; ri += nw) {
-    const PkHead cur = nxt;
-    pk_head(text, cs_off, offset, qlen, ri + nw < n ? ri + nw : ri, lane, nxt);
-    const uint64_t base = cur.base, L = cur.L;
-    const uint64_t last = L ? (base + L - 1) & ~3ull : base & ~3ull;
+    // this record's head (two stages loaded ahead); the next record's first window words and the
+    // one after's head are issued before this record is decoded
+    pin(h1);
+    pin(d0n);
+    pin(d1n);
+    const PkHead cur = h1;
+    const uint32_t w0 = d0n, w1 = d1n;
+    pin(h2);
+    pk_words(text, h2.base, pk_last(h2), lane, d0n, d1n);
+    h1 = h2;
+    pk_head(cs_off, offset, qlen, ri + 2 * nw < n ? ri + 2 * nw : nl1, h2);
+    const uint64_t base = __builtin_amdgcn_readfirstlane((int)(uint32_t)cur.base) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(cur.base >> 32)) << 32;
+    const uint64_t L = cur.end - cur.base;
+    const uint64_t last = pk_last(cur);
     const int off = cur.off, ql = cur.ql;
     int qpos = 0, tpos = 0;
     uint32_t nops = 0, nlits = 0, nev = 0;
     uint64_t bound = 0;
     bool bad = false, acgt = true;
     uint64_t pos = 0;
-    while (pos < L) {
+    uint32_t* const ops_r = ops + base;  // (uniform: stores take 32-bit lane offsets)
+    uint8_t* const lits_r = lits + base;
+    // one 256-character window at pos (the first from the prefetched words; later ones load theirs)
+    auto window = [&](uint32_t d0, uint32_t d1) -> bool {
       const int wl = (int)(L - pos < (uint64_t)kPackWin ? L - pos : (uint64_t)kPackWin);
       const bool last_win = pos + (uint64_t)wl == L;
       // this lane's 4 characters (zeros past the window)
-      uint32_t d0 = cur.d0, d1 = cur.d1;
-      if (pos) pk_words(text, base + pos, last, lane, d0, d1);
       const uint32_t sh = (uint32_t)((base + pos) & 3ull);
       uint32_t c4 = __builtin_amdgcn_alignbyte(d1, d0, sh);
       const int have = min(max(wl - 4 * lane, 0), 4);  // characters of this lane in the window
@@ -165,85 +184,70 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       const uint32_t sm = smask & ((1u << lim_l) - 1u);
       const int ns = __popc(sm);
       lbad = lbad || ns > 2;
+      // the (at most two) ops of this lane, without branches: every quantity is computed for both
+      // slots and selected by the op kind (a divergent branch per kind costs every wave all kinds)
       int q_a = 0, t_a = 0;                  // query / target advance of this lane's ops
       uint32_t cnt = 0;                      // ops emitted | events << 10 | substitutions << 20
-      uint32_t opw[2] = {0u, 0u};
-      int qb[2] = {0, 0}, qn[2] = {0, 0};    // bounds checks: query advance before the op, its length
-      int kind[2] = {-1, -1};                // 0 ':' 1 '*' 2 '-' 3 '+' (PW_OP_* order), -1 none
+      uint32_t opw[2];
+      bool emit[2];
+      int qb[2], qn[2];                      // bounds checks: query advance before the op, its length
+      int kind[2];                           // 0 ':' 1 '*' 2 '-' 3 '+' (PW_OP_* order), -1 none
+      const uint32_t sm1 = sm & (sm - 1u);
 #pragma unroll
       for (int t = 0; t < 2; t++) {
-        const uint32_t rest = t == 0 ? sm : (sm & (sm - 1u));
-        if (!rest) continue;
-        const int j = __builtin_ctz(rest);
+        const uint32_t rest = t == 0 ? sm : sm1;
+        const bool valid = rest != 0;
+        const int j = __builtin_ctz(rest | 8u);  // (3 when none: any in-range value)
         const uint32_t after = smask & ~((2u << j) - 1u);  // this lane's next start (a carried op's too)
-        const int s = 4 * lane + j, e = after ? 4 * lane + __builtin_ctz(after) : next_start;
-        const int len = e - s - 1;
-        const uint32_t c = (c4 >> (8 * j)) & 0xFFu;
-        // the 8 characters after the op start (zeros past the window)
+        const int e = after ? 4 * lane + __builtin_ctz(after) : next_start;
+        const int len = e - (4 * lane + j) - 1;
+        const uint32_t c = __builtin_amdgcn_ubfe(c4, 8u * (uint32_t)j, 8u);
+        // the 9 characters after the op start (zeros past the window)
         const uint32_t k1 = (uint32_t)j + 1u;
-        const uint32_t lo = k1 < 4 ? __builtin_amdgcn_alignbyte(n1, c4, k1) : n1;
-        const uint32_t hi = k1 < 4 ? __builtin_amdgcn_alignbyte(n2, n1, k1) : n2;
-        const uint32_t c9 = (k1 < 4 ? __builtin_amdgcn_alignbyte(n3, n2, k1) : n3) & 0xFFu;  // the 9th
-        const int ty = c == ':' ? PW_OP_MATCH : (c == '*' ? PW_OP_SUB : (c == '-' ? PW_OP_INS : PW_OP_DEL));
-        kind[t] = ty;
+        const bool k4 = k1 >= 4;
+        const uint32_t lo = k4 ? n1 : __builtin_amdgcn_alignbyte(n1, c4, k1);
+        const uint32_t hi = k4 ? n2 : __builtin_amdgcn_alignbyte(n2, n1, k1);
+        const uint32_t c9 = (k4 ? n3 : __builtin_amdgcn_alignbyte(n3, n2, k1)) & 0xFFu;
+        const bool is_col = valid && c == ':', is_sub = valid && c == '*', is_ins = valid && c == '-',
+                   is_del = valid && c == '+';
+        kind[t] = is_col ? PW_OP_MATCH : (is_sub ? PW_OP_SUB : (is_ins ? PW_OP_INS : (is_del ? PW_OP_DEL : -1)));
+        // ':' - 1..9 digits, checked and converted in SIMD (8 as two 4-digit halves, then the 9th)
+        const uint64_t d = (uint64_t)(lo ^ 0x30303030u) | (uint64_t)(hi ^ 0x30303030u) << 32;
+        const uint64_t have_d = (uint64_t)bytes_digit(lo) | (uint64_t)bytes_digit(hi) << 32;
+        const int ln = min(max(len, 1), 8);
+        const uint64_t lmask = ln >= 8 ? ~0ull : ((1ull << (8 * ln)) - 1ull);
+        const bool dig_bad = len < 1 || len > 9 || (lmask & 0x8080808080808080ull & ~have_d) || (len == 9 && c9 - '0' > 9u);
+        const uint64_t al = (d & lmask) << (8 * (8 - ln));  // right-aligned
+        const uint32_t v8 = dec4((uint32_t)al) * 10000u + dec4((uint32_t)(al >> 32));
+        const uint32_t v = len == 9 ? v8 * 10u + (c9 - '0') : v8;
+        lbad = lbad | (is_col & dig_bad) | (is_sub & (len != 2)) | ((is_ins | is_del) & (len < 1));
+        const int n_op = is_col ? (int)v : (is_sub ? 1 : max(len, 0));
         qb[t] = q_a;
-        if (ty == PW_OP_MATCH) {
-          // 1..9 digits: checked and converted in SIMD (8 as two 4-digit halves, then the 9th)
-          const uint64_t d = (uint64_t)(lo ^ 0x30303030u) | (uint64_t)(hi ^ 0x30303030u) << 32;
-          const uint32_t dg_lo = bytes_digit(lo), dg_hi = bytes_digit(hi);
-          const uint64_t need = len >= 8 ? 0x8080808080808080ull : (0x8080808080808080ull & ((1ull << (8 * len)) - 1ull));
-          const uint64_t have_d = (uint64_t)dg_lo | (uint64_t)dg_hi << 32;
-          if (len < 1 || len > 9 || (need & ~have_d) || (len == 9 && c9 - '0' > 9u)) lbad = true;
-          const int ln = min(max(len, 1), 8);
-          const uint64_t al = (d & (ln >= 8 ? ~0ull : ((1ull << (8 * ln)) - 1ull))) << (8 * (8 - ln));  // right-aligned
-          const uint32_t v8 = dec4((uint32_t)al) * 10000u + dec4((uint32_t)(al >> 32));
-          const uint32_t v = len == 9 ? v8 * 10u + (c9 - '0') : v8;
-          qn[t] = (int)v;
-          q_a += (int)v;
-          t_a += (int)v;
-          if (v > 0) {
-            opw[t] = PW_OP(PW_OP_MATCH, v);
-            cnt += 1u;
-          }
-        } else if (ty == PW_OP_SUB) {
-          if (len != 2) lbad = true;  // (any two characters, as the host packer takes them)
-          qn[t] = 0;
-          q_a += 1;
-          t_a += 1;
-          opw[t] = PW_OP(PW_OP_SUB, 1u);
-          cnt += 1u | 1u << 10 | 1u << 20;
-        } else {
-          if (len < 1) lbad = true;
-          qn[t] = ty == PW_OP_DEL ? len : 0;
-          if (ty == PW_OP_INS) t_a += len;
-          else q_a += len;
-          opw[t] = PW_OP((uint32_t)ty, (uint32_t)max(len, 0));
-          cnt += 1u | 1u << 10;
-        }
+        qn[t] = is_sub ? 0 : n_op;
+        q_a += (is_col || is_sub || is_del) ? n_op : 0;
+        t_a += (is_col || is_sub || is_ins) ? n_op : 0;
+        emit[t] = valid && (!is_col || v > 0);
+        opw[t] = PW_OP((uint32_t)(kind[t] & 3), (uint32_t)n_op);
+        cnt += (emit[t] ? 1u : 0u) | (valid && !is_col ? 1u << 10 : 0u) | (is_sub ? 1u << 20 : 0u);
       }
       // per character: its governing op (this lane's last start at or before it, else the last
       // one below the lane) -> literal ('*' pair, '-' bases) or letter required ('+' / '-')
-      const int klast = kind[ns >= 2 ? 1 : 0];
+      const int klast = sm1 ? kind[1] : kind[0];
       const uint32_t key_own = sm ? ((uint32_t)(4 * lane + 31 - __builtin_clz(sm)) << 2 | (uint32_t)(klast & 3)) + 1u : 0u;
       const uint32_t key_below = wave_shr1(dpp_max_incl(key_own));
+      const int g_below = (int)((key_below - 1u) >> 2), ty_below = key_below ? (int)((key_below - 1u) & 3u) : -1;
+      const int j0 = __builtin_ctz(sm | 16u), j1 = __builtin_ctz(sm1 | 16u);  // (4: none)
       uint32_t litm = 0;  // literal characters of this lane (bit j)
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int i = 4 * lane + j;
-        if (i >= lim || ((sm >> j) & 1u)) continue;
-        const uint32_t own = sm & ((1u << j) - 1u);
-        int g, ty;
-        if (own) {
-          const int jj = 31 - __builtin_clz(own);
-          g = 4 * lane + jj;
-          ty = (jj == __builtin_ctz(sm)) ? kind[0] : kind[1];
-        } else {
-          g = key_below ? (int)((key_below - 1u) >> 2) : -1;
-          ty = key_below ? (int)((key_below - 1u) & 3u) : -1;
-        }
+        const bool in = i < lim && !((sm >> j) & 1u);
+        // governing start: the lane's second start if before j, else its first, else the one below
+        const int g = j1 < j ? 4 * lane + j1 : (j0 < j ? 4 * lane + j0 : g_below);
+        const int ty = j1 < j ? kind[1] : (j0 < j ? kind[0] : ty_below);
         const bool letter = ((m_alp >> (8 * j + 7)) & 1u) != 0;
-        if ((ty == PW_OP_INS || ty == PW_OP_DEL) && !letter) lbad = true;
-        if (ty == PW_OP_INS || (ty == PW_OP_SUB && i - g - 1 < 2)) litm |= 1u << j;
+        lbad = lbad | (in & ((ty == PW_OP_INS) | (ty == PW_OP_DEL)) & !letter);
+        litm |= (in && (ty == PW_OP_INS || (ty == PW_OP_SUB && i - g - 1 < 2))) ? 1u << j : 0u;
       }
       // exclusive prefixes over the lanes (ops and characters are in lane order)
       const uint32_t nlit = (uint32_t)__popc(litm);
@@ -253,33 +257,28 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       const int q0 = qpos + iq - q_a;
 #pragma unroll
       for (int t = 0; t < 2; t++) {
-        if (kind[t] < 0) continue;
         const int qp = off + q0 + qb[t];
-        if (kind[t] == PW_OP_SUB) {
-          if (qp < 0 || qp > ql) lbad = true;
-        } else if (kind[t] != PW_OP_INS) {
-          if (qp < 0 || (int64_t)qp + qn[t] > ql) lbad = true;
-        }
+        const bool chk = kind[t] == PW_OP_MATCH || kind[t] == PW_OP_SUB || kind[t] == PW_OP_DEL;
+        lbad = lbad | (chk & ((qp < 0) | ((int64_t)qp + qn[t] > ql)));
       }
       if (__ballot(lbad) || !starts || (!last_win && last_start == 0)) {
         bad = true;  // (one op filling a window also lands here)
-        break;
+        return false;
       }
-      // op words and literal bytes at their places
-      uint32_t op_i = nops + ((ic - cnt) & 0x3FFu);
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-        if (opw[t]) ops[base + op_i++] = opw[t];
-      const uint32_t lp0 = nlits + il - nlit;
+      // op words and literal bytes at their places (32-bit offsets from the record's bases)
+      const uint32_t op_i = nops + ((ic - cnt) & 0x3FFu);
+      if (emit[0]) ops_r[op_i] = opw[0];
+      if (emit[1]) ops_r[op_i + (emit[0] ? 1u : 0u)] = opw[1];
       const uint32_t u4 = up_bytes(c4);
-      uint32_t lp = lp0;
+      uint32_t lp = nlits + il - nlit;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        if (!((litm >> j) & 1u)) continue;
-        const uint32_t a = (u4 >> (8 * j)) & 0xFFu;
-        lits[base + lp++] = (uint8_t)a;
-        acgt = acgt && (a == 'A' || a == 'C' || a == 'G' || a == 'T');
+        if ((litm >> j) & 1u) lits_r[lp] = (uint8_t)(u4 >> (8 * j));
+        lp += (litm >> j) & 1u;
       }
+      // A/C/G/T literals: per byte of the upper-cased characters
+      const uint32_t m_acgt = bytes_eq(u4, 'A') | bytes_eq(u4, 'C') | bytes_eq(u4, 'G') | bytes_eq(u4, 'T');
+      acgt = acgt && (msb_bits(m_acgt) & litm) == litm;
       // ':' values up to 999,999,999: sums stay in range for queries below 2^31
       qpos += wave_last(iq);
       tpos += wave_last(it);
@@ -291,6 +290,14 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       bound += (uint64_t)kPkBoundIndel * ((ctot >> 10 & 0x3FFu) - nsub) + (uint64_t)kPkBoundSub * nsub;
       pos += (uint64_t)lim;
       __builtin_amdgcn_wave_barrier();
+      return true;
+    };
+    if (L > 0 && window(w0, w1)) {
+      while (pos < L) {  // (records longer than one window: their later windows load on the spot)
+        uint32_t d0, d1;
+        pk_words(text, base + pos, last, lane, d0, d1);
+        if (!window(d0, d1)) break;
+      }
     }
     const bool all_acgt = __ballot(!acgt) == 0;
     if (lane == 0) {
