@@ -24,8 +24,8 @@
 //                      32 packed 5-bit register counters — no scatter, no atomic per base.
 //                      (pw_msa_count stops here: with rows sharded over GPUs the partial counts are
 //                      summed by an all-reduce before the call)
-//   K4 call_columns:   bestChar of every column (pw_msa_call)
-//   K5 zero_scan:      first zero-coverage column in [mincol, maxcol] (ErrZeroCov, :1121-1131).
+//   K4 call_columns:   bestChar of every column (pw_msa_call) and the first zero-coverage column
+//                      in [mincol, maxcol] (ErrZeroCov, :1121-1131)
 // Column-closed form of bestChar: max count wins, ties resolved A<C<G<T; a tie between only N
 // and '-' gives '-' (glibc qsort of 6 elements is a stable merge sort).
 //
@@ -779,8 +779,10 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
   }
 }
 
-// bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage
+// bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage, and the
+// first such column in [mincol, maxcol] (ErrZeroCov, :1121-1131) into minmax[3]
 __global__ __launch_bounds__(256) void call_columns(const pw_msa_args A, int32_t lo, int32_t hi) {
+  const int zlo = A.minmax[0], zhi = A.minmax[1];
   for (int64_t c = lo + (int64_t)blockIdx.x * 256 + threadIdx.x; c < hi; c += (int64_t)gridDim.x * 256) {
     int v[6];
     const int32_t* src = A.counts + c * 6;
@@ -800,14 +802,8 @@ __global__ __launch_bounds__(256) void call_columns(const pw_msa_args A, int32_t
       if (bi == 4 && v[5] == m) best = '-';
     }
     A.consensus[c] = best;
+    if (best == 0 && c >= zlo && c <= zhi) atomicMin(&A.minmax[3], (int)c);
   }
-}
-
-// (columns [c_lo, c_hi) of the consensus are this call's: the whole layout, or a rank's range)
-__global__ __launch_bounds__(256) void zero_scan(const pw_msa_args A, int32_t c_lo, int32_t c_hi) {
-  const int lo = max(A.minmax[0], c_lo), hi = min(A.minmax[1], c_hi - 1);
-  for (int c = lo + blockIdx.x * 256 + threadIdx.x; c <= hi; c += gridDim.x * 256)
-    if (c >= 0 && c < A.n_cols && A.consensus[c] == 0) atomicMin(&A.minmax[3], c);
 }
 
 // ---------------------------------------------------------------- refineMSA (pw_msa_refine)
@@ -818,6 +814,7 @@ __device__ __forceinline__ bool cons_gap(const pw_msa_args& A, int lo, int hi, i
 // K6: consensus-gap columns per 2048-column tile
 __global__ __launch_bounds__(256) void gap_tiles(const pw_msa_args A, pw_msa_refine_args R) {
   __shared__ int part[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *R.cons_len = 0;  // (gap_scan sets it when maxcol is a column)
   const int lo = A.minmax[0], hi = A.minmax[1];
   const int c0 = blockIdx.x * kTileW;
   int n = 0;
@@ -1015,7 +1012,6 @@ extern "C" int pw_msa_call_cols(const pw_msa_args* a, int32_t col_lo, int32_t co
   if (counts_lo) b.counts = const_cast<int32_t*>(counts_lo) - (int64_t)col_lo * 6;  // column c at counts_lo[(c - lo) * 6]
   const uint64_t nb = ((uint64_t)(col_hi - col_lo) + 255) / 256;
   hipLaunchKernelGGL(pw::call_columns, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, s, b, col_lo, col_hi);
-  hipLaunchKernelGGL(pw::zero_scan, dim3(256), dim3(256), 0, s, b, col_lo, col_hi);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
@@ -1035,7 +1031,6 @@ extern "C" int pw_msa_refine(const pw_msa_args* a, const pw_msa_refine_args* r, 
   if (!msa_args_ok(a) || !r || !r->gap_prefix || !r->tile_gaps || !r->cons_out || !r->cons_len) return PW_E_ARG;
   if (r->remove_gaps && (!r->row_offset || !r->ofs_out || !r->offset_out || !r->numgaps_out)) return PW_E_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(r->cons_len, 0, sizeof(int32_t), s) != hipSuccess) return PW_E_HIP;
   const unsigned ntiles = (unsigned)pw_msa_refine_tiles(a->n_cols);
   hipLaunchKernelGGL(pw::gap_tiles, dim3(ntiles), dim3(256), 0, s, *a, *r);
   hipLaunchKernelGGL(pw::gap_scan, dim3(ntiles), dim3(256), 0, s, *a, *r);
