@@ -462,11 +462,12 @@ struct RowA {
   int rs;
 };
 __device__ __forceinline__ uint32_t load_a(const pw_msa_args& A, uint32_t r, int lane) {
+  // (three loads from uniform bases with small lane offsets, then a select: no per-lane pointers)
   const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
-  const uint32_t* p = reinterpret_cast<const uint32_t*>(A.col0 + rr);
-  if (lane < 4) p = reinterpret_cast<const uint32_t*>(A.slot_base + rr) + lane;
-  else if (lane < 6) p = reinterpret_cast<const uint32_t*>(A.row_off + rr) + (lane - 4);
-  return *p;
+  const uint32_t x = reinterpret_cast<const uint32_t*>(A.slot_base + rr)[lane & 3];
+  const uint32_t y = reinterpret_cast<const uint32_t*>(A.row_off + rr)[lane & 1];
+  const uint32_t z = (uint32_t)A.col0[rr];
+  return lane < 4 ? x : (lane < 6 ? y : z);
 }
 __device__ __forceinline__ RowA get_a(uint32_t v) {
   RowA a;
@@ -484,8 +485,9 @@ __device__ __forceinline__ uint32_t load_b(const pw_msa_args& A, const int32_t* 
   const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
   int64_t idx = (int64_t)(c0 >> 11) - (int64_t)(a.rs >> 11);
   idx = idx < 0 ? 0 : (idx > a.sbn - a.sb - 1 ? a.sbn - a.sb - 1 : idx);
-  const int32_t* p = lane < 8 ? rinfo + kRowInfo * rr + lane : tstart + 2 * (a.sb + idx) + (lane & 1);
-  return (uint32_t)*p;
+  const uint32_t x = (uint32_t)(rinfo + kRowInfo * rr)[lane & 7];
+  const uint32_t y = (uint32_t)(tstart + 2 * (a.sb + idx))[lane & 1];
+  return lane < 8 ? x : y;
 }
 __device__ __forceinline__ uint32_t rd(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 // the tile's first chunk and first base for this row (kt = -1: not in the table, search)
@@ -527,10 +529,12 @@ __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt
   const int nch = (int)(rd(b, 5) & ~kNoTable);
   const int len = (int)rd(b, 4);
   kt = min(max(kt, 0), nch);  // (a row that does not reach the tile reads a stale entry: clamped)
-  const int64_t sb = a.sb;
-  c.ckv = ckpt[sb + min(kt + lane, nch)];
+  // (uniform row bases, 32-bit lane offsets)
+  const int32_t* ck_r = ckpt + a.sb;
+  const uint32_t* ru_r = runs + (uint64_t)a.sb * kRunCap;
+  c.ckv = ck_r[min(kt + lane, nch)];
 #pragma unroll
-  for (int h = 0; h < 3; h++) c.gv[h] = runs[(sb + min(kt + (lane >> 4) + 4 * h, nch)) * kRunCap + (lane & 15)];
+  for (int h = 0; h < 3; h++) c.gv[h] = ru_r[min(kt + (lane >> 4) + 4 * h, nch) * kRunCap + (lane & 15)];
   load_win(A, a.roff, len, ib, lane, c.w0, c.w1, c.w2);
 }
 __device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
