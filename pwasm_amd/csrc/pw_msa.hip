@@ -103,13 +103,15 @@ __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* s
 
 // K1: per 256-base chunk, sum of (1 + max(ofs, 0)) and its gap runs.  A run is the gap before a
 // base with ofs > 0 (~1 % of bases in an assembly layout): entry = (column offset of the run in
-// the chunk, from the chunk's checkpoint) << 16 | length, in layout order, at most kRunCap per
-// chunk, 0 = unused; kRunOverflow in entry 0 when a chunk has more runs or its columns pass 16 bits
+// the chunk, from the chunk's checkpoint) << 6 | length, 16 bits, in layout order, at most kRunCap
+// per chunk, 0 = unused; kRunOverflow in entry 0 when a chunk has more runs, a run longer than 63
+// or more than kRunCols columns
 // (K2 / K3 then read that chunk's ofs).  A wavefront takes 4 consecutive slots at a time, 16 lanes
 // per slot, 16 bases per lane (two 16-byte loads when the row starts 8-base aligned); the next
 // group's loads are issued before this group is reduced.
 constexpr int kRunCap = 16;  // (one per lane of the chunk's 16; > 16 runs in 256 bases: ~1e-7 at 1 % gaps)
-constexpr uint32_t kRunOverflow = 0xFFFFFFFFu;
+constexpr uint32_t kRunOverflow = 0xFFFFu;
+constexpr int kRunCols = 1000;  // (so no real entry is kRunOverflow)
 // K1's inputs per lane: the slot's descriptor two groups ahead, its 16 gaps one group ahead
 struct SumPre {
   v4u q0, q1;
@@ -140,7 +142,7 @@ __device__ __forceinline__ uint32_t row16_scan_incl(uint32_t v) {  // inclusive 
   return v;
 }
 __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const uint64_t* sdesc,
-                                                      uint32_t* runs) {
+                                                      uint16_t* runs) {
   const int lane = threadIdx.x & 63, sub = lane & 15;
   const uint64_t ng = (A.n_slots + 3) / 4;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
@@ -173,18 +175,23 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
       s += lo + hi;
       pm |= (uint32_t)min(lo, 1) << (2 * d) | (uint32_t)min(hi, 1) << (2 * d + 1);
     }
+    int big = 0;  // a gap longer than a 6-bit run length
+#pragma unroll
+    for (int d = 0; d < 8; d++) big |= ((int)(int16_t)(w[d] & 0xFFFFu) > 63) | ((int)(int16_t)(w[d] >> 16) > 63);
     const int n = __popc(pm);
-    const uint32_t is = row16_scan_incl((uint32_t)s), in = row16_scan_incl((uint32_t)n), iv = row16_scan_incl((uint32_t)nv);
-    const int ts = __shfl((int)is, lane | 15, 64), tn = __shfl((int)in, lane | 15, 64), tv = __shfl((int)iv, lane | 15, 64);
+    const uint32_t is = row16_scan_incl((uint32_t)s), in = row16_scan_incl((uint32_t)n | (uint32_t)big << 8),
+                   iv = row16_scan_incl((uint32_t)nv);
+    const int ts = __shfl((int)is, lane | 15, 64), tnb = __shfl((int)in, lane | 15, 64), tv = __shfl((int)iv, lane | 15, 64);
+    const int tn = tnb & 0xFF;
     const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
     if (c < A.n_slots) {
       if (sub == 0) chunk_sum[c] = tv + ts;
-      uint32_t* rl = runs + c * kRunCap;
-      if (tn > kRunCap || tv + ts > 0xFFFF) {
-        if (sub == 0) rl[0] = kRunOverflow;
+      uint16_t* rl = runs + c * kRunCap;
+      if (tn > kRunCap || (tnb >> 8) || tv + ts > kRunCols) {
+        if (sub == 0) rl[0] = (uint16_t)kRunOverflow;
       } else {
-        if (sub >= tn) rl[sub] = 0u;
-        int slot = (int)in - n;
+        if (sub >= tn) rl[sub] = 0;
+        int slot = (int)(in & 0xFFu) - n;
         int col = 16 * sub + ((int)is - s);  // column offset of this lane's first base's gap run
         int prev = 0;                        // base index (in the lane) the column offset refers to
         while (pm) {                         // (~0.15 runs per lane)
@@ -196,7 +203,7 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
           const uint32_t gg = (t & 1) ? dw >> 16 : dw & 0xFFFFu;
           col += t - prev;
           prev = t;
-          rl[slot++] = (uint32_t)col << 16 | gg;
+          rl[slot++] = (uint16_t)((uint32_t)col << 6 | gg);
           col += (int)gg;
         }
       }
@@ -222,13 +229,15 @@ constexpr int kCntW = 2048;  // K3 tile width
 struct Runs {
   uint32_t v[kRunCap];
 };
-__device__ __forceinline__ Runs load_runs(const uint32_t* rl) {  // (rl 16-byte aligned)
+__device__ __forceinline__ Runs load_runs(const uint16_t* rl) {  // (rl 16-byte aligned: two 16-byte loads)
   Runs R;
   const v4u* p = reinterpret_cast<const v4u*>(rl);
 #pragma unroll
-  for (int e = 0; e < kRunCap / 4; e++) {
+  for (int e = 0; e < kRunCap / 8; e++) {
     const v4u v = p[e];
-    R.v[4 * e] = v.x, R.v[4 * e + 1] = v.y, R.v[4 * e + 2] = v.z, R.v[4 * e + 3] = v.w;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++) R.v[8 * e + 2 * q] = d[q] & 0xFFFFu, R.v[8 * e + 2 * q + 1] = d[q] >> 16;
   }
   return R;
 }
@@ -240,7 +249,7 @@ __device__ __forceinline__ int first_base_at(const pw_msa_args& A, const Runs& R
 #pragma unroll
     for (int e = 0; e < kRunCap; e++) {
       const uint32_t v = R.v[e];
-      const int co = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
+      const int co = (int)(v >> 6), gg = (int)(v & 63u);
       if (ib < 0 && v != 0 && x >= co) {
         if (x < co + gg) ib = co - G;  // inside the run: the base after it
         else G += gg;
@@ -276,7 +285,7 @@ __device__ __forceinline__ int base_col(const pw_msa_args& A, const Runs& R, uin
 #pragma unroll
     for (int e = 0; e < kRunCap; e++) {
       const uint32_t v = R.v[e];
-      const int co = (int)(v >> 16), gg = (int)(v & 0xFFFFu);
+      const int co = (int)(v >> 6), gg = (int)(v & 63u);
       const int idx = co - G;  // the base this run precedes
       if (!done && v != 0 && (run_start ? idx < i : idx <= i)) G += gg;
       else done = true;
@@ -302,7 +311,7 @@ constexpr int kRowInfo = 8;  // int32 words per row record
 constexpr uint32_t kNoTable = 0x80000000u;
 constexpr int kPfxUnroll = 4;  // chunk sums a thread keeps in registers (rows of <= 4096 chunks)
 __global__ __launch_bounds__(1024) void row_prefix(const pw_msa_args A, const int32_t* chunk_sum, int32_t* ckpt,
-                                                   int32_t* rinfo, const uint32_t* runs, int32_t* tstart) {
+                                                   int32_t* rinfo, const uint16_t* runs, int32_t* tstart) {
   __shared__ int wsum[16];
   __shared__ uint32_t notab;
   const int64_t* chunk_base = A.slot_base;
@@ -519,10 +528,10 @@ __device__ __forceinline__ void load_win(const pw_msa_args& A, uint64_t roff, in
 }
 struct RowC {  // 1 row ahead
   int ckv;
-  uint32_t gv[3];  // runs of chunks kt + (lane >> 4) + 4h, entry lane & 15 (h = 2: lanes 0-15)
+  uint32_t gv[2];  // runs (two per dword) of chunks kt + (lane >> 3) (h = 0) and kt + 8 (h = 1, lanes 0-7)
   v4u w0, w1, w2;
 };
-__device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint32_t* runs, const RowA& a,
+__device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint16_t* runs, const RowA& a,
                                        uint32_t b, int c0, int lane, RowC& c) {
   int kt, ib;
   tile_start(a, b, c0, kt, ib);
@@ -531,10 +540,10 @@ __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt
   kt = min(max(kt, 0), nch);  // (a row that does not reach the tile reads a stale entry: clamped)
   // (uniform row bases, 32-bit lane offsets)
   const int32_t* ck_r = ckpt + a.sb;
-  const uint32_t* ru_r = runs + (uint64_t)a.sb * kRunCap;
+  const uint32_t* ru_r = reinterpret_cast<const uint32_t*>(runs + (uint64_t)a.sb * kRunCap);
   c.ckv = ck_r[min(kt + lane, nch)];
-#pragma unroll
-  for (int h = 0; h < 3; h++) c.gv[h] = ru_r[min(kt + (lane >> 4) + 4 * h, nch) * kRunCap + (lane & 15)];
+  c.gv[0] = ru_r[min(kt + (lane >> 3), nch) * (kRunCap / 2) + (lane & 7)];
+  c.gv[1] = ru_r[min(kt + 8, nch) * (kRunCap / 2) + (lane & 7)];
   load_win(A, a.roff, len, ib, lane, c.w0, c.w1, c.w2);
 }
 __device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
@@ -605,7 +614,7 @@ __device__ int slow_bitmap(const pw_msa_args& A, const int32_t* ckpt, int64_t sb
   return ib == INT_MAX ? len : ib;
 }
 __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_args A, const int32_t* __restrict__ ckpt,
-                                                              const uint32_t* __restrict__ runs,
+                                                              const uint16_t* __restrict__ runs,
                                                               const int32_t* __restrict__ rinfo,
                                                               const int32_t* __restrict__ tstart) {
   __shared__ __attribute__((aligned(16))) TileLds L;
@@ -667,7 +676,6 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
       pin(cc.ckv);
       pin(cc.gv[0]);
       pin(cc.gv[1]);
-      pin(cc.gv[2]);
       const int elo = (int)rd(bv1, 0), ehi = (int)rd(bv1, 1);
       const int a = max(elo, c0), z = min(ehi, c1 - 1);  // counted columns of this row here
       if (a <= z) {
@@ -682,21 +690,21 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         // gap bitmap: the columns outside [rs, re), then the runs of the batch's chunks
         bm[lane] = outside_mask(lane, rs - c0, re - c0);
         // the batch's chunks kt .. kt + 8 (chunk kt holds c0; each later one spans >= 256 columns)
-        bool cv[3], ovl = false;
+        bool cv[2], ovl = false;
 #pragma unroll
-        for (int h = 0; h < 3; h++) {
-          cv[h] = kt >= 0 && kt + (lane >> 4) + 4 * h < nch && (h < 2 || lane < 16);
-          ovl = ovl || (cv[h] && (lane & 15) == 0 && cc.gv[h] == kRunOverflow);
+        for (int h = 0; h < 2; h++) {
+          cv[h] = kt >= 0 && (h == 0 ? kt + (lane >> 3) < nch : (kt + 8 < nch && lane < 8));
+          ovl = ovl || (cv[h] && (lane & 7) == 0 && (cc.gv[h] & 0xFFFFu) == kRunOverflow);
         }
         const bool ovf = kt < 0 || __ballot(ovl) != 0;
         wave_sync();
         if (!ovf) {
 #pragma unroll
-          for (int h = 0; h < 3; h++) {
-            const uint32_t v = cv[h] ? cc.gv[h] : 0u;
-            const int ck = __shfl(cc.ckv, (lane >> 4) + 4 * h, 64);
+          for (int h = 0; h < 4; h++) {  // (h >> 1: which dword, h & 1: which half)
+            const uint32_t v = cv[h >> 1] ? (cc.gv[h >> 1] >> (16 * (h & 1))) & 0xFFFFu : 0u;
+            const int ck = (h >> 1) == 0 ? __shfl(cc.ckv, lane >> 3, 64) : __builtin_amdgcn_readlane(cc.ckv, 8);
             if (v != 0u) {
-              const int s = max(ck + (int)(v >> 16) - c0, 0), e = min(ck + (int)(v >> 16) + (int)(v & 0xFFFFu) - c0, kCntW);
+              const int s = max(ck + (int)(v >> 6) - c0, 0), e = min(ck + (int)(v >> 6) + (int)(v & 63u) - c0, kCntW);
               for (int x = s; x < e; x = (x | 31) + 1) {
                 const int xe = min(e, (x | 31) + 1);
                 const uint32_t m = (xe - x >= 32 ? 0xFFFFFFFFu : ((1u << (xe - x)) - 1u)) << (x & 31);
@@ -958,7 +966,7 @@ __global__ __launch_bounds__(64) void row_finish(const pw_msa_args A, pw_msa_ref
 // scratch word of the row records (16-byte aligned: K3 reads them as uint4)
 // scratch words: chunk sums | checkpoints | slot -> row | runs (kRunCap per slot) | tile starts (2 per slot) | row records
 inline uint64_t runs_word(uint64_t n_slots) { return (3 * n_slots + 3) & ~(uint64_t)3; }  // (16-byte aligned)
-inline uint64_t tstart_word(uint64_t n_slots) { return runs_word(n_slots) + (uint64_t)kRunCap * n_slots; }
+inline uint64_t tstart_word(uint64_t n_slots) { return runs_word(n_slots) + (uint64_t)kRunCap / 2 * n_slots; }
 inline uint64_t rinfo_word(uint64_t n_slots) { return (tstart_word(n_slots) + 2 * n_slots + 3) & ~(uint64_t)3; }
 
 }  // namespace pw
@@ -991,7 +999,7 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   int32_t* chunk_sum = a->scratch;
   int32_t* ckpt = a->scratch + a->n_slots;
   int32_t* slot_row = a->scratch + 2 * a->n_slots;
-  uint32_t* runs = reinterpret_cast<uint32_t*>(a->scratch + pw::runs_word(a->n_slots));
+  uint16_t* runs = reinterpret_cast<uint16_t*>(a->scratch + pw::runs_word(a->n_slots));
   int32_t* tstart = a->scratch + pw::tstart_word(a->n_slots);
   int32_t* rinfo = a->scratch + pw::rinfo_word(a->n_slots);
   uint64_t* sdesc = reinterpret_cast<uint64_t*>(tstart);  // (K1's input; K2 then writes the tile starts there)

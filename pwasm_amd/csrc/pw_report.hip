@@ -2204,19 +2204,25 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
   __shared__ __attribute__((aligned(16))) FixLane fl[256];
   __shared__ uint64_t mk[kWaves][kWave];  // the long-line masks of the wave's 64 chunks
   __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts
+  // workgroups [fix_wg, gridDim.x): the per-record results (finalize_kernel's work: one launch
+  // less per pass; they do not depend on the long lines' bytes), one record per thread, beside
+  // the long lines of workgroups [0, fix_wg) — the two dependent-load chains run side by side
+  const uint32_t fix_wg = gridDim.x - (A.n_alns + 255) / 256;
+  if (blockIdx.x >= fix_wg) {  // (the whole workgroup: before any barrier)
+    const uint32_t ai = (blockIdx.x - fix_wg) * 256 + threadIdx.x;
+    if (ai < A.n_alns) finalize_record(A, W, ai);
+    return;
+  }
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, 256);
   __syncthreads();
   LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x];
   const bool skip = A.skip_codan != 0;
-  // the per-record results first (finalize_kernel's work: one launch less per pass; they do not
-  // depend on the long lines' bytes)
-  for (uint32_t ai = blockIdx.x * 256 + threadIdx.x; ai < A.n_alns; ai += gridDim.x * 256) finalize_record(A, W, ai);
   if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten
   // a wave takes 64 chunks at a time and spreads their long lines over its lanes (line j of the
   // group -> lane j % 64): the chunk of line j is the last one whose prefix is <= j
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  const uint64_t nwt = (uint64_t)gridDim.x * kWaves;
+  const uint64_t nwt = (uint64_t)fix_wg * kWaves;
   for (uint64_t c0 = ((uint64_t)blockIdx.x * kWaves + wv) * kWave; c0 < W.n_chunks; c0 += nwt * kWave) {
     const uint64_t cl = c0 + (uint64_t)lane;
     const uint64_t m = cl < W.n_chunks ? W.lmask[cl] : 0ull;
@@ -2480,10 +2486,12 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   pw::Work W;
   pw::work_layout(static_cast<uint8_t*>(args->workspace), args->n_ev_slots, args->n_alns, &W);
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;  // counters
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
   const bool planned = args->max_rec_ops == 0 || args->max_rec_ops > (uint32_t)pw::kBlkOps;
+  // the counters (a memset launch: without it index_kernel starts at once and the next-stop table
+  // built beside it on a side stream slows it down — index 127 -> 143 us, table 29 -> 66 us)
+  if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;
   // (two rounds at 5 waves/SIMD; sweep: 16 -> 10 per CU saved ~10 us of index + tctx); with long
   // records the blocks of 1.. are spread over the full grid whatever the record count
   if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;
@@ -2503,7 +2511,9 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     // (render is the first kernel that reads next_stop)
     if (next_stop_ready && hipStreamWaitEvent(st, (hipEvent_t)next_stop_ready, 0) != hipSuccess) return PW_E_HIP;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0, st, *args, W);  // (+ finalize)
+    // (+ finalize: ncu workgroups for the long lines, then one thread per record)
+    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,
+                       st, *args, W);
   } else {
     hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);
   }
