@@ -453,6 +453,15 @@ __device__ __forceinline__ uint32_t bin_codes5(uint32_t s4) {
   const uint32_t m = (nz << 1) - (nz >> 7);                                  // 0xFF per such byte
   return (m & 0x14141414u) | (~m & code);
 }
+// the same codes when every byte is one of A C T G H * - N (the one character of each h): the
+// byte's h's character XOR the byte goes to d (nonzero: redo with bin_codes5)
+__device__ __forceinline__ uint32_t bin_codes_fast(uint32_t s4, uint32_t& d) {
+  const uint32_t h = (s4 >> 1) & 0x07070707u;
+  const uint32_t code = __builtin_amdgcn_perm(0x14191914u, 0x0A0F0500u, h);  // 0 5 15 10 | 20 25 25 20
+  const uint32_t ex = __builtin_amdgcn_perm(0x4E2D2A48u, 0x47544341u, h);    // A C T G | H * - N
+  d = s4 ^ ex;
+  return code;
+}
 // bits of columns [32 lane, 32 lane + 32) that are < lo or >= hi (tile-relative)
 __device__ __forceinline__ uint32_t outside_mask(int lane, int lo, int hi) {
   const int a = min(max(lo - 32 * lane, 0), 32), b = min(max(hi - 32 * lane, 0), 32);
@@ -463,44 +472,53 @@ __device__ __forceinline__ uint32_t outside_mask(int lane, int lo, int hi) {
 // Per-row values loaded ahead are spread over the lanes of one VGPR (a lane per dword, read
 // back with readlane): vector loads, so their waits are vmcnt waits in issue order, not lgkmcnt
 // waits that every LDS wait of the row body would share.
-//   RowA (3 rows ahead), lanes 0-6: slot_base[r] (2), slot_base[r + 1] (2), row_off (2), col0
-//   RowB (2 rows ahead), lanes 0-7: the row record; lanes 8-9: its tile-start entry
+//   RowA (3 rows ahead): slot_base[r], slot_base[r + 1] (x, lanes 0-3), row_off (y, 0-1), col0 (z)
+//   RowB (2 rows ahead): the row record (x, lanes 0-7), its tile-start entry (y, lanes 0-1)
 struct RowA {
   int64_t sb, sbn;
   uint64_t roff;
   int rs;
 };
-__device__ __forceinline__ uint32_t load_a(const pw_msa_args& A, uint32_t r, int lane) {
-  // (three loads from uniform bases with small lane offsets, then a select: no per-lane pointers)
+// (no select between the loads: a select would wait for all of them where it is computed, and
+// hipcc turns a lane select of loads into branches that wait vmcnt(0) — every later prefetch then
+// waits too.  Each value stays in the VGPR it was loaded into; readlane picks lanes at use.)
+struct AV {
+  uint32_t x, y, z;
+};
+struct BV {
+  uint32_t x, y;
+};
+__device__ __forceinline__ AV load_a(const pw_msa_args& A, uint32_t r, int lane) {
+  // (three loads from uniform bases with small lane offsets: no per-lane pointers)
   const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
-  const uint32_t x = reinterpret_cast<const uint32_t*>(A.slot_base + rr)[lane & 3];
-  const uint32_t y = reinterpret_cast<const uint32_t*>(A.row_off + rr)[lane & 1];
-  const uint32_t z = (uint32_t)A.col0[rr];
-  return lane < 4 ? x : (lane < 6 ? y : z);
+  AV v;
+  v.x = reinterpret_cast<const uint32_t*>(A.slot_base + rr)[lane & 3];
+  v.y = reinterpret_cast<const uint32_t*>(A.row_off + rr)[lane & 1];
+  v.z = (uint32_t)A.col0[rr];
+  return v;
 }
-__device__ __forceinline__ RowA get_a(uint32_t v) {
+__device__ __forceinline__ uint32_t rd(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ RowA get_a(const AV& v) {
   RowA a;
-  a.sb = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 0) |
-                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 1) << 32);
-  a.sbn = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 2) |
-                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 3) << 32);
-  a.roff = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 4) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)v, 5) << 32;
-  a.rs = __builtin_amdgcn_readlane((int)v, 6);
+  a.sb = (int64_t)((uint64_t)rd(v.x, 0) | (uint64_t)rd(v.x, 1) << 32);
+  a.sbn = (int64_t)((uint64_t)rd(v.x, 2) | (uint64_t)rd(v.x, 3) << 32);
+  a.roff = (uint64_t)rd(v.y, 0) | (uint64_t)rd(v.y, 1) << 32;
+  a.rs = (int)rd(v.z, 0);
   return a;
 }
-__device__ __forceinline__ uint32_t load_b(const pw_msa_args& A, const int32_t* rinfo, const int32_t* tstart, uint32_t r,
-                                           const RowA& a, int c0, int lane) {
+__device__ __forceinline__ BV load_b(const pw_msa_args& A, const int32_t* rinfo, const int32_t* tstart, uint32_t r,
+                                     const RowA& a, int c0, int lane) {
   const uint64_t rr = r < A.n_rows ? r : A.n_rows - 1;
   int64_t idx = (int64_t)(c0 >> 11) - (int64_t)(a.rs >> 11);
   idx = idx < 0 ? 0 : (idx > a.sbn - a.sb - 1 ? a.sbn - a.sb - 1 : idx);
-  const uint32_t x = (uint32_t)(rinfo + kRowInfo * rr)[lane & 7];
-  const uint32_t y = (uint32_t)(tstart + 2 * (a.sb + idx))[lane & 1];
-  return lane < 8 ? x : y;
+  BV v;
+  v.x = (uint32_t)(rinfo + kRowInfo * rr)[lane & 7];
+  v.y = (uint32_t)(tstart + 2 * (a.sb + idx))[lane & 1];
+  return v;
 }
-__device__ __forceinline__ uint32_t rd(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-// the tile's first chunk and first base for this row (kt = -1: not in the table, search)
-__device__ __forceinline__ void tile_start(const RowA& a, uint32_t b, int c0, int& kt, int& ib) {
+// word l of the row record (0-7) or of its tile-start entry (8-9)
+__device__ __forceinline__ uint32_t rd(const BV& b, int l) { return l < 8 ? rd(b.x, l) : rd(b.y, l - 8); }
+__device__ __forceinline__ void tile_start(const RowA& a, const BV& b, int c0, int& kt, int& ib) {
   if (c0 <= a.rs) {
     kt = 0;
     ib = 0;
@@ -532,7 +550,7 @@ struct RowC {  // 1 row ahead
   v4u w0, w1, w2;
 };
 __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint16_t* runs, const RowA& a,
-                                       uint32_t b, int c0, int lane, RowC& c) {
+                                       const BV& b, int c0, int lane, RowC& c) {
   int kt, ib;
   tile_start(a, b, c0, kt, ib);
   const int nch = (int)(rd(b, 5) & ~kNoTable);
@@ -644,11 +662,11 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
   uint32_t r = wv;
   if (r < A.n_rows) {
     // prologue: rows r (A, B, C), r + W (A, B), r + 2W (A)
-    uint32_t av1 = load_a(A, r, lane0), av2 = load_a(A, r + W, lane0), av3 = load_a(A, r + 2 * W, lane0);
+    AV av1 = load_a(A, r, lane0), av2 = load_a(A, r + W, lane0), av3 = load_a(A, r + 2 * W, lane0);
     RowA a1 = get_a(av1);
-    uint32_t bv1 = load_b(A, rinfo, tstart, r, a1, c0, lane0);
+    BV bv1 = load_b(A, rinfo, tstart, r, a1, c0, lane0);
     RowA a2 = get_a(av2);
-    uint32_t bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane0);
+    BV bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane0);
     RowC cc;
     load_c(A, ckpt, runs, a1, bv1, c0, lane0, cc);
     for (;; r += W) {
@@ -671,8 +689,8 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
       RowC cn;
       load_c(A, ckpt, runs, a2, bv2, c0, lane, cn);
       const RowA a3 = get_a(av3);
-      const uint32_t bv3 = load_b(A, rinfo, tstart, r + 2 * W, a3, c0, lane);
-      const uint32_t av4 = load_a(A, r + 3 * W, lane);
+      const BV bv3 = load_b(A, rinfo, tstart, r + 2 * W, a3, c0, lane);
+      const AV av4 = load_a(A, r + 3 * W, lane);
       pin(cc.ckv);
       pin(cc.gv[0]);
       pin(cc.gv[1]);
@@ -738,9 +756,12 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         const uint32_t rb = rot ? __builtin_amdgcn_alignbit(bmv, bmv, 4u * (uint32_t)rot) : bmv;
         const int base0 = so + 4 * rot - __popc(__builtin_amdgcn_ubfe(bmv, 0, 4u * (uint32_t)rot));
         const int wrapc = 32 - pc, qwrap = 8 - rot;
-        auto groups = [&](auto edge_c) {
-          constexpr bool kEdge = decltype(edge_c)::value;
-          uint32_t rom = 0;
+        // the 8 groups' codes (fast classifier; a wave with another character redoes them with
+        // the general one), then the 32 counters
+        uint32_t codes[8];
+        auto groups = [&](auto edge_c, auto fast_c) {
+          constexpr bool kEdge = decltype(edge_c)::value, kFast = decltype(fast_c)::value;
+          uint32_t rom = 0, bad = 0;
           if constexpr (kEdge) {
             const uint32_t om = outside_mask(lane, a - c0, z - c0 + 1);
             rom = rot ? __builtin_amdgcn_alignbit(om, om, 4u * (uint32_t)rot) : om;
@@ -752,19 +773,30 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
             const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
             const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
             const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);
-            uint32_t codes = bin_codes5(e4);
-            if constexpr (kEdge) {
+            uint32_t d = 0;
+            uint32_t cq = kFast ? bin_codes_fast(e4, d) : bin_codes5(e4);
+            if constexpr (kEdge) {  // (columns outside the extent: code none, never "bad")
               const uint32_t on = (rom >> (4 * q)) & 15u;
               const uint32_t b1 = (on * 0x00204081u) & 0x01010101u;  // 4 bits -> 4 bytes
               const uint32_t bmask = (b1 << 8) - b1;
-              codes = (codes & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
+              cq = (cq & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
+              d &= ~bmask;
             }
-#pragma unroll
-            for (int j = 0; j < 4; j++) acc[4 * q + j] += 1u << ((codes >> (8 * j)) & 31u);
+            bad |= d;
+            codes[q] = cq;
           }
+          return bad;
         };
-        if (a > c0 || z < c1 - 1) groups(std::true_type{});  // the row's counted extent starts / ends here
-        else groups(std::false_type{});
+        const bool edge = a > c0 || z < c1 - 1;  // the row's counted extent starts / ends here
+        const uint32_t bad = edge ? groups(std::true_type{}, std::true_type{}) : groups(std::false_type{}, std::true_type{});
+        if (__ballot(bad != 0u)) {  // lower case, or a character outside A C G T N - * H
+          if (edge) groups(std::true_type{}, std::false_type{});
+          else groups(std::false_type{}, std::false_type{});
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+#pragma unroll
+          for (int j = 0; j < 4; j++) acc[4 * q + j] += 1u << ((codes[q] >> (8 * j)) & 31u);
         wave_sync();
       }
       a1 = a2;
