@@ -82,6 +82,13 @@ __device__ __forceinline__ int64_t vary(int64_t v) {
   return v;
 }
 
+// (orders a wave's LDS stores before its later LDS reads by other lanes)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // K0: the row of every slot (slot_row) and K1's chunk descriptor (sdesc: the chunk's first ofs
 // element | its base count << 48 | 16-byte aligned << 63), one workgroup per row, coalesced
 constexpr uint64_t kDescVec = 1ull << 63;
@@ -107,26 +114,32 @@ __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* s
 // per chunk, 0 = unused; kRunOverflow in entry 0 when a chunk has more runs, a run longer than 63
 // or more than kRunCols columns
 // (K2 / K3 then read that chunk's ofs).  A wavefront takes 4 consecutive slots at a time, 16 lanes
-// per slot, 16 bases per lane (two 16-byte loads when the row starts 8-base aligned); the next
-// group's loads are issued before this group is reduced.
+// per slot, 16 bases per lane (two 16-byte loads when the row starts 8-base aligned); the loads of
+// the next three groups are in flight while a group is reduced.
 constexpr int kRunCap = 16;  // (one per lane of the chunk's 16; > 16 runs in 256 bases: ~1e-7 at 1 % gaps)
 constexpr uint32_t kRunOverflow = 0xFFFFu;
 constexpr int kRunCols = 1000;  // (so no real entry is kRunOverflow)
-// K1's inputs per lane: the slot's descriptor two groups ahead, its 16 gaps one group ahead
+// K1's inputs per lane: the slot's descriptor four groups ahead, its 16 gaps three groups ahead
 struct SumPre {
   v4u q0, q1;
   uint64_t off;  // first ofs element of this lane's 16
   int nv;        // bases of this lane (0..16)
+  int tv;        // bases of the chunk
   bool vec;
 };
+// (the descriptor load is unconditional and its value is not touched until sums_load: a select
+// next to the load would make hipcc wait for it there)
 __device__ __forceinline__ uint64_t sums_desc(const pw_msa_args& A, const uint64_t* sdesc, uint64_t g, int lane) {
   const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
-  return c < A.n_slots ? sdesc[c] : sdesc[A.n_slots - 1] & ((1ull << 48) - 1);  // (past the end: no bases)
+  return sdesc[c < A.n_slots ? c : A.n_slots - 1];
 }
-__device__ __forceinline__ void sums_load(const pw_msa_args& A, uint64_t d, int lane, SumPre& p) {
+__device__ __forceinline__ void sums_load(const pw_msa_args& A, uint64_t d, uint64_t g, int lane, SumPre& p) {
   const int sub = lane & 15;
+  const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
+  if (c >= A.n_slots) d &= (1ull << 48) - 1;  // past the end: no bases
   p.off = (d & ((1ull << 48) - 1)) + 16ull * (uint64_t)sub;
-  p.nv = min(max((int)((d >> 48) & 0x1FFu) - 16 * sub, 0), 16);
+  p.tv = (int)((d >> 48) & 0x1FFu);
+  p.nv = min(max(p.tv - 16 * sub, 0), 16);
   p.vec = (d & kDescVec) && p.nv == 16;
   // (unconditional loads: a row tail or unaligned row reads the scratch instead and takes the
   // element path when consumed)
@@ -141,75 +154,115 @@ __device__ __forceinline__ uint32_t row16_scan_incl(uint32_t v) {  // inclusive 
   v += dpp_or_zero<0x118>(v);
   return v;
 }
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// one group of 4 chunks: the 16 gaps of this lane (two per dword, packed int16 math: per dword a
+// max, a dot2 into the sum, a min into the nonzero mask, a max into the "long gap" check).  The
+// chunk's run entries go to the wave's LDS strip (lr: 16 entries of this lane's chunk); returns the
+// chunk sum (valid in every lane of the chunk)
+__device__ __forceinline__ int sums_group(const pw_msa_args& A, const SumPre& cur, int lane, LDS uint16_t* lr) {
+  const int sub = lane & 15;
+  uint32_t w[8];  // 16 int16 gaps, two per dword
+  if (cur.vec) {
+    w[0] = cur.q0.x, w[1] = cur.q0.y, w[2] = cur.q0.z, w[3] = cur.q0.w;
+    w[4] = cur.q1.x, w[5] = cur.q1.y, w[6] = cur.q1.z, w[7] = cur.q1.w;
+  } else {  // row tail / unaligned row
+#pragma unroll
+    for (int d = 0; d < 8; d++) w[d] = 0;
+    for (int i = 0; i < cur.nv; i++) w[i >> 1] |= (uint32_t)(uint16_t)A.ofs[cur.off + i] << (16 * (i & 1));
+  }
+  const i16x2 zero = {0, 0};
+  const u16x2 one = {1, 1};
+  uint32_t s = 0, pmw = 0;
+  i16x2 bg = zero;
+#pragma unroll
+  for (int d = 0; d < 8; d++) {
+    const i16x2 v = __builtin_bit_cast(i16x2, w[d]);
+    const u16x2 m = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, zero));
+    s = __builtin_amdgcn_udot2(m, one, s, false);
+    pmw |= __builtin_bit_cast(uint32_t, __builtin_elementwise_min(m, one)) << d;  // element 2d: bit d, 2d + 1: 16 + d
+    bg = __builtin_elementwise_max(bg, v);
+  }
+  // interleave: bit t of pm = element t has a gap
+  uint32_t x = pmw;
+  x = (x | x << 4) & 0x0F0F0F0Fu;
+  x = (x | x << 2) & 0x33333333u;
+  x = (x | x << 1) & 0x55555555u;
+  uint32_t pm = (x & 0xFFFFu) | (x >> 15);
+  const int big = max((int)bg.x, (int)bg.y) > 63 ? 1 : 0;  // a gap longer than a 6-bit run length
+  const int n = __popc(pm);
+  const uint32_t is = row16_scan_incl(s), in = row16_scan_incl((uint32_t)n | (uint32_t)big << 8);
+  const int ts = __shfl((int)is, lane | 15, 64), tnb = __shfl((int)in, lane | 15, 64);
+  const int tn = tnb & 0xFF, tv = cur.tv;
+  const bool ovf = tn > kRunCap || (tnb >> 8) || tv + ts > kRunCols;
+  // entries [0, tn) from the lanes with runs, [tn, 16) zero, or kRunOverflow in entry 0 (the rest
+  // is then never read)
+  if (sub >= tn && !(ovf && sub == 0)) lr[sub] = 0;
+  if (ovf) {
+    if (sub == 0) lr[0] = (uint16_t)kRunOverflow;
+  } else {
+    int slot = (int)(in & 0xFFu) - n;
+    int col = 16 * sub + ((int)is - (int)s);  // column offset of this lane's first base's gap run
+    int prev = 0;                             // base index (in the lane) the column offset refers to
+    while (pm) {                              // (~0.15 runs per lane)
+      const int t = __builtin_ctz(pm);
+      pm &= pm - 1;
+      const int d = t >> 1;
+      const uint32_t dw = (d & 4) ? ((d & 2) ? ((d & 1) ? w[7] : w[6]) : ((d & 1) ? w[5] : w[4]))
+                                  : ((d & 2) ? ((d & 1) ? w[3] : w[2]) : ((d & 1) ? w[1] : w[0]));
+      const uint32_t gg = (t & 1) ? dw >> 16 : dw & 0xFFFFu;
+      col += t - prev;
+      prev = t;
+      lr[slot++] = (uint16_t)((uint32_t)col << 6 | gg);
+      col += (int)gg;
+    }
+  }
+  return tv + ts;
+}
 __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32_t* chunk_sum, const uint64_t* sdesc,
                                                       uint16_t* runs) {
-  const int lane = threadIdx.x & 63, sub = lane & 15;
+  __shared__ uint32_t lruns[4][4][kRunCap / 2];  // [wave][chunk of the group][entry pairs]
+  const int lane = threadIdx.x & 63, sub = lane & 15, wv = threadIdx.x >> 6;
+  LDS uint32_t* lr32 = (LDS uint32_t*)&lruns[wv][lane >> 4][0];
   const uint64_t ng = (A.n_slots + 3) / 4;
   const uint64_t nw = (uint64_t)gridDim.x * 4;
-  uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint64_t g = (uint64_t)blockIdx.x * 4 + (uint64_t)wv;
   if (g >= ng) return;
-  uint64_t dn = sums_desc(A, sdesc, g + nw, lane);
-  SumPre cur;
-  sums_load(A, sums_desc(A, sdesc, g, lane), lane, cur);
-  for (; g < ng; g += nw) {
-    SumPre nxt;
-    asm volatile("" : "+v"(dn));
-    sums_load(A, dn, lane, nxt);
-    dn = sums_desc(A, sdesc, g + 2 * nw, lane);
-    asm volatile("" : "+v"(cur.q0), "+v"(cur.q1));
-    uint32_t w[8];  // 16 int16 gaps, two per dword
-    if (cur.vec) {
-      w[0] = cur.q0.x, w[1] = cur.q0.y, w[2] = cur.q0.z, w[3] = cur.q0.w;
-      w[4] = cur.q1.x, w[5] = cur.q1.y, w[6] = cur.q1.z, w[7] = cur.q1.w;
-    } else {  // row tail / unaligned row
-#pragma unroll
-      for (int d = 0; d < 8; d++) w[d] = 0;
-      for (int i = 0; i < cur.nv; i++) w[i >> 1] |= (uint32_t)(uint16_t)A.ofs[cur.off + i] << (16 * (i & 1));
-    }
-    const int nv = cur.nv;
-    int s = 0;
-    uint32_t pm = 0;
-#pragma unroll
-    for (int d = 0; d < 8; d++) {
-      const int lo = max((int)(int16_t)(w[d] & 0xFFFFu), 0), hi = max((int)(int16_t)(w[d] >> 16), 0);
-      s += lo + hi;
-      pm |= (uint32_t)min(lo, 1) << (2 * d) | (uint32_t)min(hi, 1) << (2 * d + 1);
-    }
-    int big = 0;  // a gap longer than a 6-bit run length
-#pragma unroll
-    for (int d = 0; d < 8; d++) big |= ((int)(int16_t)(w[d] & 0xFFFFu) > 63) | ((int)(int16_t)(w[d] >> 16) > 63);
-    const int n = __popc(pm);
-    const uint32_t is = row16_scan_incl((uint32_t)s), in = row16_scan_incl((uint32_t)n | (uint32_t)big << 8),
-                   iv = row16_scan_incl((uint32_t)nv);
-    const int ts = __shfl((int)is, lane | 15, 64), tnb = __shfl((int)in, lane | 15, 64), tv = __shfl((int)iv, lane | 15, 64);
-    const int tn = tnb & 0xFF;
-    const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
-    if (c < A.n_slots) {
-      if (sub == 0) chunk_sum[c] = tv + ts;
-      uint16_t* rl = runs + c * kRunCap;
-      if (tn > kRunCap || (tnb >> 8) || tv + ts > kRunCols) {
-        if (sub == 0) rl[0] = (uint16_t)kRunOverflow;
-      } else {
-        if (sub >= tn) rl[sub] = 0;
-        int slot = (int)(in & 0xFFu) - n;
-        int col = 16 * sub + ((int)is - s);  // column offset of this lane's first base's gap run
-        int prev = 0;                        // base index (in the lane) the column offset refers to
-        while (pm) {                         // (~0.15 runs per lane)
-          const int t = __builtin_ctz(pm);
-          pm &= pm - 1;
-          const int d = t >> 1;
-          const uint32_t dw = (d & 4) ? ((d & 2) ? ((d & 1) ? w[7] : w[6]) : ((d & 1) ? w[5] : w[4]))
-                                      : ((d & 2) ? ((d & 1) ? w[3] : w[2]) : ((d & 1) ? w[1] : w[0]));
-          const uint32_t gg = (t & 1) ? dw >> 16 : dw & 0xFFFFu;
-          col += t - prev;
-          prev = t;
-          rl[slot++] = (uint16_t)((uint32_t)col << 6 | gg);
-          col += (int)gg;
-        }
-      }
-    }
-    cur = nxt;
+  // (pw_msa_count checks that 32 * n_slots fits a 32-bit offset)
+  const __amdgpu_buffer_rsrc_t rs_runs =
+      __builtin_amdgcn_make_buffer_rsrc(runs, (short)0, (int)((uint32_t)A.n_slots * (uint32_t)(2 * kRunCap)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_cs = __builtin_amdgcn_make_buffer_rsrc(chunk_sum, (short)0, (int)((uint32_t)A.n_slots * 4u), 0x00020000);
+  constexpr uint32_t kOut = 0xFFFFFFF0u;
+  // three groups' loads in flight (p0, p1, p2: unrolled by three, so no register copy waits for a
+  // load issued one group earlier), the descriptor of the group after them.  vmcnt counts stores
+  // too: a step issues its loads first and then a fixed two stores (chunk sum, run entries from the
+  // LDS strip), so a wait for a load never waits for a younger load behind a variable number of
+  // stores.
+  SumPre p0, p1;
+  sums_load(A, sums_desc(A, sdesc, g, lane), g, lane, p0);
+  sums_load(A, sums_desc(A, sdesc, g + nw, lane), g + nw, lane, p1);
+  uint64_t dn = sums_desc(A, sdesc, g + 2 * nw, lane);
+  auto step = [&](SumPre& p) {
+    asm volatile("" : "+v"(p.q0), "+v"(p.q1));
+    const int cs = sums_group(A, p, lane, (LDS uint16_t*)lr32);
+    const uint64_t dnn = sums_desc(A, sdesc, g + 3 * nw, lane);
+    asm volatile("" : "+v"(dn)::"memory");
+    sums_load(A, dn, g + 2 * nw, lane, p);
+    dn = dnn;
+    wave_sync();
+    const uint32_t rw = lr32[sub & 7];
+    const uint32_t c = (uint32_t)(g * 4) + (uint32_t)(lane >> 4);
+    __builtin_amdgcn_raw_buffer_store_b32(rw, rs_runs, sub < 8 ? c * (uint32_t)(2 * kRunCap) + 4u * (uint32_t)sub : kOut, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)cs, rs_cs, sub == 0 ? 4u * c : kOut, 0, 0);
+    wave_sync();
+    g += nw;
+  };
+  const uint64_t n_mine = (ng - g + nw - 1) / nw;
+  for (uint64_t k = 2; k <= n_mine; k += 2) {
+    step(p0);
+    step(p1);
   }
+  if (n_mine & 1) step(p0);
 }
 
 // K2: one 1024-thread workgroup per row: chunk checkpoints (column where chunk k's first gap run
@@ -568,11 +621,6 @@ __device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(v2u& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 __device__ __forceinline__ void cnt_flush(uint32_t (&acc)[32], LDS uint32_t* tab, int lane) {
   const int rot = (lane >> 2) & 7;
 #pragma unroll
@@ -1025,6 +1073,7 @@ static bool msa_args_ok(const pw_msa_args* a) {
 
 extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   if (!msa_args_ok(a)) return PW_E_ARG;
+  if (a->n_slots >= (1ull << 27)) return PW_E_ARG;  // (K1's 32-bit buffer offsets: < 34 G bases)
   hipStream_t s = (hipStream_t)stream;
   // scratch: chunk sums | checkpoints | slot -> row | gap runs (kRunCap per slot) | tile starts |
   // row records

@@ -273,6 +273,28 @@ def test_gapassem_synthetic(built, tmp_path, scale):
     assert ga_same(lay, tmp_path) == 0
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_gapassem_odd_characters(built, tmp_path, seed):
+    """tile_counts classifies A C G T N - * (and H) with a fast check and redoes a wave's groups
+    with the general bin rule (toupper, anything else N) when a byte is outside that set: rows over
+    several 2048-column tiles, some pure A/C/G/T/N, some with lower case, '*', '-' and other bytes."""
+    rng = random.Random(900 + seed)
+    rows = []
+    for r in range(24):
+        n = rng.randint(2000, 9000)
+        odd = r % 3 != 0
+        pool = "ACGTACGTACGTN" + ("acgtn*-RYxH." if odd else "")
+        seq = "".join(rng.choice(pool) if rng.random() < (0.05 if odd else 1.0) else rng.choice("ACGT")
+                      for _ in range(n))
+        ofs = [0] + [rng.choice([0] * 40 + [1, 2, 5, 70]) for _ in range(n - 1)]
+        rows.append((rng.randint(0, 6000), seq, ofs, rng.randint(0, 30), rng.randint(0, 30), r % 2))
+    rows[0] = (0, "".join(rng.choice("ACGT") for _ in range(20000)), [0] * 20000, 0, 0, 0)  # coverage
+    lay = tmp_path / "o.pwl"
+    write_pwl(lay, rows)
+    assert ga_same(lay, tmp_path, writers=False) == 0
+    assert ga_same(lay, tmp_path, ["--remove-gaps"], writers=False) == 0
+
+
 def test_gapassem_tile_boundaries(built, tmp_path):
     # rows long enough to cross several 2048-column tiles and 256-base chunks with gaps
     lay = tmp_path / "b.pwl"
