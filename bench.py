@@ -328,7 +328,8 @@ def main():
 
 def bench_gapassem(args, world, rank, dev_name):
     """BASELINE.json configs[4]: GapAssem consensus of one 200-row, ~1M-column layout (pwsynth
-    cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step = pw_msa_count on the
+    cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step on one GPU =
+    pw_msa_columns (count and bestChar in one pass) + pw_msa_refine; on N > 1 = pw_msa_count on the
     rank's rows + pw_msa_call_sharded (RCCL reduce-scatter of the [n_cols x 6] histograms by
     column range + bounds, bestChar of the rank's columns, all-gather of the consensus) +
     pw_msa_refine (consensus string; with --remove-gaps also the removeConsGaps row edits).  Default removeConsGaps=false: pafreport's setting (pafreport.cpp:31,203), which is
@@ -360,6 +361,10 @@ def bench_gapassem(args, world, rank, dev_name):
     red = torch.empty(2, dtype=torch.int32, device=dev_name)
 
     def step():
+        if world == 1:  # one shard: count + call in one pass (pw_msa_columns), then refine
+            eng.columns(st)
+            eng.refine(st, remove)
+            return
         counts, _ = eng.count(st)
         if rccl:  # column-sharded: reduce-scatter by column range, own-range bestChar, all-gather
             eng.call_sharded(st, lo, comm, rank, world)
@@ -448,7 +453,7 @@ def bench_gapassem(args, world, rank, dev_name):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": prof.get("hbm_bytes_per_launch"),
-                         "kernel": "pw_msa_count+pw_msa_call+pw_msa_refine (rank 0)", "kernel_ms": round(kern_ms, 4),
+                         "kernel": ("pw_msa_columns+pw_msa_refine" if world == 1 else "pw_msa_count+pw_msa_call+pw_msa_refine") + " (rank 0)", "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg,
                          "alg_formula": "SURVEY 8(d): sum_rows(16 + 3*seqlen) + 25*n_cols",
                          "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd"),

@@ -584,9 +584,10 @@ __device__ __forceinline__ void tile_start(const RowA& a, const BV& b, int c0, i
   }
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const pw_msa_args& A, uint64_t roff, int len) {
-  // base 16-byte aligned at or before the row; the range ends at the row's readable end
+  // base 16-byte aligned at or before the row; the range ends at the row's readable end (len < 0:
+  // an empty range — every load returns 0 without a memory access)
   const uint64_t b0 = roff & ~(uint64_t)15;
-  const uint32_t nrec = (uint32_t)(roff - b0) + (((uint32_t)max(len, 0) + 3u) & ~3u);
+  const uint32_t nrec = len < 0 ? 0u : (uint32_t)(roff - b0) + (((uint32_t)len + 3u) & ~3u);
   return __builtin_amdgcn_make_buffer_rsrc((void*)(A.seq + b0), (short)0, (int)nrec, 0x00020000);
 }
 __device__ __forceinline__ void load_win(const pw_msa_args& A, uint64_t roff, int len, int ib, int lane, v4u& w0, v4u& w1,
@@ -603,7 +604,7 @@ struct RowC {  // 1 row ahead
   v4u w0, w1, w2;
 };
 __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt, const uint16_t* runs, const RowA& a,
-                                       const BV& b, int c0, int lane, RowC& c) {
+                                       const BV& b, int c0, int c1, int lane, RowC& c) {
   int kt, ib;
   tile_start(a, b, c0, kt, ib);
   const int nch = (int)(rd(b, 5) & ~kNoTable);
@@ -615,7 +616,9 @@ __device__ __forceinline__ void load_c(const pw_msa_args& A, const int32_t* ckpt
   c.ckv = ck_r[min(kt + lane, nch)];
   c.gv[0] = ru_r[min(kt + (lane >> 3), nch) * (kRunCap / 2) + (lane & 7)];
   c.gv[1] = ru_r[min(kt + 8, nch) * (kRunCap / 2) + (lane & 7)];
-  load_win(A, a.roff, len, ib, lane, c.w0, c.w1, c.w2);
+  // (a row whose counted extent misses the tile loads no window: ~1/4 of a tile's rows at cfg5)
+  const bool ov = max((int)rd(b, 0), c0) <= min((int)rd(b, 1), c1 - 1);
+  load_win(A, a.roff, ov ? len : -1, ib, lane, c.w0, c.w1, c.w2);
 }
 __device__ __forceinline__ void pin(v4u& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(v2u& v) { asm volatile("" : "+v"(v)); }
@@ -679,10 +682,25 @@ __device__ int slow_bitmap(const pw_msa_args& A, const int32_t* ckpt, int64_t sb
   }
   return ib == INT_MAX ? len : ib;
 }
+// bestChar of one column's six counts (GapAssem.cpp:1048-1069 in closed form; 0 = no coverage)
+__device__ __forceinline__ uint8_t best_char(const int (&v)[6]) {
+  const int layers = v[0] + v[1] + v[2] + v[3] + v[4] + v[5];
+  if (layers <= 0) return 0;
+  int m = v[0], bi = 0;
+#pragma unroll
+  for (int q = 1; q < 6; q++)
+    if (v[q] > m) {
+      m = v[q];
+      bi = q;
+    }
+  uint8_t best = (uint8_t)"ACGTN-"[bi];
+  if (bi == 4 && v[5] == m) best = '-';
+  return best;
+}
 __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_args A, const int32_t* __restrict__ ckpt,
                                                               const uint16_t* __restrict__ runs,
                                                               const int32_t* __restrict__ rinfo,
-                                                              const int32_t* __restrict__ tstart) {
+                                                              const int32_t* __restrict__ tstart, int call) {
   __shared__ __attribute__((aligned(16))) TileLds L;
   LDS TileLds* lp = (LDS TileLds*)&L;
   const int tid = threadIdx.x, lane0 = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -716,7 +734,7 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
     RowA a2 = get_a(av2);
     BV bv2 = load_b(A, rinfo, tstart, r + W, a2, c0, lane0);
     RowC cc;
-    load_c(A, ckpt, runs, a1, bv1, c0, lane0, cc);
+    load_c(A, ckpt, runs, a1, bv1, c0, c1, lane0, cc);
     for (;; r += W) {
       // (lane-derived values are recomputed per row from a lane index the compiler cannot hoist:
       // left alone it keeps 64-bit per-lane pointers live across the loop and spills them)
@@ -735,7 +753,7 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         if (lane < 8) w4[128 + lane] = cc.w2;
       }
       RowC cn;
-      load_c(A, ckpt, runs, a2, bv2, c0, lane, cn);
+      load_c(A, ckpt, runs, a2, bv2, c0, c1, lane, cn);
       const RowA a3 = get_a(av3);
       const BV bv3 = load_b(A, rinfo, tstart, r + 2 * W, a3, c0, lane);
       const AV av4 = load_a(A, r + 3 * W, lane);
@@ -869,6 +887,17 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
     const int c = i / 6, f = i - 6 * c;
     dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];
   }
+  if (call) {  // pw_msa_columns (all rows in this launch): the call step from the same table
+    const int zlo = A.minmax[0], zhi = A.minmax[1];
+    for (int c = tid; c < cw; c += 64 * kCntWaves) {
+      int v[6];
+#pragma unroll
+      for (int f = 0; f < 6; f++) v[f] = (int)tab[f * kCntW + cnt_swz(c)];
+      const uint8_t best = best_char(v);
+      A.consensus[c0 + c] = best;
+      if (best == 0 && c0 + c >= zlo && c0 + c <= zhi) atomicMin(&A.minmax[3], c0 + c);
+    }
+  }
 }
 
 // bestChar of each column (GapAssem.cpp:1048-1069 in closed form); 0 = no coverage, and the
@@ -880,19 +909,7 @@ __global__ __launch_bounds__(256) void call_columns(const pw_msa_args A, int32_t
     const int32_t* src = A.counts + c * 6;
 #pragma unroll
     for (int q = 0; q < 6; q++) v[q] = src[q];
-    const int layers = v[0] + v[1] + v[2] + v[3] + v[4] + v[5];
-    uint8_t best = 0;
-    if (layers > 0) {
-      int m = v[0], bi = 0;
-#pragma unroll
-      for (int q = 1; q < 6; q++)
-        if (v[q] > m) {
-          m = v[q];
-          bi = q;
-        }
-      best = (uint8_t)"ACGTN-"[bi];
-      if (bi == 4 && v[5] == m) best = '-';
-    }
+    const uint8_t best = best_char(v);
     A.consensus[c] = best;
     if (best == 0 && c >= zlo && c <= zhi) atomicMin(&A.minmax[3], (int)c);
   }
@@ -1071,7 +1088,8 @@ static bool msa_args_ok(const pw_msa_args* a) {
          a->n_slots >= a->n_rows;
 }
 
-extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
+// count (+ with call, the bestChar step in tile_counts' epilogue: every row is in this launch)
+static int msa_count(const pw_msa_args* a, void* stream, bool call) {
   if (!msa_args_ok(a)) return PW_E_ARG;
   if (a->n_slots >= (1ull << 27)) return PW_E_ARG;  // (K1's 32-bit buffer offsets: < 34 G bases)
   hipStream_t s = (hipStream_t)stream;
@@ -1092,7 +1110,8 @@ extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) {
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(1024), 0, s, *a, chunk_sum, ckpt,
                      rinfo, runs, tstart);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kCntW - 1) / pw::kCntW);
-  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kCntWaves), 0, s, *a, ckpt, runs, rinfo, tstart);
+  hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kCntWaves), 0, s, *a, ckpt, runs, rinfo, tstart,
+                     call ? 1 : 0);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
@@ -1113,10 +1132,11 @@ extern "C" int pw_msa_call(const pw_msa_args* a, void* stream) {
   return pw_msa_call_cols(a, 0, a->n_cols, nullptr, stream);
 }
 
-extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) {
-  const int rc = pw_msa_count(a, stream);
-  return rc != PW_OK ? rc : pw_msa_call(a, stream);
-}
+extern "C" int pw_msa_count(const pw_msa_args* a, void* stream) { return msa_count(a, stream, false); }
+
+// count + call in one pass: tile_counts holds a tile's complete counts (all rows) in LDS, so it
+// writes bestChar and the zero-coverage column too (no call_columns launch, no counts re-read)
+extern "C" int pw_msa_columns(const pw_msa_args* a, void* stream) { return msa_count(a, stream, true); }
 
 extern "C" uint64_t pw_msa_refine_tiles(int32_t n_cols) { return n_cols > 0 ? ((uint64_t)n_cols + pw::kTileW - 1) / pw::kTileW : 0; }
 

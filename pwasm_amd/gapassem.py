@@ -175,6 +175,12 @@ class HipEngine:
         self._rc("pw_msa_count", self.lib.pw_msa_count(ctypes.byref(st["args"]), self.stream.cuda_stream))
         return st["d"]["counts"], st["d"]["mm"]
 
+    def columns(self, st):
+        """count + call of a single shard in one pass (pw_msa_columns: bestChar from tile_counts'
+        complete per-tile counts) -> (counts, minmax); the consensus is st["d"]["cons"]."""
+        self._rc("pw_msa_columns", self.lib.pw_msa_columns(ctypes.byref(st["args"]), self.stream.cuda_stream))
+        return st["d"]["counts"], st["d"]["mm"]
+
     def merge(self, st, row_base: int, comm):
         """pw_msa_counts_allreduce over an RCCL communicator (rccl_comm): histograms summed,
         bounds reduced, the bad row made global — in place on every rank."""
@@ -404,9 +410,10 @@ def consensus(layout_path: str, remove_gaps: bool = False, group=None, engine=No
                 and (mode in ("rccl", "rccl-allreduce") or (mode == "auto" and world > 1)))
     sharded = use_rccl and mode != "rccl-allreduce"  # column-sharded call (reduce-scatter + all-gather)
     st = engine.stage(lay, range(lo, hi), ncols, world if sharded else 1)
-    counts, mm = engine.count(st)
+    fused = world == 1 and not use_rccl and hasattr(engine, "columns")  # (one shard: count + call in one pass)
+    counts, mm = engine.columns(st) if fused else engine.count(st)
     mm_h = [int(x) for x in mm.cpu().tolist()]
-    called = None
+    called = (st["d"]["cons"], mm) if fused else None
     if sharded:  # pw_msa_call_sharded: reduce-scatter by column range, own-range bestChar, all-gather
         cons_cols, mm, part = engine.call_sharded(st, lo, rccl_comm(group), rank, world)
         called = (cons_cols, mm)
