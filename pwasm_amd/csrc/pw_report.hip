@@ -2054,8 +2054,8 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
 // ------------------------------------------------------------------ tctx_kernel
 // Target contexts that are not a plain copy of query bytes (another event within 5 bases, an
 // S run, a long insertion; setTContext, pafreport.cpp:120-128, revCompl :631, abbreviation
-// :918-927).  A wavefront takes 256 consecutive slots, compacts the flagged ones (ballots over
-// the flag bytes) and gives each lane one event: the lane stages its event's op words, forward
+// :918-927).  A wavefront scans its 256-slot groups' flag bytes (one group ahead), queues the
+// flagged slots in LDS across groups and takes them 64 at a time, one event per lane: the lane stages its event's op words, forward
 // query bytes and literal bytes in LDS windows (independent loads, one wait), then walks the op
 // stream from the event's head op through the windows (tseq is never materialised; reads
 // outside a window fall back to global memory) and stores the 32-byte record (length byte +
@@ -2069,7 +2069,7 @@ struct TctxLane {
 };
 struct TctxWave {
   TctxLane ln[kWave];
-  uint32_t list[4 * kWave];  // compacted flagged slots of the wave's 256-slot group (offsets)
+  uint32_t list[5 * kWave];  // the wave's queue of flagged slots (< 64 carried + a 256-slot group)
 };
 __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
@@ -2088,6 +2088,90 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
   uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv;
   const uint64_t flast = nf32 ? nf32 - 1 : 0;
   uint32_t fnext = nf32 ? f32[gi * kWave + lane < nf32 ? gi * kWave + lane : flast] : 0u;
+  // flagged slots queue up in the wave's list across its groups and are processed 64 at a time
+  // (every lane has an event except in the wave's last batch): the walk runs once per 64 events,
+  // not once per group (~40 flagged slots per 256 at cfg2)
+  uint32_t nl = 0;  // entries in the list (wave-uniform)
+  auto batch = [&](uint32_t nb) {
+    if ((uint32_t)lane < nb) {
+      const uint64_t s = w->list[lane];
+      const Hot h = W.hot[s];
+      const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+      const v4u p0 = tp4[0], p1 = tp4[1];  // op_begin, j, n_ops, qs | ts, T, offset (index_kernel)
+      Rec r;
+      r.ops = A.ops + p0.x;
+      r.lits = A.lits;
+      r.R = A.qseq + ((uint64_t)h.qb << 4);
+      r.L = h.L;
+      r.NS = nullptr;
+      r.tab = tp;
+      r.offset = (int)p1.z;
+      r.T = (int)p1.y;
+      r.n_ops = p0.z;
+      r.rev = (h.fn >> 29) & 1u;
+      r.acgt = false;
+      // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
+      // and forward query bytes around the event are staged in LDS
+      r.lit0 = h.l0;
+      r.lit1 = h.l1;
+      r.ls0 = h.ls;
+      r.ln = 8;
+      r.lw = nullptr;
+      r.l_lo = 0;
+      r.l_n = 0;
+      const int j = (int)p0.y;
+      int o0 = j - kTcOps / 2;
+      if (o0 < 0) o0 = 0;
+      // (indices clamped to the record's last op, values masked after: a guarded load would be
+      // a branch and a vmcnt(0) per word)
+      uint32_t ow[kTcOps];
+      const uint32_t olast = r.n_ops ? r.n_ops - 1 : 0u;
+#pragma unroll
+      for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
+#pragma unroll
+      for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
+      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
+      int x0 = fc - kTcQ / 2;
+      if (x0 < 0) x0 = 0;
+      const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
+      const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
+      v4u qv[kTcQ / 16];
+#pragma unroll
+      for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
+#pragma unroll
+      for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
+#pragma unroll
+      for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];
+      r.opw = me->opw;
+      r.op_lo = o0;
+      r.op_n = (uint32_t)kTcOps;
+      r.qw = me->qw;
+      r.qlo = x0a;
+      r.qn = kTcQ;
+      const uint32_t wd = opword(r, (uint32_t)j);
+      int ne = (int)(h.fn & kNBig);
+      if ((uint32_t)ne == kNBig) ne = event_len(r, (uint32_t)j, wd);
+      LdsSink<kTx - 1> ks;
+      ks.buf = me->out + 1;
+      ks.junk = me->out + kTx;
+      ks.pos = 0;
+      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);
+      me->out[0] = (uint8_t)ks.pos;
+      const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
+      v4u t0, t1;
+      t0.x = t32[0];
+      t0.y = t32[1];
+      t0.z = t32[2];
+      t0.w = t32[3];
+      t1.x = t32[4];
+      t1.y = t32[5];
+      t1.z = t32[6];
+      t1.w = t32[7];
+      v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
+      dtx[0] = t0;
+      dtx[1] = t1;
+    }
+  };
   for (; gi < n_groups; gi += gstride) {
     const uint64_t fi = gi * kWave + lane;
     uint32_t fcur = fnext;
@@ -2099,94 +2183,34 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = wave_last(incl);
     if (total == 0) continue;
-    uint32_t o = incl - cnt;
+    uint32_t o = nl + incl - cnt;
 #pragma unroll
     for (int q = 0; q < 4; q++)
-      if ((f4 >> (8 * q)) & 1u) w->list[o++] = (uint32_t)(4 * lane + q);
+      if ((f4 >> (8 * q)) & 1u) w->list[o++] = (uint32_t)(gi * 256 + (uint64_t)(4 * lane + q));
+    nl += total;
     wave_sync();
-    for (uint32_t b = 0; b < total; b += kWave) {
-      const bool act = b + (uint32_t)lane < total;
-      if (act) {
-        const uint64_t s = gi * 256 + w->list[b + lane];
-        const Hot h = W.hot[s];
-        const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
-        const v4u p0 = tp4[0], p1 = tp4[1];  // op_begin, j, n_ops, qs | ts, T, offset (index_kernel)
-        Rec r;
-        r.ops = A.ops + p0.x;
-        r.lits = A.lits;
-        r.R = A.qseq + ((uint64_t)h.qb << 4);
-        r.L = h.L;
-        r.NS = nullptr;
-        r.tab = tp;
-        r.offset = (int)p1.z;
-        r.T = (int)p1.y;
-        r.n_ops = p0.z;
-        r.rev = (h.fn >> 29) & 1u;
-        r.acgt = false;
-        // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
-        // and forward query bytes around the event are staged in LDS
-        r.lit0 = h.l0;
-        r.lit1 = h.l1;
-        r.ls0 = h.ls;
-        r.ln = 8;
-        r.lw = nullptr;
-        r.l_lo = 0;
-        r.l_n = 0;
-        const int j = (int)p0.y;
-        int o0 = j - kTcOps / 2;
-        if (o0 < 0) o0 = 0;
-        // (indices clamped to the record's last op, values masked after: a guarded load would be
-        // a branch and a vmcnt(0) per word)
-        uint32_t ow[kTcOps];
-        const uint32_t olast = r.n_ops ? r.n_ops - 1 : 0u;
+    while (nl >= (uint32_t)kWave) {
+      batch((uint32_t)kWave);
+      // the entries after the batch move to the front (<= 4 per lane)
+      const uint32_t rest = nl - (uint32_t)kWave;
+      uint32_t mv[4];
+      wave_sync();
 #pragma unroll
-        for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
-#pragma unroll
-        for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
-        const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
-        int x0 = fc - kTcQ / 2;
-        if (x0 < 0) x0 = 0;
-        const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
-        const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
-        v4u qv[kTcQ / 16];
-#pragma unroll
-        for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
-#pragma unroll
-        for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
-#pragma unroll
-        for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];
-        r.opw = me->opw;
-        r.op_lo = o0;
-        r.op_n = (uint32_t)kTcOps;
-        r.qw = me->qw;
-        r.qlo = x0a;
-        r.qn = kTcQ;
-        const uint32_t wd = opword(r, (uint32_t)j);
-        int ne = (int)(h.fn & kNBig);
-        if ((uint32_t)ne == kNBig) ne = event_len(r, (uint32_t)j, wd);
-        LdsSink<kTx - 1> ks;
-        ks.buf = me->out + 1;
-        ks.junk = me->out + kTx;
-        ks.pos = 0;
-        emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);
-        me->out[0] = (uint8_t)ks.pos;
-        const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
-        v4u t0, t1;
-        t0.x = t32[0];
-        t0.y = t32[1];
-        t0.z = t32[2];
-        t0.w = t32[3];
-        t1.x = t32[4];
-        t1.y = t32[5];
-        t1.z = t32[6];
-        t1.w = t32[7];
-        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
-        dtx[0] = t0;
-        dtx[1] = t1;
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = (uint32_t)(lane + kWave * k);
+        mv[k] = i < rest ? w->list[kWave + i] : 0u;
       }
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = (uint32_t)(lane + kWave * k);
+        if (i < rest) w->list[i] = mv[k];
+      }
+      nl = rest;
+      wave_sync();
     }
-    wave_sync();
   }
+  if (nl) batch(nl);
 }
 
 // ------------------------------------------------------------------ fixup_kernel
