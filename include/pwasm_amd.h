@@ -114,7 +114,8 @@ typedef struct pw_report_args {
   uint32_t skip_codan;      /* 1 = no codon impact column (pafreport.cpp:259-262, 915) */
   void* workspace;          /* device scratch, 64-byte aligned, >= pw_report_workspace_bytes() */
   uint64_t workspace_bytes;
-  uint64_t n_ev_slots;      /* event slots of the batch = sum of pw_cs_totals.n_events_max */
+  uint64_t n_ev_slots;      /* event slots of the batch = sum of pw_cs_totals.n_events_max
+                               (< 2^32 - 2^16, else PW_E_ARG: cut larger inputs into batches) */
   pw_page* pages;           /* [pw_report_page_count(n_ev_slots)] */
   uint32_t max_rec_ops;     /* largest desc[].n_ops of the batch, or 0 = unknown.  Records of more
                                than PW_BLOCK_OPS ops are decoded as blocks of PW_BLOCK_OPS ops by

@@ -2502,6 +2502,9 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   if (((uintptr_t)args->qseq & 15) || ((uintptr_t)args->lits & 3) || ((uintptr_t)args->text & 15)) return PW_E_ARG;
   if (args->n_ev_slots && (!args->pages || args->text_total < pw_report_page_count(args->n_ev_slots) * PW_PAGE_BYTES))
     return PW_E_ARG;
+  // (event slots are 32-bit indices in the fixup records and tctx_kernel's queue: a batch holds
+  // fewer than 2^32 - 2^16 slots; the hosts cut batches far below that)
+  if (args->n_ev_slots >= (1ull << 32) - (1ull << 16)) return PW_E_ARG;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t p;
