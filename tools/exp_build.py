@@ -79,6 +79,21 @@ extern "C" int pw_exp_prof(unsigned long long* out) {
 """
 
 
+# counts of render waves on the fast / general emit_event instantiation and their lanes
+# (tools/exp_fastcnt.py): g_prof[0] fast waves, [1] general waves, [2] lanes not fast, [3] active
+FASTCNT_PATCH = [
+    ("struct ClampSink {\n", "__device__ unsigned long long g_prof[16];\nstruct ClampSink {\n"),
+    ("      if (__ballot(!fast) == 0) {",
+     "      {\n        const uint64_t bf_ = __ballot(!fast), ba_ = __ballot(true);\n"
+     "        if ((uint32_t)lane == (uint32_t)__builtin_ctzll(ba_)) {\n"
+     "          atomicAdd(&g_prof[bf_ == 0 ? 0 : 1], 1ull);\n"
+     "          atomicAdd(&g_prof[2], (unsigned long long)__popcll(bf_));\n"
+     "          atomicAdd(&g_prof[3], (unsigned long long)__popcll(ba_));\n        }\n      }\n"
+     "      if (__ballot(!fast) == 0) {"),
+]
+TG = "    if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;"
+
+
 def profiled(s):
     return patched(s, PROF_PATCH) + PROF_HOST
 
@@ -220,6 +235,17 @@ def variants():
         "tc_lit32": lambda: patched(cur, tc_lit(32, 12)),
         "tc_lit16_ops8": lambda: patched(cur, tc_lit(16, 8) + TC_OPS8),
         "tc_ops8": lambda: patched(cur, TC_OPS8),
+        "fastcnt": lambda: patched(cur, FASTCNT_PATCH) + PROF_HOST,
+        # timing only (parity fails): fixup_kernel without its long lines / without emit_event /
+        # without the finalize part
+        "fx_nolong": lambda: patched(cur, [("  if (W.ctr[2]) return;  // overflow", "  return;  // overflow")]),
+        "fx_noemit": lambda: patched(cur, [("    int rel;\n    emit_event(g, r, in, skip, rel);\n  }",
+                                            "    g.p[0] = (uint8_t)(in.tx[0] + me->qw[0] + me->lw[0] + (uint32_t)in.n);\n  }")]),
+        "fx_nofin": lambda: patched(cur, [("    if (ai < A.n_alns) finalize_record(A, W, ai);\n    return;", "    return;")]),
+        # tctx grid: workgroups per CU (4 resident): 2, 8 (two rounds), 12
+        "tg2": lambda: patched(cur, [(TG, TG.replace("4u", "2u"))]),
+        "tg8": lambda: patched(cur, [(TG, TG.replace("4u", "8u"))]),
+        "tg12": lambda: patched(cur, [(TG, TG.replace("4u", "12u"))]),
     }
 
 
