@@ -129,13 +129,14 @@ struct SumPre {
 };
 // (the descriptor load is unconditional and its value is not touched until sums_load: a select
 // next to the load would make hipcc wait for it there)
-__device__ __forceinline__ uint64_t sums_desc(const pw_msa_args& A, const uint64_t* sdesc, uint64_t g, int lane) {
-  const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
+// (chunk and group indices are 32-bit: pw_msa_count takes fewer than 2^27 slots)
+__device__ __forceinline__ uint64_t sums_desc(const pw_msa_args& A, const uint64_t* sdesc, uint32_t g, int lane) {
+  const uint32_t c = g * 4u + (uint32_t)(lane >> 4);
   return sdesc[c < A.n_slots ? c : A.n_slots - 1];
 }
-__device__ __forceinline__ void sums_load(const pw_msa_args& A, uint64_t d, uint64_t g, int lane, SumPre& p) {
+__device__ __forceinline__ void sums_load(const pw_msa_args& A, uint64_t d, uint32_t g, int lane, SumPre& p) {
   const int sub = lane & 15;
-  const uint64_t c = g * 4 + (uint64_t)(lane >> 4);
+  const uint32_t c = g * 4u + (uint32_t)(lane >> 4);
   if (c >= A.n_slots) d &= (1ull << 48) - 1;  // past the end: no bases
   p.off = (d & ((1ull << 48) - 1)) + 16ull * (uint64_t)sub;
   p.tv = (int)((d >> 48) & 0x1FFu);
@@ -180,7 +181,11 @@ __device__ __forceinline__ int sums_group(const pw_msa_args& A, const SumPre& cu
     const i16x2 v = __builtin_bit_cast(i16x2, w[d]);
     const u16x2 m = __builtin_bit_cast(u16x2, __builtin_elementwise_max(v, zero));
     s = __builtin_amdgcn_udot2(m, one, s, false);
-    pmw |= __builtin_bit_cast(uint32_t, __builtin_elementwise_min(m, one)) << d;  // element 2d: bit d, 2d + 1: 16 + d
+    // gap > 0 per half: bit 15 of m + 0x7FFF (m <= 0x7FFF: no carry into the other half) ->
+    // element 2d: bit d, 2d + 1: bit 16 + d (integer SWAR: a packed min here compiles to
+    // per-half compares and selects)
+    const uint32_t t = __builtin_bit_cast(uint32_t, m) + 0x7FFF7FFFu;
+    pmw |= (t >> (15 - d)) & (0x00010001u << d);
     bg = __builtin_elementwise_max(bg, v);
   }
   // interleave: bit t of pm = element t has a gap
@@ -224,9 +229,9 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
   __shared__ uint32_t lruns[4][4][kRunCap / 2];  // [wave][chunk of the group][entry pairs]
   const int lane = threadIdx.x & 63, sub = lane & 15, wv = threadIdx.x >> 6;
   LDS uint32_t* lr32 = (LDS uint32_t*)&lruns[wv][lane >> 4][0];
-  const uint64_t ng = (A.n_slots + 3) / 4;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  uint64_t g = (uint64_t)blockIdx.x * 4 + (uint64_t)wv;
+  const uint32_t ng = (uint32_t)((A.n_slots + 3) / 4);
+  const uint32_t nw = gridDim.x * 4u;
+  uint32_t g = blockIdx.x * 4u + (uint32_t)wv;
   if (g >= ng) return;
   // (pw_msa_count checks that 32 * n_slots fits a 32-bit offset)
   const __amdgpu_buffer_rsrc_t rs_runs =
@@ -251,14 +256,14 @@ __global__ __launch_bounds__(256) void row_chunk_sums(const pw_msa_args A, int32
     dn = dnn;
     wave_sync();
     const uint32_t rw = lr32[sub & 7];
-    const uint32_t c = (uint32_t)(g * 4) + (uint32_t)(lane >> 4);
+    const uint32_t c = g * 4u + (uint32_t)(lane >> 4);
     __builtin_amdgcn_raw_buffer_store_b32(rw, rs_runs, sub < 8 ? c * (uint32_t)(2 * kRunCap) + 4u * (uint32_t)sub : kOut, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b32((uint32_t)cs, rs_cs, sub == 0 ? 4u * c : kOut, 0, 0);
     wave_sync();
     g += nw;
   };
-  const uint64_t n_mine = (ng - g + nw - 1) / nw;
-  for (uint64_t k = 2; k <= n_mine; k += 2) {
+  const uint32_t n_mine = (ng - g + nw - 1) / nw;
+  for (uint32_t k = 2; k <= n_mine; k += 2) {
     step(p0);
     step(p1);
   }
