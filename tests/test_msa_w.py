@@ -15,6 +15,7 @@ import pwasm_amd as pw
 from conftest import ORACLE, SYNTH, run, synth_paf
 from test_gpu_parity import query_end_case
 
+PW_E_ARG = -1  # include/pwasm_amd.h
 FLAGS = {"-G": pw.FLAG_G, "-F": pw.FLAG_F, "-C": pw.FLAG_C, "-N": pw.FLAG_N}
 
 
@@ -58,6 +59,16 @@ def test_edge_mix(built, tmp_path, seed):
     fa, paf = synth_paf(tmp_path, 0, seed=seed)
     out = msa_same(fa, paf, tmp_path)
     assert out.count(b">") >= 2
+
+
+def test_no_msa_in_full_genome_mode(built, tmp_path):
+    """-w with -F: the reference exits with "can only generate MSA for -G mode!"
+    (pafreport.cpp:265-269), so the batch API builds no MSA there and pw_batch_write_msa refuses."""
+    fa, paf = synth_paf(tmp_path, 2, seed=3, scale=0.01)
+    rc, _, err = run([ORACLE, "-F", "-r", fa, "-w", tmp_path / "o.mfa", "-o", tmp_path / "o.txt", paf])
+    assert rc == 1 and b"can only generate MSA for -G mode!" in err
+    batch = pw.HostBatch(fa, paf, pw.FLAG_W | pw.FLAG_F)
+    assert batch.write_msa(str(tmp_path / "b.mfa")) == PW_E_ARG
 
 
 def test_cfg1(built, tmp_path):
