@@ -537,6 +537,44 @@ def test_w_refused_in_genome_mode_and_bad_path(built, tmp_path):
     assert (rp, op, ep) == (ro, oo, eo) and ro == 1
 
 
+@pytest.mark.parametrize("zero", [False, True])
+def test_msa_columns_fused_equals_count_call(built, tmp_path, zero):
+    """pw_msa_columns (bestChar in tile_counts' epilogue) against pw_msa_count + pw_msa_call on the
+    same staged layout: counts, consensus and minmax identical, over several 2048-column tiles and
+    a partial last tile; `zero` leaves a zero-coverage stretch inside [mincol, maxcol]."""
+    import torch
+    from pwasm_amd import gapassem
+    rng = random.Random(31 + zero)
+    rows = []
+    for r in range(30):
+        n = rng.randint(500, 4000)
+        seq = "".join(rng.choice("ACGTACGTNacgt*-") for _ in range(n))
+        if zero:  # two groups of rows with uncovered columns between them
+            ofs = [0] + [rng.choice([0] * 30 + [1]) for _ in range(n - 1)]
+            off = rng.randint(0, 300) if r % 2 else rng.randint(20000, 20300)
+        else:
+            ofs = [0] + [rng.choice([0] * 30 + [1, 3, 80]) for _ in range(n - 1)]
+            off = rng.randint(0, 3000)
+        rows.append((off, seq, ofs, rng.randint(0, 20), rng.randint(0, 20), r % 2))
+    lay_p = tmp_path / "f.pwl"
+    write_pwl(lay_p, rows)
+    lay = gapassem.Layout(str(lay_p))
+    eng = gapassem.HipEngine("cuda:0")
+    st = eng.stage(lay, range(lay.n), lay.length)
+    counts, mm = eng.count(st)
+    cons, mm = eng.call(st)
+    torch.cuda.synchronize()
+    want = (counts.clone(), cons.clone(), mm.clone())
+    st["d"]["cons"].fill_(7)
+    st["d"]["counts"].fill_(-1)
+    counts, mm = eng.columns(st)
+    torch.cuda.synchronize()
+    assert torch.equal(counts, want[0])
+    assert torch.equal(st["d"]["cons"], want[1])
+    assert mm.tolist() == want[2].tolist()
+    assert (int(mm[3]) != 2 ** 31 - 1) == zero  # (the zero-coverage column is found by both)
+
+
 # ---------------------------------------------------------------- RCCL collectives C-ABI
 def test_msa_counts_allreduce_world1(built, tmp_path):
     """pw_comm_* + pw_msa_counts_allreduce / reduce_scatter on a one-rank RCCL communicator:
