@@ -281,7 +281,9 @@ int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int3
 /* Both for n rows in one call: rows with replay[k] != 0 get pw_ga_row_remove_columns(alpos) first,
  * then every row pw_ga_row_finish; messages back to back in msgbuf (row k: [msg_off[k],
  * msg_off[k+1]), msg_off has n + 1 entries), failed[k] = 1 after a GError, after which it stops.
- * Returns the rows processed (or a negative PW_E_* status). */
+ * Returns the rows processed (or a negative PW_E_* status).  If the messages exceed msg_cap no row
+ * is left edited (all restored to their input state) and msg_off[returned] > msg_cap is the size to
+ * call again with. */
 int64_t pw_ga_rows_finish(pw_ga_row* rows, uint64_t n, const uint8_t* replay, const int32_t* alpos, uint64_t n_alpos,
                           const uint8_t* cons, int32_t cons_len, int32_t cpos_base, uint32_t flags, char* msgbuf,
                           uint64_t msg_cap, uint64_t* msg_off, int32_t* failed);
@@ -424,6 +426,11 @@ int pw_batch_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_res
 int pw_batch_write_at(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                       const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items, char* err_buf,
                       uint64_t err_cap);
+/* pw_batch_write_range: as pw_batch_write_at for the items [first, first + n_items) (out_off[0] is
+ * item first's offset) — the multi-GPU driver writes a batch window by window of global lines. */
+int pw_batch_write_range(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
+                         const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off, uint64_t n_items,
+                         char* err_buf, uint64_t err_cap);
 
 /* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
  * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its

@@ -177,6 +177,8 @@ _SIGS = {
     "pw_batch_items": (ctypes.c_int, [ctypes.c_void_p] * 8 + [ctypes.POINTER(ctypes.c_uint64)]),
     "pw_batch_write_at": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                                                                  ctypes.c_void_p, ctypes.c_uint64]),
+    "pw_batch_write_range": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
+                                                                    ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
     "pw_batch_genomes": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -335,6 +337,19 @@ class HostBatch:
                                      int(err_bytes))
         if rc != 0:
             raise RuntimeError(f"pw_batch_write_at: {rc}")
+        return eb.raw[: int(err_bytes)]
+
+    def write_range(self, text_host, results_host, pages_host, fd: int, first: int, out_off, err_bytes: int) -> bytes:
+        """pw_batch_write_range: stdout of items [first, first + len(out_off)) pwritten at out_off into
+        fd; returns their stderr bytes."""
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+        eb = ctypes.create_string_buffer(max(int(err_bytes), 1))
+        rc = lib().pw_batch_write_range(self._h, text_host.ctypes.data, results_host.ctypes.data,
+                                        pages_host.ctypes.data, fd, int(first),
+                                        out_off.ctypes.data if out_off.size else None, out_off.size, eb,
+                                        int(err_bytes))
+        if rc != 0:
+            raise RuntimeError(f"pw_batch_write_range: {rc}")
         return eb.raw[: int(err_bytes)]
 
     def array(self, name: str):

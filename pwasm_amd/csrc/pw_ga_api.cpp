@@ -1213,12 +1213,13 @@ extern "C" int pw_ga_row_remove_columns(pw_ga_row* row, const int32_t* alpos, ui
   return PW_OK;
 }
 
-extern "C" int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int32_t cpos_base,
-                                uint32_t flags, char* msgbuf, size_t msglen) {
-  if (!row || (row->seqlen > 0 && (!row->ofs || !row->seq)) || (cons_len > 0 && !cons)) return PW_E_ARG;
+// refineClipping / removeClipGaps / refineClipping(skipDels) of one row (refineMSA's tail,
+// GapAssem.cpp:1163-1181); what the reference prints for the row is appended to msgs, uncut
+static int row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int32_t cpos_base, uint32_t flags,
+                      std::string& msgs) {
   RowView v = view_of_row(row);
   const bool rc = flags & PW_GA_REFINE_CLIP, rm = flags & PW_GA_REMOVE_GAPS;
-  std::string err, msgs;
+  std::string err;
   const char* c = (const char*)cons;
   int status = PW_OK;
   if (rc && !refine_clipping(v, c, cons_len, rel_col(row->offset, cpos_base, 0), false, &err, &msgs)) {
@@ -1228,6 +1229,14 @@ extern "C" int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t con
     status = 1;
   }
   msgs += err;
+  return status;
+}
+
+extern "C" int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t cons_len, int32_t cpos_base,
+                                uint32_t flags, char* msgbuf, size_t msglen) {
+  if (!row || (row->seqlen > 0 && (!row->ofs || !row->seq)) || (cons_len > 0 && !cons)) return PW_E_ARG;
+  std::string msgs;
+  const int status = row_finish(row, cons, cons_len, cpos_base, flags, msgs);
   if (msgbuf && msglen) snprintf(msgbuf, msglen, "%s", msgs.c_str());
   return status;
 }
@@ -1236,30 +1245,50 @@ extern "C" int pw_ga_row_finish(pw_ga_row* row, const uint8_t* cons, int32_t con
 // replay[k] != 0 first get removeColumn replayed for alpos (pw_ga_row_remove_columns), then every
 // row pw_ga_row_finish.  Messages back to back in msgbuf (row k's are [msg_off[k], msg_off[k+1]));
 // failed[k] = 1 after a GError.  Stops after the first failing row (the reference exits there);
-// returns the number of rows processed.
+// returns the number of rows processed.  When the messages do not fit in msg_cap, every row is
+// restored to its input state (ofs, offset, numgaps, clips), msg_off still holds the full sizes
+// (msg_off[k] > msg_cap): the caller calls again with a buffer of msg_off[k] bytes.
 extern "C" int64_t pw_ga_rows_finish(pw_ga_row* rows, uint64_t n, const uint8_t* replay, const int32_t* alpos,
                                      uint64_t n_alpos, const uint8_t* cons, int32_t cons_len, int32_t cpos_base,
                                      uint32_t flags, char* msgbuf, uint64_t msg_cap, uint64_t* msg_off,
                                      int32_t* failed) {
   if ((n && (!rows || !msg_off || !failed)) || (n_alpos && !alpos)) return PW_E_ARG;
-  std::vector<char> one(1 << 16);
-  uint64_t used = 0;
+  for (uint64_t k = 0; k < n; k++)
+    if (rows[k].seqlen < 0 || (rows[k].seqlen > 0 && (!rows[k].ofs || !rows[k].seq))) return PW_E_ARG;
+  if (cons_len > 0 && !cons) return PW_E_ARG;
+  struct Saved {
+    int32_t offset, numgaps, clp5, clp3;
+    std::vector<int16_t> ofs;
+  };
+  std::vector<Saved> saved(n);
+  for (uint64_t k = 0; k < n; k++) {
+    saved[k] = {rows[k].offset, rows[k].numgaps, rows[k].clp5, rows[k].clp3, {}};
+    saved[k].ofs.assign(rows[k].ofs, rows[k].ofs + rows[k].seqlen);
+  }
+  std::string msgs;
   msg_off[0] = 0;
   uint64_t k = 0;
   for (; k < n; k++) {
     failed[k] = 0;
-    if (replay && replay[k] && pw_ga_row_remove_columns(&rows[k], alpos, n_alpos) != PW_OK) return PW_E_ARG;
-    const int rc = pw_ga_row_finish(&rows[k], cons, cons_len, cpos_base, flags, one.data(), one.size());
-    if (rc < 0) return rc;
-    const size_t m = strlen(one.data());
-    if (msgbuf && used + m <= msg_cap) memcpy(msgbuf + used, one.data(), m);
-    used += m;
-    msg_off[k + 1] = used;
+    if (replay && replay[k]) remove_columns(view_of_row(&rows[k]), alpos, n_alpos);
+    const int rc = row_finish(&rows[k], cons, cons_len, cpos_base, flags, msgs);
+    msg_off[k + 1] = msgs.size();
     if (rc == 1) {
       failed[k] = 1;
       k++;
       break;
     }
   }
+  if (msgs.size() > msg_cap || (!msgbuf && !msgs.empty())) {
+    for (uint64_t j = 0; j < n; j++) {
+      rows[j].offset = saved[j].offset;
+      rows[j].numgaps = saved[j].numgaps;
+      rows[j].clp5 = saved[j].clp5;
+      rows[j].clp3 = saved[j].clp3;
+      std::copy(saved[j].ofs.begin(), saved[j].ofs.end(), rows[j].ofs);
+    }
+    return (int64_t)k;
+  }
+  if (!msgs.empty()) memcpy(msgbuf, msgs.data(), msgs.size());
   return (int64_t)k;
 }

@@ -16,6 +16,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <future>
@@ -1254,6 +1255,10 @@ struct Device {
       ql[k] = b.recs[k].qlen;
     }
     off[na] = ct;
+    if (ct >= (1ull << 32) - 64) {  // op_begin / lit_begin are 32-bit offsets into the batch's cs text
+      fprintf(stderr, "pafreport: batch cs text of %zu bytes exceeds the 4 GiB a batch can address\n", ct);
+      return false;
+    }
     if (!cs_text.ensure(ct + 16) || !ops.ensure(ct + 16) || !lits.ensure(ct + kDevPad) || !cs_offs.ensure(na + 1) ||
         !cs_o.ensure(na + 1) || !cs_q.ensure(na + 1) || !cs_rec.ensure(na + 1)) {
       fprintf(stderr, "pafreport: device allocation failed\n");
@@ -1274,6 +1279,13 @@ struct Device {
     uint64_t ev = 0, txt = 0;
     std::vector<uint32_t> hops;
     std::vector<uint8_t> hlits;
+    // host-packed op / literal prefixes of handed-back records, uploaded after the loop on `stream`
+    // whatever the packer's verdict: index_kernel decodes d.n_ops words of a failing record too
+    // (a base mismatch before the cs error is the reference's first error, pafreport.cpp:545-548)
+    std::vector<uint32_t> fb_ops;
+    std::vector<uint8_t> fb_lits;
+    std::vector<std::array<uint64_t, 4>> fb;  // dst offset, fb_ops start, n_ops, n_lits (lits at fb_lits start = [1])
+    std::vector<uint64_t> fb_lit0;
     for (size_t k = 0; k < na; k++) {
       RecHost& rh = b.recs[k];
       pw_aln_desc& d = b.desc[k];
@@ -1292,8 +1304,12 @@ struct Device {
         hlits.resize((size_t)rh.cs_len + 1);
         rc = pack_cs_n(cs, cs + rh.cs_len, d.offset, rh.qlen, hops.data(), hops.size(), hlits.data(), hlits.size(), &tot,
                        &epos);
-        if (rc == PW_CS_OK && tot.n_ops) HIPCHK(hipMemcpy(ops.p + rh.cs_off, hops.data(), tot.n_ops * 4, hipMemcpyHostToDevice));
-        if (rc == PW_CS_OK && tot.n_lits) HIPCHK(hipMemcpy(lits.p + rh.cs_off, hlits.data(), tot.n_lits, hipMemcpyHostToDevice));
+        if (tot.n_ops || tot.n_lits) {
+          fb.push_back({rh.cs_off, fb_ops.size(), tot.n_ops, tot.n_lits});
+          fb_lit0.push_back(fb_lits.size());
+          fb_ops.insert(fb_ops.end(), hops.begin(), hops.begin() + tot.n_ops);
+          fb_lits.insert(fb_lits.end(), hlits.begin(), hlits.begin() + tot.n_lits);
+        }
         acgt = rc == PW_CS_OK && q.all_acgt(qi);
         for (uint32_t i = 0; i < tot.n_lits && acgt; i++) acgt = QueryDb::is_acgt_byte(hlits[i]);
       } else {
@@ -1324,6 +1340,11 @@ struct Device {
                                                 rh.r_alnend, rh.r_alnstart, s));
       }
     }
+    for (size_t j = 0; j < fb.size(); j++) {
+      if (fb[j][2]) HIPCHK(hipMemcpyAsync(ops.p + fb[j][0], fb_ops.data() + fb[j][1], fb[j][2] * 4, hipMemcpyHostToDevice, stream));
+      if (fb[j][3]) HIPCHK(hipMemcpyAsync(lits.p + fb[j][0], fb_lits.data() + fb_lit0[j], fb[j][3], hipMemcpyHostToDevice, stream));
+    }
+    if (!fb.empty()) HIPCHK(hipStreamSynchronize(stream));  // the staging vectors die here
     b.n_events_max = ev;
     b.text_total = txt;
     return true;
@@ -2370,17 +2391,19 @@ extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, cons
   return PW_OK;
 }
 
-// Write the stdout bytes of the batch's first n_items items at out_off[k] of fd (pwrite: ranks
-// write disjoint ranges of one file) and their stderr bytes back to back into err_buf.
-extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
-                                 const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items,
-                                 char* err_buf, uint64_t err_cap) {
-  if (!bt || (n_items && !out_off) || n_items > bt->b.log.size()) return PW_E_ARG;
+// Write the stdout bytes of the batch's items [first, first + n_items) at out_off[k - first] of fd
+// (pwrite: ranks write disjoint ranges of one file) and their stderr bytes back to back into err_buf.
+extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                                    const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off,
+                                    uint64_t n_items, char* err_buf, uint64_t err_cap) {
+  if (!bt || (n_items && !out_off) || first > bt->b.log.size() || n_items > bt->b.log.size() - first)
+    return PW_E_ARG;
   TextSrc src;
   src.host = text_host;
   uint64_t eo = 0;
-  for (uint64_t k = 0; k < n_items; k++) {
-    PwriteCookie pc{fd, out_off[k]};
+  for (uint64_t j = 0; j < n_items; j++) {
+    const uint64_t k = first + j;
+    PwriteCookie pc{fd, out_off[j]};
     FILE* o = fopencookie(&pc, "w", cookie_io_functions_t{nullptr, pwrite_write, nullptr, nullptr});
     char* eb = nullptr;
     size_t en = 0;
@@ -2399,6 +2422,12 @@ extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, c
     if (pc.bad) return PW_E_IO;
   }
   return eo <= err_cap || !err_buf ? PW_OK : PW_E_ARG;
+}
+
+extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                                 const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items,
+                                 char* err_buf, uint64_t err_cap) {
+  return pw_batch_write_range(bt, text_host, res_host, pages_host, fd, 0, out_off, n_items, err_buf, err_cap);
 }
 
 extern "C" void pw_batch_free(pw_batch* bt) { delete bt; }

@@ -284,7 +284,7 @@ def _i32(v: int) -> int:
 
 
 def finish_rows(lay: Layout, rows, base: dict, alpos, cons: bytes, mincol: int, remove_gaps: bool,
-                refine_clipping: bool):
+                refine_clipping: bool, msg_cap: int = 1 << 16):
     """refineMSA's per-row tail for `rows` on the host (GapAssem.cpp:1163-1181), all rows in one
     C call (pw_ga_rows_finish): rows holding deleted bases (ofs < 0) get removeColumn replayed from
     their input gaps, every row then refineClipping / removeClipGaps / refineClipping.  base =
@@ -328,8 +328,8 @@ def finish_rows(lay: Layout, rows, base: dict, alpos, cons: bytes, mincol: int, 
     v["clp3"] = lay.clp3[ri]
     v["rev"] = lay.rev[ri]
     v["id"] = ctypes.addressof(idbuf) + id_off
-    cap = 1 << 16
-    while True:
+    cap = max(1, int(msg_cap))
+    while True:  # an overflowing call leaves every row as it was (pw_ga_rows_finish restores them)
         msg = ctypes.create_string_buffer(cap)
         moff = np.zeros(n + 1, dtype=np.uint64)
         failed = np.zeros(n, dtype=np.int32)

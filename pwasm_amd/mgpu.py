@@ -14,13 +14,16 @@ Replaces the reference's sequential record loop (pafreport.cpp:303-436) over a n
   batches       the rank's lines in pipelined batches (PW_CHUNK_BYTES, default 256 MB): batch k+1
                 is packed on host threads while the GPU runs batch k (pw_batch_from_buffer, the
                 dedupe state moving from batch to batch; pw_stop_table_build + pw_report_events).
-  output        no rank-0 merge: the first fatal input line over all ranks ends the run (all-reduce
-                MIN); every rank's per-line stdout byte counts are summed over the ranks (all-reduce
-                of one int64 per input line) and exclusive-scanned into file offsets, and each rank
-                pwrites its own items there (pw_batch_write_at).  stderr lines (warnings, the fatal
-                message) are gathered to rank 0 and written in input-line order; the exit code is
-                the fatal item's.  stdout without -o: the file is assembled in a temporary file and
-                streamed out by rank 0.
+  output        no rank-0 merge, written window by window of global input lines (OffsetWriter,
+                PW_WINDOW_LINES) as the batches finish, so a rank holds only the batches of the
+                current window: the first fatal input line of the window over all ranks ends the run
+                (all-reduce MIN); every rank's per-line stdout byte counts of the window are summed
+                over the ranks (all-reduce of one int64 per line of the window) and exclusive-scanned
+                into file offsets after the previous windows, and each rank pwrites its own items
+                there (pw_batch_write_range).  stderr lines (warnings, the fatal message) are
+                gathered to rank 0 only and written in input-line order; the exit code is the fatal
+                item's.  stdout without -o: the file is assembled in a temporary file and streamed
+                out by rank 0 after each window.  c10d's connection messages are kept off stdout.
   per-genome    pw_genome_table sums each target's alignments / event lines / aligned bases on the
   tables        device; the rows and target names of all ranks are all-gathered (--genome-table).
 No collective touches the per-record data path: records are independent.
@@ -187,91 +190,155 @@ def batch_cuts(text, line_no, target):
     return cuts
 
 
-def write_items_at(outs, n_total, out_path, world, rank, dv, tmpdir=None):
-    """Output of all ranks' finished batches without a merge pass: outs = [(batch, text, results,
-    pages, (line, status, stdout bytes, stderr bytes))] of this rank in line order.  The first fatal
-    input line over all ranks ends the run (all-reduce MIN); per-line stdout byte counts (one owner
-    per line) are summed over the ranks and exclusive-scanned into offsets of one output file, where
-    each rank pwrites its items (pw_batch_write_at).  stderr is gathered to rank 0 and written in
-    input-line order; stdout (out_path None) is assembled in a temporary file that rank 0 streams
-    out.  Returns the exit code of the single-process run."""
-    import torch
-    import torch.distributed as dist
+class OffsetWriter:
+    """Output of this rank's finished batches, window by window of global input lines, without a
+    merge pass and without holding a rank's whole report: a batch is handed over (add) as soon as
+    its outputs are on the host, and each window [j*W, (j+1)*W) is written once every rank has the
+    items of all its lines below the window's end (advance).  Per window, in the same order on
+    every rank: the first fatal line of the window over all ranks (all-reduce MIN; an input error of
+    any rank ends the run too), the per-line stdout byte counts of the window (one owner per line;
+    all-reduce SUM of W int64) exclusive-scanned into file offsets after the previous windows, each
+    rank's pwrite of its own items there (pw_batch_write_range), stderr gathered to rank 0 only and
+    written in line order.  Batches are released once their last item is written.  stdout without
+    -o: the file is assembled in a temporary file and rank 0 streams each window out after it."""
 
-    def all_reduce_i64(vals, op):
-        t = torch.tensor(vals, dtype=torch.int64, device=dv)
+    BIG = np.iinfo(np.int64).max
+
+    def __init__(self, n_total, out_path, world, rank, dv, tmpdir=None, window=None):
+        import torch.distributed as dist
+        self.n_total, self.world, self.rank, self.dv = int(n_total), world, rank, dv
+        self.W = max(1, int(window or os.environ.get("PW_WINDOW_LINES", str(1 << 21))))
+        self.nwin = -(-self.n_total // self.W)
+        self.j, self.base, self.code, self.done, self.err = 0, 0, 0, False, None
+        self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item], ...] in line order
+        self.tmp_out = None
+        if out_path is None:  # stdout: assembled in a file, streamed out by rank 0 window by window
+            if rank == 0:
+                fd0, self.tmp_out = tempfile.mkstemp(prefix="pwmg_out_", dir=tmpdir)
+                os.close(fd0)
+            if world > 1:
+                o = [self.tmp_out]
+                dist.broadcast_object_list(o, src=0)
+                self.tmp_out = o[0]
+            out_path = self.tmp_out
+        if rank == 0:
+            os.close(os.open(out_path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644))
         if world > 1:
+            dist.barrier()
+        self.fd = os.open(out_path, os.O_WRONLY)
+        self.rd = open(self.tmp_out, "rb") if self.tmp_out and rank == 0 else None
+
+    def _reduce(self, vals, op):
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor(vals, dtype=torch.int64, device=self.dv)
+        if self.world > 1:
             dist.all_reduce(t, op=op)
         return t.cpu().numpy()
 
-    big = np.iinfo(np.int64).max
-    mine = [int(it[0][it[1] >= 0][0]) for _, _, _, _, it in outs if (it[1] >= 0).any()]
-    stop = int(all_reduce_i64([min(mine) if mine else big], dist.ReduceOp.MIN if world > 1 else None)[0])
-    lens = np.zeros(max(n_total, 1), dtype=np.int64)
-    for _, _, _, _, (ln, st, on, en) in outs:
-        keep = ln <= stop
-        lens[ln[keep].astype(np.int64)] = on[keep].astype(np.int64)
-    if world > 1:
-        tl = torch.from_numpy(lens).to(dv)
-        dist.all_reduce(tl, op=dist.ReduceOp.SUM)
-        lens = tl.cpu().numpy()
-    off = np.zeros(lens.size + 1, dtype=np.int64)
-    np.cumsum(lens, out=off[1:])
-    total = int(off[-1])
-    tmp_out = None
-    if out_path is None:  # stdout: assembled in a file, then streamed out by rank 0
-        if rank == 0:
-            fd0, tmp_out = tempfile.mkstemp(prefix="pwmg_out_", dir=tmpdir)
-            os.close(fd0)
-        if world > 1:
-            o = [tmp_out]
-            dist.broadcast_object_list(o, src=0)
-            tmp_out = o[0]
-        out_path = tmp_out
-    if rank == 0:
-        fd = os.open(out_path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
-        os.ftruncate(fd, total)
-        os.close(fd)
-    if world > 1:
-        dist.barrier()
-    fd = os.open(out_path, os.O_WRONLY)
-    errs = []
-    try:
-        for b, text_h, res_h, pages_h, (ln, st, on, en) in outs:
-            k = int((ln <= stop).sum())  # (items are in line order)
-            if k == 0:
+    def add(self, out):
+        self.pending.append([out, 0])
+
+    def advance(self, covered):
+        """This rank has the items of all its lines < covered (n_total: all it will ever have)."""
+        while not self.done and self.j < self.nwin and min((self.j + 1) * self.W, self.n_total) <= covered:
+            self._window()
+
+    def _window(self):
+        import torch
+        import torch.distributed as dist
+        lo, hi = self.j * self.W, min((self.j + 1) * self.W, self.n_total)
+        fatal = self.BIG
+        for (_, _, _, _, (ln, st, _, _)), c in self.pending:
+            sel = (ln[c:] < hi) & (st[c:] >= 0)
+            if sel.any():
+                fatal = min(fatal, int(ln[c:][sel][0]))
+        MIN = dist.ReduceOp.MIN if self.world > 1 else None
+        stop, ok = (int(x) for x in self._reduce([fatal, 0 if self.err else 1], MIN))
+        if not ok:  # an input error on some rank: the first one in rank order, printed by rank 0
+            errs = [self.err]
+            if self.world > 1:
+                errs = [None] * self.world if self.rank == 0 else None
+                dist.gather_object(self.err, errs, dst=0)
+            if self.rank == 0:
+                e = next(x for x in errs if x)
+                sys.stderr.write(e.split(": ", 1)[-1] if e.startswith("pw_batch_from_buffer") else e)
+                sys.stderr.flush()
+            self.code, self.done = 1, True
+            return
+        lens = np.zeros(hi - lo, dtype=np.int64)
+        spans, owner = [], -1
+        for ent in self.pending:
+            (_, _, _, _, (ln, st, on, en)), c = ent
+            k = c + int(np.searchsorted(ln[c:], min(hi, stop + 1) if stop != self.BIG else hi, side="left"))
+            spans.append((c, k))
+            if k > c and int(ln[k - 1]) == stop:
+                owner = int(st[k - 1])
+            lens[ln[c:k].astype(np.int64) - lo] = on[c:k].astype(np.int64)
+        if self.world > 1:
+            tl = torch.from_numpy(lens).to(self.dv)
+            dist.all_reduce(tl, op=dist.ReduceOp.SUM)
+            lens = tl.cpu().numpy()
+        off = np.empty(hi - lo + 1, dtype=np.int64)
+        off[0] = self.base
+        np.cumsum(lens, out=off[1:])
+        off[1:] += self.base
+        errs = []
+        for ent, (c, k) in zip(self.pending, spans):
+            if k == c:
                 continue
-            eb = b.write_at(text_h, res_h, pages_h, fd, off[ln[:k].astype(np.int64)], int(en[:k].sum()))
+            b, text_h, res_h, pages_h, (ln, st, on, en) = ent[0]
+            eb = b.write_range(text_h, res_h, pages_h, self.fd, c, off[ln[c:k].astype(np.int64) - lo],
+                               int(en[c:k].sum()))
             p = 0
-            for i in range(k):
+            for i in range(c, k):
                 if en[i]:
                     errs.append((int(ln[i]), eb[p:p + int(en[i])]))
                     p += int(en[i])
-    finally:
-        os.close(fd)
-    code = 0
-    if stop != big:
-        owner = [int(st[ln == stop][0]) for _, _, _, _, (ln, st, on, en) in outs if (ln == stop).any()]
-        code = int(all_reduce_i64([owner[0] if owner else -1], dist.ReduceOp.MAX if world > 1 else None)[0])
-    if world > 1:
-        allerr = [None] * world
-        dist.all_gather_object(allerr, errs)
-        errs = sorted((x for e in allerr for x in e), key=lambda t: t[0])
-        dist.barrier()
-    if rank == 0:
-        if tmp_out:
-            with open(tmp_out, "rb") as f:
-                while True:
-                    blk = f.read(1 << 24)
-                    if not blk:
-                        break
-                    sys.stdout.buffer.write(blk)
+            ent[1] = k
+        self.pending = [e for e in self.pending if e[1] < len(e[0][4][0])]
+        if self.world > 1:  # (every rank's pwrites are done once rank 0 has its stderr)
+            allerr = [None] * self.world if self.rank == 0 else None
+            dist.gather_object(errs, allerr, dst=0)
+            if self.rank == 0:
+                errs = sorted((x for e in allerr for x in e), key=lambda t: t[0])
+        if self.rd is not None:
+            left = int(off[-1]) - self.base
+            while left > 0:
+                blk = self.rd.read(min(left, 1 << 24))
+                if not blk:
+                    raise RuntimeError("mgpu: report window shorter than its offsets")
+                sys.stdout.buffer.write(blk)
+                left -= len(blk)
             sys.stdout.buffer.flush()
-            os.remove(tmp_out)
-        for _, e in errs:
-            sys.stderr.buffer.write(e)
-        sys.stderr.buffer.flush()
-    return code
+        if self.rank == 0:
+            for _, e in errs:
+                sys.stderr.buffer.write(e)
+            sys.stderr.buffer.flush()
+        self.base = int(off[-1])
+        self.j += 1
+        if stop != self.BIG:  # the exit code is the fatal item's (its owner's status)
+            self.code = int(self._reduce([owner], dist.ReduceOp.MAX if self.world > 1 else None)[0])
+            self.done = True
+
+    def close(self):
+        """Finish every window; -> the exit code of the single-process run."""
+        self.advance(self.n_total)
+        os.close(self.fd)
+        if self.rd is not None:
+            self.rd.close()
+        if self.tmp_out and self.rank == 0:
+            os.remove(self.tmp_out)
+        return self.code
+
+
+def write_items_at(outs, n_total, out_path, world, rank, dv, tmpdir=None, window=None):
+    """All of this rank's finished batches at once through OffsetWriter (tests, small runs).
+    Returns the exit code of the single-process run."""
+    w = OffsetWriter(n_total, out_path, world, rank, dv, tmpdir, window)
+    for o in outs:
+        w.add(o)
+    return w.close()
 
 
 def main(argv=None) -> int:
@@ -288,7 +355,16 @@ def main(argv=None) -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("PW_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend=backend)
+        # c10d / gloo announce their connections on fd 1: keep that off the report (stdout)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend=backend)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     if world > 1:
         backend = dist.get_backend()
     ndev = torch.cuda.device_count()
@@ -333,8 +409,10 @@ def main(argv=None) -> int:
         except RuntimeError as e:
             made[k] = e
 
+    out_path = opts.get("o") or None
+    writer = OffsetWriter(n_total, out_path, world, rank, dv, extra.get("tmpdir"))
     stream = torch.cuda.current_stream()
-    outs, gtabs = [], {}
+    gtabs = {}
     th = None
     if cuts:
         th = threading.Thread(target=make, args=(0, None))
@@ -358,25 +436,19 @@ def main(argv=None) -> int:
             acc = gtabs.setdefault(nm, np.zeros(3, np.uint64))
             acc += np.array([row[0:4].view("<u4")[0], row[4:8].view("<u4")[0], row[8:16].view("<u8")[0]], np.uint64)
         items = b.items(text_h, res_h, pages_h)
-        outs.append((b, text_h, res_h, pages_h, items))
-        del dev
+        writer.add((b, text_h, res_h, pages_h, items))
+        del dev, b
         if (items[1] >= 0).any():  # a fatal item: nothing after it is reached
             break
+        # ---- 3. the windows this rank's lines so far complete: offsets, pwrites, stderr
+        writer.advance(int(line_no[cuts[k + 1][2]]) if k + 1 < len(cuts) else n_total)
     if th is not None and th.is_alive():
         th.join()
     made.clear()
-    if world > 1:
-        errs = [None] * world
-        dist.all_gather_object(errs, err)
-        err = next((e for e in errs if e), None)
+    writer.err = err
+    code = writer.close()
     if err:
-        if rank == 0:
-            sys.stderr.write(err.split(": ", 1)[-1] if err.startswith("pw_batch_from_buffer") else err)
-        return 1
-
-    # ---- 3-5. stop line, offsets, every rank's pwrite, stderr in line order, exit code
-    out_path = opts.get("o") or None
-    code = write_items_at(outs, n_total, out_path, world, rank, dv, extra.get("tmpdir"))
+        return code
     if "genome-table" in extra:
         names = list(gtabs.keys())
         rows = (np.stack([gtabs[n] for n in names]) if names else np.zeros((0, 3), np.uint64))

@@ -179,3 +179,23 @@ def test_shard_rows_balanced_and_nonempty():
     assert [hi - lo for lo, hi in b] == [1, 1, 1, 1]
     b = shard_rows([5] * 9, 3)
     assert b == [(0, 3), (3, 6), (6, 9)]
+
+
+def test_finish_rows_message_overflow(built, tmp_path, monkeypatch):
+    """pw_ga_rows_finish with a message buffer far too small: the overflowing call must leave every
+    row as it was, so the retry with the reported size applies each row's edits exactly once
+    (a retry on already-edited rows applied removeColumn / refineClipping twice)."""
+    from pwasm_amd import gapassem
+    real = gapassem.finish_rows
+    monkeypatch.setattr(gapassem, "finish_rows", lambda *a, **k: real(*a, **{**k, "msg_cap": 1}))
+    with_msgs = 0
+    for seed in range(10):
+        rng = random.Random(900 + seed)
+        rows = random_layout(rng, 9, clip=True, dels=seed >= 5)
+        lay = tmp_path / f"m{seed}.pwl"
+        write_pwl(lay, rows)
+        for remove in (False, True):
+            want = _oracle(lay, tmp_path, remove)
+            with_msgs += bool(want[1])
+            assert gapassem.consensus(str(lay), remove_gaps=remove, engine=ModelEngine()) == want
+    assert with_msgs > 0  # some row printed a message, so the first call overflowed

@@ -130,15 +130,30 @@ def test_mgpu_cfg3_shards_gene_mode(built, tmp_path):
     assert (rc, out.read_bytes(), err) == (orc, oout, oerr) and orc == 0
 
 
-def test_mgpu_many_batches_per_rank(built, tmp_path):
+@pytest.mark.parametrize("window", [None, "37"])
+def test_mgpu_many_batches_per_rank(built, tmp_path, window):
     """Each rank's lines in several pipelined batches (PW_CHUNK_BYTES): the q~t dedupe state moves
-    from batch to batch, the output offsets span all of them."""
+    from batch to batch, the output offsets span all of them; with PW_WINDOW_LINES the report is
+    written in many windows of global lines while later batches are still being packed."""
     fa, paf = synth_paf(tmp_path, 0, seed=19)
     dup = _with_duplicates_and_comments(paf, tmp_path, 4)
     out = tmp_path / "r.txt"
-    rc, err = run_mgpu(2, ["-r", fa, dup, "-o", str(out)], tmp_path, env={"PW_CHUNK_BYTES": "4000"})
+    env = {"PW_CHUNK_BYTES": "4000", **({"PW_WINDOW_LINES": window} if window else {})}
+    rc, err = run_mgpu(2, ["-r", fa, dup, "-o", str(out)], tmp_path, env=env)
     orc, oout, oerr = run([ORACLE, "-r", fa, dup])
     assert (rc, out.read_bytes(), err) == (orc, oout, oerr)
+
+
+def test_mgpu_stdout_windows_fatal(built, tmp_path):
+    """No -o, small windows, a fatal line two thirds in: rank 0 streams each window to stdout."""
+    fa, paf = synth_paf(tmp_path, 0, seed=41)
+    bad = _inject(paf, tmp_path, "mismatch", seed=5)
+    so = tmp_path / "stdout.txt"
+    rc, err = run_mgpu(3, ["-r", fa, bad], tmp_path,
+                       env={"PW_TEST_STDOUT": str(so), "PW_CHUNK_BYTES": "20000", "PW_WINDOW_LINES": "50"})
+    orc, oout, oerr = run([ORACLE, "-r", fa, bad])
+    assert (rc, err) == (orc, oerr) and orc == 1
+    assert so.read_bytes() == oout
 
 
 def test_mgpu_stdout(built, tmp_path):
@@ -147,9 +162,8 @@ def test_mgpu_stdout(built, tmp_path):
     so = tmp_path / "stdout.txt"
     rc, err = run_mgpu(2, ["-r", fa, paf], tmp_path, env={"PW_TEST_STDOUT": str(so)})
     orc, oout, oerr = run([ORACLE, "-r", fa, paf])
-    # (under gloo, c10d prints "[Gloo] Rank 0 is connected ..." to rank 0's stdout; report lines
-    # start with '>' or an event letter)
-    got = b"".join(ln for ln in so.read_bytes().splitlines(keepends=True) if not ln.startswith(b"[Gloo]"))
+    # (c10d's "[Gloo] Rank 0 is connected ..." goes to stderr: mgpu.main keeps it off stdout)
+    got = so.read_bytes()
     assert (rc, err) == (orc, oerr)
     assert got == oout, f"stdout differs: {len(got)} vs {len(oout)} bytes, first at {_first_diff(got, oout)}"
 

@@ -113,6 +113,17 @@ def _inject(paf, tmp_path, kind, seed):
         j = s.index("*", 5)
         q = s[j + 2]
         f[cs] = s[:j + 2] + ("c" if q != "c" else "g") + s[j + 3:]
+    elif kind in ("mismatch_splice", "star_bad"):
+        # a '*' op (its query base flipped, or clean) right before a '~' / an unknown op byte: the
+        # GPU packer hands the record back, and the host-packed prefix must reach index_kernel
+        # so the first error in cs order is the one reported (pafreport.cpp:545-548, 620-624)
+        s = f[cs]
+        j = s.index("*", 5)
+        q = s[j + 2]
+        if kind == "mismatch_splice":
+            f[cs] = s[:j + 2] + ("c" if q != "c" else "g") + "~gt10ag" + s[j + 3:]
+        else:
+            f[cs] = s[:j + 3] + "Q" + s[j + 3:]
     elif kind == "bounds":
         f[cs] = f[cs] + ":1000000"
     elif kind == "cigar":
@@ -124,7 +135,7 @@ def _inject(paf, tmp_path, kind, seed):
     return out
 
 
-@pytest.mark.parametrize("kind", ["mismatch", "bounds", "cigar"])
+@pytest.mark.parametrize("kind", ["mismatch", "bounds", "cigar", "mismatch_splice", "star_bad"])
 def test_error_midway(built, tmp_path, kind):
     fa, paf = synth_paf(tmp_path, 0, seed=41)
     bad = _inject(paf, tmp_path, kind, seed=5)

@@ -115,7 +115,7 @@ def _paf_with_everything(tmp_path, fatal):
     return fa, str(p)
 
 
-def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q):
+def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
@@ -138,15 +138,23 @@ def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q):
             res = np.zeros(max(int(b.view.n_alns), 1) * 48, np.uint8)
             pages, txt = np.zeros(16, np.uint8), np.zeros(16, np.uint8)
             outs.append((b, txt, res, pages, b.items(txt, res, pages)))
-        code = mgpu.write_items_at(outs, n_total, out_path, world, rank, "cpu")
+        if window is None:
+            code = mgpu.write_items_at(outs, n_total, out_path, world, rank, "cpu")
+        else:  # windows of a few lines, each batch handed over before the windows it completes
+            w = mgpu.OffsetWriter(n_total, out_path, world, rank, "cpu", window=window)
+            for k, o in enumerate(outs):
+                w.add(o)
+                w.advance(int(o[4][0][-1]) + 1 if len(o[4][0]) else 0)
+            code = w.close()
         q.put((rank, code, n_total, [int(x) for x in line_no]))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fatal", [(2, False), (2, True), (3, True)])
-def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal):
+@pytest.mark.parametrize("world,fatal,window", [(2, False, None), (2, True, None), (3, True, None), (2, False, 7),
+                                                (3, True, 5)])
+def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window):
     """mgpu's scalable host path on the CPU (gloo): each rank reads 1/N of the PAF by byte range
     (pw_paf_split), lines are exchanged by target genome (all_to_all_single), packed in several
     batches per rank (the q~t dedupe state carried over), and written at offsets from an
@@ -164,7 +172,8 @@ def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal):
     q = ctx.Queue()
     port = _port()
     out = tmp_path / "got.out"
-    ps = [ctx.Process(target=_exchange_rank, args=(r, world, port, fa, paf, str(out), str(tmp_path / f"e{r}"), q))
+    ps = [ctx.Process(target=_exchange_rank, args=(r, world, port, fa, paf, str(out), str(tmp_path / f"e{r}"), q,
+                                                   window))
           for r in range(world)]
     for p in ps:
         p.start()
