@@ -17,7 +17,7 @@ all: $(LIB) $(CLI) $(GA_CLI) oracle synth
 $(OBJ_DIR):
 	mkdir -p $(OBJ_DIR) pwasm_amd/lib pwasm_amd/bin
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pw_tables.h include/pwasm_amd.h | $(OBJ_DIR)
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pw_tables.h $(SRC_DIR)/pw_wave.h include/pwasm_amd.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
 # the report kernels: the scheduler strategy that clusters memory instructions (same-call sweep:
@@ -25,7 +25,7 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/pw_tables.h include/pwasm_amd.h | $(
 $(OBJ_DIR)/pw_report.o: $(SRC_DIR)/pw_report.hip $(SRC_DIR)/pw_tables.h $(SRC_DIR)/pw_wave.h include/pwasm_amd.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-sched-strategy=max-memory-clause $(INC) -c $< -o $@
 
-$(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp include/pwasm_amd.h include/pwasm_gapassem.hpp $(SRC_DIR)/pw_msa_layout.h | $(OBJ_DIR)
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp $(SRC_DIR)/pw_tables.h include/pwasm_amd.h include/pwasm_gapassem.hpp $(SRC_DIR)/pw_msa_layout.h | $(OBJ_DIR)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle diff + end-to-end CLI run")
     ap.add_argument("--remove-gaps", action="store_true", help="cfg5: MSAColumns::removeConsGaps=true")
     ap.add_argument("--no-e2e", action="store_true", help="N > 1: skip the end-to-end pwasm_amd.mgpu leg")
+    ap.add_argument("--no-gapassem", action="store_true", help="N = 1, cfg2: skip the cfg5 (GapAssem) sub-object")
     ap.add_argument("--e2e-parity", action="store_true", help="N > 1: CRC the end-to-end report against the oracle")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
@@ -76,7 +77,12 @@ def main():
     dev_name = f"cuda:{local}"
     torch.cuda.set_device(local)
     if args.config == 5:
-        return bench_gapassem(args, world, rank, dev_name)
+        out = bench_gapassem(args, world, rank, dev_name)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # ---- data (synthetic, seeded; generated outside the timed region).  cfg3 is ONE 10M-record
     # set: rank r generates exactly the lines of its target-genome shard (crc32(target) % N == r,
@@ -276,7 +282,8 @@ def main():
             cli_ok = p.returncode == 0 and filecmp.cmp(cli_out, want, shallow=False)
             e2e = {"cli_wall_s": round(cli_s, 3), "events_per_s": n_or / cli_s, "parity": "ok" if cli_ok else "FAIL",
                    "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf -o report.txt (PAF text -> report file, "
-                          f"{os.path.getsize(paf)} B in, {os.path.getsize(want)} B out)"}
+                          f"{os.path.getsize(paf)} B in, {os.path.getsize(want)} B out)",
+                   "phases": cli_phases(flags_cli, fa, paf, os.path.join(tmp, "cli2.txt"))}
             if not cli_ok:
                 parity = "FAIL"
             gpack = gpu_pack_check(pw, paf)
@@ -321,6 +328,16 @@ def main():
             "e2e": e2e if e2e is not None else e2e_node,
             "gpu_pack": gpack,
         }
+        if world == 1 and args.config == 2 and not args.no_gapassem:
+            # BASELINE configs[4] beside it, timed in its own region after the cfg2 one (cfg2's
+            # device buffers released first): the GapAssem step, its roofline, parity, CPU baseline
+            del dev
+            torch.cuda.empty_cache()
+            ga = argparse.Namespace(**{**vars(args), "config": 5, "scale": 1.0, "remove_gaps": False,
+                                       "traffic_json": latest_profile(5)})
+            g = bench_gapassem(ga, 1, 0, dev_name)
+            out["gapassem"] = {k: g[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
+                                                 "config", "parity", "roofline", "cpu_baseline")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -460,9 +477,8 @@ def bench_gapassem(args, world, rank, dev_name):
                          "issue_busy": issue_busy(prof, ("pw::tile_counts", "pw::row_chunk_sums"))},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        return out
+    return None
 
 
 def host_cpu():
@@ -582,22 +598,46 @@ def hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp):
         open(fifo, "wb").close()
     th.join()
     batch_ok = rc == 0 and got.get("r") == want[:3]
+    # the drop-in CLI writing its report to a local file (-o), timed alone; CRC-checked afterwards
+    cli_out = os.path.join(tmp, "cli.txt")
     t0 = time.perf_counter()
-    p = subprocess.Popen([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf], stdout=subprocess.PIPE,
-                         stderr=subprocess.DEVNULL)
-    cli = crc_stream(p.stdout)
-    cli_rc = p.wait()
+    cli_rc = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", cli_out],
+                            stderr=subprocess.DEVNULL).returncode
     cli_s = time.perf_counter() - t0
+    with open(cli_out, "rb") as f:
+        cli = crc_stream(f)
+    os.remove(cli_out)
     cli_ok = cli_rc == 0 and cli == want[:3]
     e2e = {"cli_wall_s": round(cli_s, 3), "events_per_s": want[2] / cli_s, "parity": "ok" if cli_ok else "FAIL",
-           "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf > pipe (PAF text -> report stream, "
-                  f"{os.path.getsize(paf)} B in, {cli[1]} B out, CRC-32 checked)"}
+           "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf -o report.txt (PAF text -> report file, "
+                  f"{os.path.getsize(paf)} B in, {cli[1]} B out, CRC-32 checked after the run)"}
     log(f"[parity] batch report {'ok' if batch_ok else 'FAIL'} (crc {got.get('r')} vs {want[:3]}); "
         f"CLI {'ok' if cli_ok else 'FAIL'} {cli_s:.1f}s")
     parity = {"result": "ok" if batch_ok and cli_ok else "FAIL", "method": "CRC-32 + bytes + events, streamed",
               "oracle": f"oracle/pafreport_oracle over {host_threads() * 4} byte ranges, {host_threads()} processes, "
                         f"{want[3]:.1f}s", "bytes": want[1], "crc32": f"{want[0]:08x}"}
     return parity, e2e, want[2]
+
+
+def cli_phases(flags_cli, fa, paf, outp):
+    """A second CLI run with PW_PROFILE_HOST=1: its own phase timestamps (FASTA load, first batch read
+    + pack, device init, per batch GPU run + result copies and emit, total), parsed from stderr."""
+    import re
+    env = {**os.environ, "PW_PROFILE_HOST": "1"}
+    p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", outp],
+                       stderr=subprocess.PIPE, env=env)
+    ph = {}
+    for ln in p.stderr.decode(errors="replace").splitlines():
+        if not ln.startswith("[cli]"):
+            continue
+        for name, val in re.findall(r"([a-z][a-z +()\-]*?) ([0-9.]+) s", ln[5:]):
+            key = re.sub(r"[^a-z0-9]+", "_", name.strip()).strip("_")
+            ph[key] = round(ph.get(key, 0.0) + float(val), 4)
+    try:
+        os.remove(outp)
+    except OSError:
+        pass
+    return ph or None
 
 
 def host_threads():

@@ -24,9 +24,11 @@
 //                   already in OUTPUT order ('-' records fill their slots back to front =
 //                   tdiffs.Reverse(), :643).  Events whose target context needs an op walk are
 //                   flagged for tctx_kernel.
-//  tctx_kernel      a wavefront takes 256 slots, compacts the flagged ones by ballot and walks
-//                   each one's op stream through LDS windows (setTContext, :120-128): a 32-byte
-//                   pre-rendered target-context record.
+//  tctx_kernel      a wavefront scans the flag bytes of its 256-slot groups (one group ahead),
+//                   queues the flagged slots in an LDS list that carries across groups, and takes
+//                   them 64 at a time, one event per lane: the lane walks its op stream through
+//                   LDS windows (setTContext, :120-128) and writes a 32-byte pre-rendered
+//                   target-context record.
 //  render_kernel    lane-dense: wavefront g takes chunks g, g + NW, ... of 64 consecutive event
 //                   slots (static stride, no work queue); each lane renders its event's report
 //                   line into an LDS line buffer from its Hot record and a 48-byte forward-query
