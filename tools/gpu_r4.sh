@@ -1,0 +1,16 @@
+#!/bin/bash
+# On the GPU box: the GPU test suite, the default bench line (cfg2 + the cfg5 sub-object), then the
+# large configs at HEAD (tools/gpu_big.sh: full cfg3, cfg4 >= 1,024 records, kernel traces).
+# Usage: bash tools/gpu_r4.sh <tag> [cfg4 scale] [skip-tests]
+set -uo pipefail
+TAG=${1:-r4}
+S4=${2:-0.11}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+if [ "${3:-}" != "skip-tests" ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest failed: $?"; tail -60 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+  tail -3 gpurun_out/pytest_gpu_$TAG.log
+fi
+timeout -k 10 400 python3 -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed: $?"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+bash tools/gpu_big.sh $TAG $S4
