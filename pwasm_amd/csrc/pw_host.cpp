@@ -11,6 +11,7 @@
 #include <string.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <sched.h>
@@ -1598,6 +1599,142 @@ int emit(const Batch& b, const TextSrc& text, const pw_aln_result* res, const pw
   return -1;
 }
 
+// Parallel emit of a batch into a regular output file (-o): when no item of the batch ends the
+// run or prints a partial record, every stdout byte's file offset is known up front (headers on
+// the host, lines in the device text pages), so the batch is written as pieces — each record's
+// header, then its page spans — by `nt` threads with pwritev at their offsets, window by window of
+// the page region as the pinned TextStream windows arrive (the DMA of window k + 2 runs while
+// window k + 1 is written); stderr lines are printed in item order by this thread.  The FILE's
+// position is moved past the batch afterwards.  Returns -1 (continue) when done, -2 when the batch
+// needs the sequential emit (a fatal item, a partial record, a -w message), -3 on a write error.
+int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, const pw_page* pages, FILE* out, int nt) {
+  for (const LogItem& it : b.log) {
+    if (it.kind == 2) return -2;
+    if (it.kind != 1) continue;
+    const RecHost& rh = b.recs[it.idx];
+    const pw_aln_result& r = res[it.idx];
+    if (rh.pre_msg >= 0 || r.err != 0 || rh.cs_msg >= 0 || rh.post_msg >= 0 || rh.w_msg >= 0 ||
+        (rh.qlen < 9 && r.n_events > 0))
+      return -2;
+  }
+  if (fflush(out) != 0) return -3;
+  const int fd = fileno(out);
+  const off_t base = lseek(fd, 0, SEEK_CUR);
+  if (base < 0) return -2;
+  // pieces in output order: a host source (headers, arena pages) or a page-region offset
+  struct Piece {
+    const uint8_t* host;
+    uint64_t src, len, dst;
+    int64_t win;  // page-region window of the source (-1: on the host)
+  };
+  std::vector<Piece> pc;
+  pc.reserve(b.log.size() * 3);
+  uint64_t dst = 0;
+  for (const LogItem& it : b.log) {
+    if (it.kind == 0) continue;
+    const RecHost& rh = b.recs[it.idx];
+    const pw_aln_result& r = res[it.idx];
+    pc.push_back({(const uint8_t*)b.hdr.data() + rh.hdr_off, 0, rh.hdr_len, dst, -1});
+    dst += rh.hdr_len;
+    if (r.n_events == 0) continue;
+    for (uint32_t c = r.page_first;; c++) {
+      const uint64_t lo = c == r.page_first ? r.text_off : pages[c].off;
+      const uint64_t hi = c == r.page_last ? r.text_end : pages[c].off + pages[c].len;
+      if (hi > lo) {
+        if (lo >= ts.arena0) pc.push_back({ts.arena.data() + (lo - ts.arena0), 0, hi - lo, dst, -1});
+        else pc.push_back({nullptr, lo, hi - lo, dst, (int64_t)(lo / TextStream::kWin)});
+        dst += hi - lo;
+      }
+      if (c == r.page_last) break;
+    }
+  }
+  // host pieces go with the window of the next page-region piece (page-region sources increase
+  // along the list; pages never straddle a window)
+  int64_t next = 0;
+  for (const Piece& p : pc) next = std::max(next, p.win);
+  for (size_t i = pc.size(); i-- > 0;) {
+    if (pc[i].win >= 0) next = pc[i].win;
+    else pc[i].win = next;
+  }
+  for (size_t i = 1; i < pc.size(); i++)
+    if (pc[i].win < pc[i - 1].win) return -2;  // (not monotone: cannot happen; keep the sequential path)
+  for (const LogItem& it : b.log) {  // stderr, in item order
+    if (it.kind == 0) {
+      fputs(b.msgs[it.idx].c_str(), stderr);
+      continue;
+    }
+    const RecHost& rh = b.recs[it.idx];
+    for (int k = 0; k < rh.n_softclip; k++)
+      fprintf(stderr, "Warning: soft clipping shouldn't be found in this application!\n%s\n",
+              b.buf.data() + rh.line_off);
+  }
+  const int64_t nwin = pc.empty() ? 0 : pc.back().win + 1;
+  std::atomic<bool> bad{false};
+  size_t i0 = 0;
+  for (int64_t w = 0; w < nwin; w++) {
+    size_t i1 = i0;
+    while (i1 < pc.size() && pc[i1].win == w) i1++;
+    const int slot = (int)(w & 1);
+    const uint64_t wlo = (uint64_t)w * TextStream::kWin;
+    const bool dma = wlo < ts.region_end;
+    if (dma) {
+      if (ts.base[slot] != wlo) return -3;  // (windows are consumed in order)
+      (void)hipEventSynchronize(ts.ev[slot]);
+    }
+    const uint8_t* wb = ts.buf[slot];
+    if (i1 > i0) {
+      const uint64_t d0 = pc[i0].dst, d1 = pc[i1 - 1].dst + pc[i1 - 1].len;
+      const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(nt, 1), (d1 - d0) >> 20));
+      auto work = [&](int t) {  // the pieces whose destination starts in this thread's byte range
+        const uint64_t a = d0 + (d1 - d0) * (uint64_t)t / (uint64_t)T;
+        const uint64_t z = d0 + (d1 - d0) * (uint64_t)(t + 1) / (uint64_t)T;
+        size_t j = (size_t)(std::lower_bound(pc.begin() + (long)i0, pc.begin() + (long)i1, a,
+                                             [](const Piece& p, uint64_t v) { return p.dst < v; }) -
+                            pc.begin());
+        iovec iov[256];
+        while (j < i1 && pc[j].dst < z) {
+          int n = 0;
+          const uint64_t at = pc[j].dst;
+          uint64_t len = 0;
+          for (; n < 256 && j < i1 && pc[j].dst < z; n++, j++) {
+            iov[n].iov_base = (void*)(pc[j].host ? pc[j].host : wb + (pc[j].src - wlo));
+            iov[n].iov_len = pc[j].len;
+            len += pc[j].len;
+          }
+          uint64_t done = 0;
+          int q0 = 0;
+          while (done < len) {  // (short writes: resume inside the vector)
+            const ssize_t k = pwritev(fd, iov + q0, n - q0, base + (off_t)(at + done));
+            if (k <= 0) {
+              bad = true;
+              return;
+            }
+            done += (uint64_t)k;
+            uint64_t m = (uint64_t)k;
+            while (q0 < n && m >= iov[q0].iov_len) m -= iov[q0++].iov_len;
+            if (q0 < n) {
+              iov[q0].iov_base = (uint8_t*)iov[q0].iov_base + m;
+              iov[q0].iov_len -= m;
+            }
+          }
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < T; t++) th.emplace_back(work, t);
+      work(0);
+      for (auto& x : th) x.join();
+    }
+    if (dma) {  // this window's buffer takes window w + 2
+      ts.base[slot] += 2 * TextStream::kWin;
+      ts.fetch(slot);
+    }
+    i0 = i1;
+  }
+  if (bad) return -3;
+  if (fseeko(out, base + (off_t)dst, SEEK_SET) != 0) return -3;
+  return -1;
+}
+
 #define USAGE                                                             \
   "Usage:\n\
  pafreport <paf_with_cg_cs> -r <refseq.fa> [-s <summary.txt>]\n\
@@ -1811,6 +1948,13 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     pk.pack(B);
     return true;
   };
+  // -o into a regular file: batches without a fatal item are written by pk.nt threads at known
+  // offsets (emit_parallel); PW_SERIAL_EMIT=1 keeps the sequential stdio emit
+  bool par_emit = false;
+  if (out.f != stdout && !(getenv("PW_SERIAL_EMIT") && atoi(getenv("PW_SERIAL_EMIT")) != 0)) {
+    struct stat os;
+    par_emit = fstat(fileno(out.f), &os) == 0 && S_ISREG(os.st_mode);
+  }
   int cur = 0;
   bool have = pack_next(bb[0]);
   const double t_pack0 = prof ? now() : 0;
@@ -1834,7 +1978,16 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     const double t_r1 = prof ? now() : 0;
     TextSrc src;
     src.stream = &tstream;
-    const int rc = ran ? emit(B, src, res_h.data(), pages_h.data(), out.f) : 2;
+    int rc = 2;
+    if (ran) {
+      rc = par_emit ? emit_parallel(B, tstream, res_h.data(), pages_h.data(), out.f, pk.nt) : -2;
+      if (rc == -3) {
+        fprintf(stderr, "pafreport: error writing the report\n");
+        rc = 2;
+      } else if (rc == -2) {
+        rc = emit(B, src, res_h.data(), pages_h.data(), out.f);
+      }
+    }
     tstream.end();
     if (prof)
       fprintf(stderr, "[cli] batch: gpu run + result copies %.3f s, emit (text streamed) %.3f s\n", t_r1 - t_r0,

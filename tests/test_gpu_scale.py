@@ -304,15 +304,18 @@ def test_cli_many_batches(built, tmp_path, chunk, kind, monkeypatch):
 
 
 @pytest.mark.parametrize("chunk,kind", [(None, None), (3000, None), (20000, "dups"), (5000, "mismatch"),
-                                        (None, "cfg2")])
+                                        (None, "cfg2"), (None, "long"), (60000, "long")])
 def test_cli_output_file(built, tmp_path, chunk, kind, monkeypatch):
     """-o to a regular file (a stale longer file is truncated), one batch or many, clean batches and
     batches with messages / a fatal record: same bytes, stderr and exit code as the oracle."""
     from test_gpu_parity import _inject
     from test_shard import _with_duplicates_and_comments
-    if kind == "cfg2":
-        fa, paf = synth_paf(tmp_path, 2, seed=31, scale=0.2)
+    if kind == "cfg2":  # (~90 MB of report: three pinned text windows, written by threads at offsets)
+        fa, paf = synth_paf(tmp_path, 2, seed=31, scale=0.3)
         flags = ["-G", "-C"]
+    elif kind == "long":  # long lines (fixup_kernel) and pages that overflow into the arena
+        fa, paf = synth_paf(tmp_path, 0, seed=21, extra=["--longindel", 0.5, "--subrun", 0.6, "--err", 0.05])
+        flags = []
     else:
         fa, paf = synth_paf(tmp_path, 0, seed=29)
         flags = []

@@ -1,0 +1,61 @@
+"""Experiment variants of pw_msa.hip for attributing tile_counts' time and LDS bank conflicts
+(never shipped; timing only — the counting variants give wrong counts, parity FAILs by design):
+  cur      the product source
+  noflush  the LDS counter-table flush (cnt_flush) never runs (counters still accumulated)
+  nowin    the row window is not stored to LDS (loads kept, reads see a stale window)
+  noruns   the gap-run ORs into the bitmap are skipped
+  rp_lds   tools/variants/row_prefix_lds.patch (row_prefix stages the row's runs in LDS)
+Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "pwasm_amd/csrc/pw_msa.hip")
+TMP = os.path.join(REPO, "build_exp")
+
+
+def sub(s, old, new):
+    assert old in s, old
+    return s.replace(old, new)
+
+
+def make(name):
+    s = open(SRC).read()
+    if name == "noflush":
+        s = sub(s, "if (last || nrow == kFlushRows) {", "if ((last || nrow == kFlushRows) && A.n_cols < 0) {")
+    elif name == "nowin":
+        s = sub(s, """        LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+        w4[lane] = cc.w0;
+        w4[64 + lane] = cc.w1;
+        if (lane < 8) w4[128 + lane] = cc.w2;
+      }
+      RowC cn;""", """        LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+        if (A.n_cols < 0) {
+        w4[lane] = cc.w0;
+        w4[64 + lane] = cc.w1;
+        if (lane < 8) w4[128 + lane] = cc.w2;
+        }
+      }
+      RowC cn;""")
+    elif name == "noruns":
+        s = sub(s, "            if (v != 0u) {\n              const int s = max(ck",
+                "            if (v != 0u && A.n_cols < 0) {\n              const int s = max(ck")
+    elif name == "rp_lds":
+        os.makedirs(TMP, exist_ok=True)
+        p = os.path.join(TMP, "rp_lds.hip")
+        open(p, "w").write(s)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_prefix_lds.patch")], check=True)
+        s = open(p).read()
+    elif name != "cur":
+        raise SystemExit(f"unknown variant {name}")
+    os.makedirs(TMP, exist_ok=True)
+    p = os.path.join(TMP, f"{name}.hip")
+    open(p, "w").write(s)
+    return p
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or ["cur", "noflush", "nowin", "noruns", "rp_lds"]
+    args = [f"{n}={make(n)}" for n in names]
+    subprocess.run([sys.executable, os.path.join(REPO, "tools/exp_msa.py"), *args], check=True)

@@ -1,0 +1,7 @@
+"""Print the pw:: rows of a rocprofv3 kernel_stats.csv: name and average µs.  Usage: kstat.py <csv>"""
+import csv
+import sys
+
+for r in csv.DictReader(open(sys.argv[1])):
+    if r["Name"].startswith("pw::"):
+        print(f"   {r['Name'].split('(')[0]:28s} {float(r['AverageNs']) / 1000:9.1f} us")
