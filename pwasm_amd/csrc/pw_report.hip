@@ -1026,6 +1026,373 @@ __device__ __forceinline__ int emit_event(S& k, const R& r, const EvIn& in, bool
   return modseq_err;
 }
 
+// ------------------------------------------------------------------ render fast path: dword lines
+// The RecFast case of emit_event (every read in registers or the lane's query window, A/C/G/T,
+// numbers below 10^8) restated with register images: each field is composed in VGPRs (numbers by
+// SWAR decimal conversion, bases from the literal registers or the window, codons by one multiply
+// per codon index) and appended to the lane's line buffer as whole dwords — the partial dword at
+// the line end is read back and merged with v_perm, so a 16-byte field costs one read, five perms
+// and three stores instead of sixteen byte stores.  Same bytes as emit_event (pafreport.cpp:886-953).
+struct DLine {
+  LDS uint8_t* buf;  // the lane's line buffer (4-byte aligned, kLine + kLSlack bytes)
+  int pos;
+};
+// (a line that grows past kLine is rewritten by fixup_kernel: its appends are folded onto the slack)
+constexpr int kAppMax = kLine & ~3;
+// append bytes [0, n) of f (4D bytes; bytes past n may be anything) at the line end
+template <int D>
+__device__ __forceinline__ void app(DLine& L, const uint32_t (&f)[D], int n) {
+  const int p = L.pos;
+  const int a = min(p & ~3, kAppMax);
+  const uint32_t sh = (uint32_t)p & 3u;
+  LDS uint32_t* d = reinterpret_cast<LDS uint32_t*>(L.buf + a);
+  const uint32_t cur = d[0];  // bytes [a, p) of the line
+  // result byte j of dword i = stream byte 4i + j - sh: selector 4 - sh + j over {f[i], f[i - 1]};
+  // dword 0 keeps its first sh bytes from cur
+  const uint32_t sel = 0x07060504u - 0x01010101u * sh;
+  const uint32_t m = (uint32_t)((1ull << (8 * sh)) - 1ull);
+  const uint32_t sel0 = (sel & ~m) | (0x03020100u & m);
+  uint32_t g[D + 1];
+  g[0] = __builtin_amdgcn_perm(f[0], cur, sel0);
+#pragma unroll
+  for (int i = 1; i < D; i++) g[i] = __builtin_amdgcn_perm(f[i], f[i - 1], sel);
+  g[D] = __builtin_amdgcn_perm(0u, f[D - 1], sel);
+#pragma unroll
+  for (int i = 0; i <= D; i++) d[i] = g[i];
+  L.pos = p + n;
+}
+// OR the bytes of w into img at byte offset k (k + the bytes w uses <= 4N)
+template <int N>
+__device__ __forceinline__ void or_at(uint32_t (&img)[N], uint32_t w, int k) {
+  const uint64_t v = (uint64_t)w << (8 * (k & 3));
+  const int q = k >> 2;
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int i = 0; i < N; i++) img[i] |= (q == i ? lo : 0u) | (q == i - 1 ? hi : 0u);
+}
+__device__ __forceinline__ uint32_t keep32(uint32_t v, int n) {  // bytes [0, n) of v (n clamped to [0, 4])
+  return n >= 4 ? v : (n <= 0 ? 0u : (v & ((1u << (8 * n)) - 1u)));
+}
+__device__ __forceinline__ uint64_t keep64(uint64_t v, int n) {  // bytes [0, n) of v (n clamped to [0, 8])
+  return n >= 8 ? v : (n <= 0 ? 0ull : (v & ((1ull << (8 * n)) - 1ull)));
+}
+// N dwords of an LDS window from byte offset off (off >= 0; reads one dword past them)
+template <int N>
+__device__ __forceinline__ void lds_img(const LDS uint8_t* qw, int off, uint32_t (&o)[N]) {
+  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
+  const uint32_t sh = (uint32_t)off & 3u;
+  uint32_t d[N + 1];
+#pragma unroll
+  for (int i = 0; i <= N; i++) d[i] = p[i];
+#pragma unroll
+  for (int i = 0; i < N; i++) o[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+}
+// "%u" of v < 10^8 by SWAR: two 4-digit halves, each split into 2-digit pairs (x / 100 =
+// x * 5243 >> 19) and tens (y * 103 >> 10) — the digits in memory order in lo | hi << 32, nd of them
+struct Num {
+  uint32_t lo, hi;
+  int nd;
+};
+__device__ __forceinline__ uint32_t dig4(uint32_t x) {  // x < 10^4 -> 4 digit values, first in byte 0
+  const uint32_t q = (x * 5243u) >> 19;
+  const uint32_t p = q | (x - 100u * q) << 16;
+  const uint32_t t = ((p * 103u) >> 10) & 0x000F000Fu;
+  return t | (p - 10u * t) << 8;
+}
+__device__ __forceinline__ Num fmt8(uint32_t v) {
+  const uint32_t h = __umulhi(v, 3518437209u) >> 13;  // v / 10^4 (exact for v < 10^8)
+  const uint64_t raw = (uint64_t)dig4(h) | (uint64_t)dig4(v - 10000u * h) << 32;
+  const uint32_t lo = (uint32_t)raw, hi = (uint32_t)(raw >> 32);
+  // leading zero digits = trailing zero bytes of raw (at least one digit stays)
+  int z = (lo ? __builtin_ctz(lo) : 32 + (hi ? __builtin_ctz(hi) : 32)) >> 3;
+  z = z > 7 ? 7 : z;
+  const uint64_t s = (raw + 0x3030303030303030ull) >> (8 * z);
+  Num r;
+  r.lo = (uint32_t)s;
+  r.hi = (uint32_t)(s >> 32);
+  r.nd = 8 - z;
+  return r;
+}
+// codon64 index of the three bases in bytes 0-2 of w (A/C/G/T: code (c >> 1) & 3)
+__device__ __forceinline__ uint32_t cidx(uint32_t w) {
+  const uint32_t c = (w >> 1) & 0x00030303u;
+  return ((c * 0x00100401u) >> 16) & 63u;
+}
+// constant text as dwords
+template <int N>
+struct Txt {
+  uint32_t w[(N + 2) / 4];
+};
+template <int N>
+__host__ __device__ constexpr Txt<N> txt(const char (&s)[N]) {
+  Txt<N> t{};
+  for (int i = 0; i < N - 1; i++) t.w[i >> 2] |= (uint32_t)(uint8_t)s[i] << (8 * (i & 3));
+  return t;
+}
+
+// One event's line (the fast case); returns the modseq error index (S) or -1, rel as emit_event.
+__device__ __forceinline__ int emit_fast(DLine& L, const LDS uint8_t* qw, int qlo, const LDS SmallTables* tab,
+                                         const EvIn& in, bool rev, int Lq, uint32_t l0, uint32_t l1,
+                                         const int32_t* NS, bool skip, int& rel) {
+  const uint32_t typ = in.typ;
+  const int n = in.n;
+  const bool isS = typ == PW_OP_SUB, isI = typ == PW_OP_INS, isD = typ == PW_OP_DEL;
+  const int rloc = event_rloc(Lq, rev, typ, in.qp, n);
+  const int aap0 = rloc / 3;
+  const int rt = 3 * (aap0 - 1);  // r_trloc (rloc >= 8 here)
+  rel = rloc - rt;
+  const uint64_t l64 = (uint64_t)l1 << 32 | l0;
+  const LDS uint8_t* c64 = tab->codon64;
+
+  // ---- "E\trloc\taapos(aa)\t" (pafreport.cpp:897-899, 918)
+  {
+    uint32_t aw[1];
+    lds_img(qw, 3 * aap0 - qlo, aw);
+    const uint32_t aa = c64[cidx(aw[0])];
+    const Num a1 = fmt8((uint32_t)rloc + 1u);
+    const uint32_t tc = isS ? 'S' : (isI ? 'I' : 'D');
+    uint32_t f1[3] = {tc | (uint32_t)'\t' << 8 | a1.lo << 16, a1.lo >> 16 | a1.hi << 16, a1.hi >> 16};
+    or_at(f1, '\t', 2 + a1.nd);
+    app(L, f1, 3 + a1.nd);
+    const Num a2 = fmt8((uint32_t)aap0 + 1u);
+    uint32_t f2[3] = {a2.lo, a2.hi, 0u};
+    or_at(f2, (uint32_t)'(' | aa << 8 | (uint32_t)')' << 16 | (uint32_t)'\t' << 24, a2.nd);
+    app(L, f2, a2.nd + 4);
+  }
+  // ---- bases ("SUB:BASES", ":INS", "DEL:"), evtbases in final orientation (:563, 594-596,
+  // 612-614, 637, 928-941); b0 / same for hpolyCheck
+  uint32_t alt = 0, sub = 0;
+  uint32_t b0;
+  bool same;
+  if (isS) {  // (target, query) literal pairs
+    alt = pack_even4(l64);
+    sub = pack_even4(l64 >> 8);
+    if (rev) {
+      alt = (uint32_t)comp_acgt8(__builtin_bswap32(alt) >> (8 * (4 - n)));
+      sub = (uint32_t)comp_acgt8(__builtin_bswap32(sub) >> (8 * (4 - n)));
+    }
+    alt = keep32(alt, n);
+    sub = keep32(sub, n);
+    b0 = alt & 0xFFu;
+    same = keep32(alt ^ (b0 * 0x01010101u), n) == 0u;
+    const uint64_t s1 = (uint64_t)sub | (uint64_t)':' << (8 * n), s2 = (uint64_t)alt | (uint64_t)'\t' << (8 * n);
+    const uint32_t g1[2] = {(uint32_t)s1, (uint32_t)(s1 >> 32)}, g2[2] = {(uint32_t)s2, (uint32_t)(s2 >> 32)};
+    app(L, g1, n + 1);
+    app(L, g2, n + 1);
+  } else if (isI) {  // inserted target bases
+    const uint64_t b = keep64(rev ? comp_acgt8(__builtin_bswap64(l64) >> (8 * (8 - n))) : l64, n);
+    b0 = (uint32_t)b & 0xFFu;
+    same = keep64(b ^ (b0 * 0x0101010101010101ull), n) == 0ull;
+    const uint32_t blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+    uint32_t g[3] = {(uint32_t)':' | blo << 8, blo >> 24 | bhi << 8, bhi >> 24};
+    or_at(g, '\t', n + 1);
+    app(L, g, n + 2);
+  } else {  // deleted query bases, Q[rloc, rloc + n) on either strand (comp2 is the identity on A/C/G/T)
+    uint32_t w[3];
+    lds_img(qw, rloc - qlo, w);
+    uint32_t g[4] = {w[0], w[1], w[2], 0u};
+    b0 = g[0] & 0xFFu;
+    const uint32_t bb = b0 * 0x01010101u;
+    same = keep32(g[0] ^ bb, n) == 0u && keep32(g[1] ^ bb, n - 4) == 0u && keep32(g[2] ^ bb, n - 8) == 0u;
+    g[0] = keep32(g[0], n);
+    g[1] = n > 4 ? keep32(g[1], n - 4) : 0u;
+    g[2] = n > 8 ? keep32(g[2], n - 8) : 0u;
+    or_at(g, (uint32_t)':' | (uint32_t)'\t' << 8, n);
+    app(L, g, n + 2);
+  }
+  {  // ---- tloc + 1
+    const Num a4 = fmt8((uint32_t)in.tloc + 1u);
+    uint32_t f4[3] = {a4.lo, a4.hi, 0u};
+    or_at(f4, '\t', a4.nd);
+    app(L, f4, a4.nd + 1);
+  }
+  // ---- target context (setTContext :120-128, revCompl :631): fast form or the tx record
+  if (in.tmode == 0) {
+    const int nm = isD ? 0 : (isS ? 1 : n);
+    const int qpa = in.qp + (isS ? 1 : (isD ? n : 0));
+    const int f1 = rev ? Lq - qpa - in.rl : in.qp - in.ll, n1 = rev ? in.rl : in.ll;
+    const int f2 = rev ? Lq - in.qp : qpa, n2 = rev ? in.ll : in.rl;
+    uint32_t a[2], b[2];
+    lds_img(qw, f1 - qlo, a);
+    lds_img(qw, f2 - qlo, b);
+    uint64_t mv = isS ? (l64 & 0xFFull) : l64;
+    if (rev) mv = nm > 0 ? comp_acgt8(__builtin_bswap64(mv) >> (8 * (8 - nm))) : 0ull;
+    mv |= 0x2020202020202020ull;
+    const uint32_t g[2] = {(uint32_t)mv, (uint32_t)(mv >> 32)};
+    app(L, a, n1);
+    app(L, g, nm);
+    app(L, b, n2);
+  } else {  // length byte + field
+    const uint32_t t[7] = {in.tx[0], in.tx[1], in.tx[2], in.tx[3], in.tx[4], in.tx[5], 0u};
+    uint32_t g[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) g[i] = __builtin_amdgcn_alignbyte(t[i + 1], t[i], 1u);
+    app(L, g, (int)(in.tx[0] & 0xFFu));
+  }
+  // ---- "\tRCTX\tstatus" (getRefContext :721-733, hpolyCheck :735-748, mmotifCheck :751-763)
+  {
+    int c0 = rloc - 4, eloc = 4;
+    if (c0 + 8 >= Lq) {
+      eloc += Lq - c0 - 9;
+      c0 = Lq - 9;
+    }
+    uint32_t rw[3];
+    lds_img(qw, c0 - qlo, rw);
+    const uint32_t rw2 = rw[2] & 0xFFu;
+    const uint64_t lo = (uint64_t)rw[0] | ((uint64_t)rw[1] << 32);
+    int l = -1;
+    bool m0 = false, m1 = false, m2 = false, m3 = false;
+#pragma unroll
+    for (int p = 5; p >= 0; p--) {
+      const uint32_t v4 = p <= 4 ? (uint32_t)(lo >> (8 * p)) : ((rw[1] >> 8) | (rw2 << 24));
+      const uint32_t c4 = p < 4 ? (uint32_t)(lo >> (8 * (p + 4))) & 0xFFu : (p == 4 ? rw2 : 0u);
+      if (v4 == 0x01010101u * b0) l = p;
+      m0 = m0 || (v4 == 0x47544343u && c4 == 'G');  // "CCTGG"
+      m1 = m1 || (v4 == 0x47414343u && c4 == 'G');  // "CCAGG"
+      m2 = m2 || v4 == 0x43544147u;                 // "GATC"
+      m3 = m3 || v4 == 0x43415447u;                 // "GTAC"
+    }
+    const int st = (same && l >= 0 && l <= eloc && l + 4 >= eloc) ? 1 : (m0 ? 2 : (m1 ? 3 : (m2 ? 4 : (m3 ? 5 : 0))));
+    const uint32_t f6[3] = {(uint32_t)'\t' | rw[0] << 8, rw[0] >> 24 | rw[1] << 8,
+                            rw[1] >> 24 | rw2 << 8 | (uint32_t)'\t' << 16};
+    app(L, f6, 11);
+    const LDS uint32_t* sw = reinterpret_cast<const LDS uint32_t*>(tab->status[st]);
+    const uint32_t sv[3] = {sw[0], sw[1], sw[2]};
+    app(L, sv, (int)(sv[2] >> 24));
+  }
+  // ---- codon consequence (predictImpact, pafreport.cpp:801-883)
+  int merr = -1;
+  if (skip) {
+    const uint32_t e[1] = {(uint32_t)'\t' | (uint32_t)'\n' << 8};
+    app(L, e, 2);
+    return -1;
+  }
+  if (isS) {  // codons ao = 1, 2 of modseq (r_trloc + 3 .. + 8): bytes 3-10 of Q[r_trloc ..] in t
+    uint32_t q[3];
+    lds_img(qw, rt - qlo, q);
+    const uint64_t t = (uint64_t)(q[0] >> 24) | (uint64_t)q[1] << 8 | (uint64_t)q[2] << 40;
+    const int sh = 8 * (rel - 3);  // evtbases at modseq byte rel (3..5)
+    const uint32_t nmask = keep32(0xFFFFFFFFu, n);
+    const uint32_t diff = ((uint32_t)(t >> sh) ^ sub) & nmask;  // modseq check (:811-814)
+    merr = diff ? (int)(__builtin_ctz(diff) >> 3) : -1;
+    const uint64_t mt = (t & ~((uint64_t)nmask << sh)) | ((uint64_t)alt << sh);
+    const uint32_t caa1 = c64[cidx((uint32_t)t)], cmaa1 = c64[cidx((uint32_t)mt)];
+    const uint32_t caa2 = c64[cidx((uint32_t)(t >> 24))], cmaa2 = c64[cidx((uint32_t)(mt >> 24))];
+    const bool ch1 = caa1 != cmaa1, ch2 = rel + n - 1 >= 6 && caa2 != cmaa2;
+    if (!ch1 && !ch2) {
+      constexpr Txt<13> syn = txt("\tsynonymous\n");
+      app(L, syn.w, 12);
+      return merr;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const bool ch = k == 0 ? ch1 : ch2;
+      if (!ch) continue;
+      const uint32_t caa = k == 0 ? caa1 : caa2, cmaa = k == 0 ? cmaa1 : cmaa2;
+      const bool first = k == 0 || !ch1;
+      const uint32_t pf[1] = {first ? 0x0041'4109u : 0x4141'202Cu};  // "\tAA" / ", AA"
+      app(L, pf, first ? 3 : 4);
+      const Num an = fmt8((uint32_t)(aap0 + 1 + k));  // ap = ao + rloc / 3
+      uint32_t g[3] = {an.lo, an.hi, 0u};
+      or_at(g, (uint32_t)'|' | caa << 8 | (uint32_t)':' << 16 | cmaa << 24, an.nd);
+      app(L, g, an.nd + 4);
+      if (cmaa == '.') {
+        constexpr Txt<22> ps = txt("|premature stop at AA");
+        app(L, ps.w, 21);
+        const uint32_t d[2] = {an.lo, an.hi};
+        app(L, d, an.nd);
+      }
+    }
+    const uint32_t e[1] = {'\n'};
+    app(L, e, 1);
+    return merr;
+  }
+  // indel: modseq = Q[r_trloc, rloc) + X + Q[rloc + dl, ..), codons 0-4 and reference codons 1-4
+  const int a = rel;
+  const int x = isI ? n : 0, dl = isD ? n : 0;
+  const int sfx = rloc + dl;
+  const int M = (Lq - rt) + x - dl;
+  const int trlen = Lq - rt;
+  uint32_t q0[4], q1[4];
+  lds_img(qw, rt - qlo, q0);
+  lds_img(qw, rt - qlo + dl - x, q1);
+  const uint64_t X = isI ? keep64(rev ? comp_acgt8(__builtin_bswap64(l64) >> (8 * (8 - x))) : l64, x) : 0ull;
+  // X << 8a over four dwords (a = 3..5)
+  const uint32_t xs[4] = {(uint32_t)(X << (8 * a)), (uint32_t)((X << (8 * a)) >> 32), (uint32_t)(X >> (64 - 8 * a)),
+                          a == 5 ? (uint32_t)(X >> 56) : 0u};
+  uint32_t mw[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int ca = min(max(a - 4 * i, 0), 4), cx = min(max(a + x - 4 * i, 0), 4);
+    const uint32_t ma = (uint32_t)((1ull << (8 * ca)) - 1ull), mx = (uint32_t)((1ull << (8 * cx)) - 1ull) & ~ma;
+    mw[i] = (q0[i] & ma) | (xs[i] & mx) | (q1[i] & ~(ma | mx));
+  }
+  uint32_t mm[5], rr[5];
+  {
+    const uint32_t mc[5] = {mw[0], __builtin_amdgcn_alignbyte(mw[1], mw[0], 3u),
+                            __builtin_amdgcn_alignbyte(mw[2], mw[1], 2u), mw[2] >> 8, mw[3]};
+    const uint32_t rc[5] = {0u, __builtin_amdgcn_alignbyte(q0[1], q0[0], 3u),
+                            __builtin_amdgcn_alignbyte(q0[2], q0[1], 2u), q0[2] >> 8, q0[3]};
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+      mm[c] = c64[cidx(mc[c])];
+      rr[c] = c == 0 ? 0u : (uint32_t)c64[cidx(rc[c])];
+    }
+  }
+  // (bytes past the query end are the zero padding: they only reach codons the scan does not use)
+  int stopc = 5, nvalid = 0;
+#pragma unroll
+  for (int c = 4; c >= 0; c--) {
+    const bool valid = 3 * c + 2 < M;
+    if (valid && mm[c] == '.') stopc = c;
+    nvalid += valid ? 1 : 0;
+  }
+  const int last = stopc < nvalid ? stopc : nvalid;
+  uint32_t aa4 = 0, maa4 = 0;
+  int aa4n = 0, maa4n = 0;
+#pragma unroll
+  for (int c = 1; c < 5; c++) {
+    if (c < last) {
+      if (3 * c + 2 < trlen) {
+        aa4 |= rr[c] << (8 * aa4n);
+        aa4n++;
+      }
+      maa4 |= mm[c] << (8 * maa4n);
+      maa4n++;
+    }
+  }
+  int stop_i = -1;
+  if (stopc < nvalid) {
+    stop_i = 3 * stopc;
+  } else if (nvalid == 5 && 15 + 2 < M && NS) {
+    const int k0 = sfx + (15 - a - x);
+    if (k0 >= 0 && k0 < Lq) {
+      const int st = in.ns_pre != kNsNone ? in.ns_pre : NS[k0];
+      if (st != kNoStop) stop_i = st - sfx + a + x;
+    }
+  }
+  if (stop_i >= 0) {
+    constexpr Txt<22> ps = txt("\tpremature stop at AA");
+    app(L, ps.w, 21);
+    const Num an = fmt8((uint32_t)(1 + (stop_i + rt) / 3));
+    uint32_t g[3] = {an.lo, an.hi, 0u};
+    or_at(g, '\n', an.nd);
+    app(L, g, an.nd + 1);
+  } else if (aa4n > 0 && maa4n > 0) {
+    constexpr Txt<14> fs = txt("\tframe shift ");
+    app(L, fs.w, 13);
+    const uint64_t u = (uint64_t)aa4 | (uint64_t)('+' | ':' << 8) << (8 * aa4n);
+    const uint64_t v = (uint64_t)maa4 | (uint64_t)('+' | '\n' << 8) << (8 * maa4n);
+    const uint32_t gu[2] = {(uint32_t)u, (uint32_t)(u >> 32)}, gv[2] = {(uint32_t)v, (uint32_t)(v >> 32)};
+    app(L, gu, aa4n + 2);
+    app(L, gv, maa4n + 2);
+  } else {
+    const uint32_t e[1] = {(uint32_t)'\t' | (uint32_t)'\n' << 8};
+    app(L, e, 2);
+  }
+  return merr;
+}
+
 // ------------------------------------------------------------------ workspace
 // Device scratch of one pass (pw_report_workspace_bytes):
 //   ctr      u32 [1] long-line count, [2] overflow flags; u64 at byte 16: arena bytes used
@@ -1905,18 +2272,21 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       // r_trloc + deletion, ends by rloc + 25)
       const int rlc = event_rloc(r.L, rev, typ, h.qp, n);
       const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
-      const bool fast = r.acgt && rlc >= 8 && pre.qlo <= rlc - 8 &&
+      // (and numbers below 10^8: emit_fast's decimal conversion)
+      const bool fast = r.acgt && rlc >= 8 && pre.qlo <= rlc - 8 && r.L < 100000000 && h.tloc < 99999999 &&
                         (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L)
                                           : (typ == PW_OP_INS ? (n <= 8 && rt - pre.qlo >= n) : n <= 12));
       int merr;
       if (__ballot(!fast) == 0) {
-        RecFast rf;
-        static_cast<Rec&>(rf) = r;
-        merr = emit_event(k, rf, in, skip, rel);
+        DLine dl;
+        dl.buf = my_line;
+        dl.pos = 0;
+        merr = emit_fast(dl, my_qw, pre.qlo, tp, in, rev, r.L, h.l0, h.l1, r.NS, skip, rel);
+        linelen = dl.pos;
       } else {
         merr = emit_event(k, r, in, skip, rel);
+        linelen = k.pos;
       }
-      linelen = k.pos;
       if (merr >= 0) {  // modseq error: first failing event of the record in output order
         const uint32_t ai = rec_of_slot(A, s);
         const pw_aln_desc d = A.desc[ai];
