@@ -177,7 +177,8 @@ def main():
     n_events = int(res["n_events"].sum())
     errs = int((res["err"] != 0).sum())
     text_bytes = int(res["text_len"].astype(np.int64).sum())
-    assert errs == 0, f"{errs} records reported errors"
+    if not os.environ.get("PW_BENCH_NOCHECK"):  # (set by attribution sweeps of variants that render wrong)
+        assert errs == 0, f"{errs} records reported errors"
     ctr = dev["work"][:16].cpu().numpy().view(np.uint32)
     log(f"[rank {rank}] {n_events} events, {text_bytes} text bytes; long lines {int(ctr[1])}")
 

@@ -69,8 +69,8 @@ constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dw
 constexpr int kLine = 92;       // render_kernel: report lines up to this long are built in LDS (99.94 % at cfg2)
 constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
-constexpr int kLStride = kLine + kLSlack;  // 132 bytes = 33 dwords: per-lane byte stores conflict-free
-constexpr int kMap = kWave * kLine / 16 + 2;  // chunk-map entries
+static_assert(kLine + kLSlack <= 144, "line buffer stride");
+constexpr int kLStride = 144;  // line buffer stride (16-byte aligned for the copy-out reads)
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
 constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, failed records)
@@ -316,9 +316,12 @@ __device__ __forceinline__ uint8_t codon_at(const LDS SmallTables* t, u128 v, in
 }
 // complement of A/C/G/T bytes (A<->T: ^0x15, C<->G: ^0x04; bit 1 tells them apart).  Maps no
 // other byte onto A/C/G/T, so a validity check after it still rejects non-ACGT input.
+__device__ __forceinline__ uint32_t comp_acgt4(uint32_t v) {
+  const uint32_t t = (v >> 1) & 0x01010101u, u = t ^ 0x01010101u;  // (0 / 1 per byte: shifts, no carries)
+  return v ^ (t << 2 | u | u << 2 | u << 4);
+}
 __device__ __forceinline__ uint64_t comp_acgt8(uint64_t v) {
-  const uint64_t t = (v >> 1) & 0x0101010101010101ull;
-  return v ^ (t * 0x04ull | (t ^ 0x0101010101010101ull) * 0x15ull);
+  return (uint64_t)comp_acgt4((uint32_t)v) | (uint64_t)comp_acgt4((uint32_t)(v >> 32)) << 32;
 }
 
 // bytes qw[off, off + 8) of an LDS window (off >= 0)
@@ -717,8 +720,8 @@ __device__ __forceinline__ bool sub_image(const R& r, const Event& e, int p0, u1
   uint32_t alt = pack_even4(l64), sub = pack_even4(l64 >> 8);
   const int n = e.n;
   if (r.rev) {  // evtbases / evtsub reversed and complemented (pafreport.cpp:636-637)
-    alt = (uint32_t)comp_acgt8(__builtin_bswap32(alt) >> (8 * (4 - n)));
-    sub = (uint32_t)comp_acgt8(__builtin_bswap32(sub) >> (8 * (4 - n)));
+    alt = comp_acgt4(__builtin_bswap32(alt) >> (8 * (4 - n)));
+    sub = comp_acgt4(__builtin_bswap32(sub) >> (8 * (4 - n)));
   }
   const uint32_t nm = n == 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
   const u128 place = (u128)nm << (8 * p0);
@@ -1049,7 +1052,7 @@ __device__ __forceinline__ void app(DLine& L, const uint32_t (&f)[D], int n) {
   const uint32_t cur = d[0];  // bytes [a, p) of the line
   // result byte j of dword i = stream byte 4i + j - sh: selector 4 - sh + j over {f[i], f[i - 1]};
   // dword 0 keeps its first sh bytes from cur
-  const uint32_t sel = 0x07060504u - 0x01010101u * sh;
+  const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);  // (byte 0 of sh in every byte)
   const uint32_t m = (uint32_t)((1ull << (8 * sh)) - 1ull);
   const uint32_t sel0 = (sel & ~m) | (0x03020100u & m);
   uint32_t g[D + 1];
@@ -1093,15 +1096,17 @@ struct Num {
   uint32_t lo, hi;
   int nd;
 };
+// (24-bit multiplies: every operand here is below 2^24, and v_mul_u32_u24 is full rate)
+__device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return __umul24(a, b); }
 __device__ __forceinline__ uint32_t dig4(uint32_t x) {  // x < 10^4 -> 4 digit values, first in byte 0
-  const uint32_t q = (x * 5243u) >> 19;
-  const uint32_t p = q | (x - 100u * q) << 16;
-  const uint32_t t = ((p * 103u) >> 10) & 0x000F000Fu;
-  return t | (p - 10u * t) << 8;
+  const uint32_t q = mul24(x, 5243u) >> 19;
+  const uint32_t p = q | (x - mul24(100u, q)) << 16;
+  const uint32_t t = (mul24(p, 103u) >> 10) & 0x000F000Fu;
+  return t | (p - mul24(10u, t)) << 8;
 }
 __device__ __forceinline__ Num fmt8(uint32_t v) {
   const uint32_t h = __umulhi(v, 3518437209u) >> 13;  // v / 10^4 (exact for v < 10^8)
-  const uint64_t raw = (uint64_t)dig4(h) | (uint64_t)dig4(v - 10000u * h) << 32;
+  const uint64_t raw = (uint64_t)dig4(h) | (uint64_t)dig4(v - mul24(10000u, h)) << 32;
   const uint32_t lo = (uint32_t)raw, hi = (uint32_t)(raw >> 32);
   // leading zero digits = trailing zero bytes of raw (at least one digit stays)
   int z = (lo ? __builtin_ctz(lo) : 32 + (hi ? __builtin_ctz(hi) : 32)) >> 3;
@@ -1116,7 +1121,7 @@ __device__ __forceinline__ Num fmt8(uint32_t v) {
 // codon64 index of the three bases in bytes 0-2 of w (A/C/G/T: code (c >> 1) & 3)
 __device__ __forceinline__ uint32_t cidx(uint32_t w) {
   const uint32_t c = (w >> 1) & 0x00030303u;
-  return ((c * 0x00100401u) >> 16) & 63u;
+  return (mul24(c, 0x00100401u) >> 16) & 63u;  // (low 32 bits of the product: bits 16-21 are exact)
 }
 // constant text as dwords
 template <int N>
@@ -1168,8 +1173,8 @@ __device__ __forceinline__ int emit_fast(DLine& L, const LDS uint8_t* qw, int ql
     alt = pack_even4(l64);
     sub = pack_even4(l64 >> 8);
     if (rev) {
-      alt = (uint32_t)comp_acgt8(__builtin_bswap32(alt) >> (8 * (4 - n)));
-      sub = (uint32_t)comp_acgt8(__builtin_bswap32(sub) >> (8 * (4 - n)));
+      alt = comp_acgt4(__builtin_bswap32(alt) >> (8 * (4 - n)));
+      sub = comp_acgt4(__builtin_bswap32(sub) >> (8 * (4 - n)));
     }
     alt = keep32(alt, n);
     sub = keep32(sub, n);
@@ -1405,6 +1410,9 @@ struct Fixup {
   uint64_t dst;  // text offset of the line
 };
 
+// render_kernel: the bytes a page keeps free after its text (a line's last 16-byte store may reach
+// 12 bytes past its end)
+constexpr uint32_t kPageSlack = 16;
 struct Work {
   uint32_t* ctr;
   unsigned long long* arena_used;
@@ -2069,9 +2077,6 @@ __global__ __launch_bounds__(kWave* kWaves) void carry_kernel(pw_report_args A, 
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
-  uint32_t ostart[kWave + 1];       // starts of the page's non-empty lines (+ the page end)
-  uint8_t olane[kWave + 1];         // their lanes
-  uint8_t cmap[kMap];               // 16-byte output block -> line holding its first byte
 };
 
 // the record owning event slot s: the last one whose first slot is <= s (error path only)
@@ -2213,17 +2218,26 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     const uint64_t s = c * kWave + (uint64_t)lane;
     const bool act = h.fn != kNoEv;
     render_pre_ready(pre);
+#pragma unroll
+    for (int q = 0; q < kQWin / 16; q++) {
+      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
+      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};
+    }
+    const v4u t0 = pre.t0, t1 = pre.t1;
+    const int ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
+    const int qlo = pre.qlo, n_cur = pre.n;
+    const Hot& hc = h;
     int linelen = 0;
     if (act) {
-      const uint32_t typ = h.fn >> 30;
-      const bool rev = (h.fn >> 29) & 1u;
-      const int n = pre.n;
-      const bool use_tx = !((h.fn >> 28) & 1u);
+      const uint32_t typ = hc.fn >> 30;
+      const bool rev = (hc.fn >> 29) & 1u;
+      const int n = n_cur;
+      const bool use_tx = !((hc.fn >> 28) & 1u);
       Rec r;
       r.lits = A.lits;
-      r.R = A.qseq + ((uint64_t)h.qb << 4);
-      r.L = h.L;
-      r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;
+      r.R = A.qseq + ((uint64_t)hc.qb << 4);
+      r.L = hc.L;
+      r.NS = A.next_stop ? A.next_stop + ((uint64_t)hc.qb << 4) : nullptr;
       r.tab = tp;
       r.opw = nullptr;
       r.op_lo = 0;
@@ -2231,36 +2245,30 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       r.lw = nullptr;
       r.l_lo = 0;
       r.l_n = 0;
-      r.lit0 = h.l0;
-      r.lit1 = h.l1;
-      r.ls0 = h.ls;
+      r.lit0 = hc.l0;
+      r.lit1 = hc.l1;
+      r.ls0 = hc.ls;
       r.ln = 8;
       r.rev = rev;
-      r.acgt = (h.fn & kFnAcgt) != 0;
+      r.acgt = (hc.fn & kFnAcgt) != 0;
       r.offset = 0;
       r.T = 0;
       r.ops = nullptr;
       r.n_ops = 0;
-#pragma unroll
-      for (int q = 0; q < kQWin / 16; q++) {
-        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
-        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};
-      }
       r.qw = my_qw;
-      r.qlo = pre.qlo;
+      r.qlo = qlo;
       r.qn = kQWin;
       EvIn in;
       in.typ = typ;
       in.n = n;
-      in.qp = h.qp;
-      in.tloc = h.tloc;
-      in.ls = h.ls;
+      in.qp = hc.qp;
+      in.tloc = hc.tloc;
+      in.ls = hc.ls;
       in.tmode = use_tx ? 1 : 0;
-      in.ll = (int)((h.fn >> 23) & 7u);
-      in.rl = (int)((h.fn >> 20) & 7u);
-      in.tx[0] = pre.t0.x, in.tx[1] = pre.t0.y, in.tx[2] = pre.t0.z, in.tx[3] = pre.t0.w, in.tx[4] = pre.t1.x,
-      in.tx[5] = pre.t1.y;
-      in.ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
+      in.ll = (int)((hc.fn >> 23) & 7u);
+      in.rl = (int)((hc.fn >> 20) & 7u);
+      in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
+      in.ns_pre = ns_pre;
       LineSink k;
       k.line = my_line;
       k.pos = 0;
@@ -2270,18 +2278,18 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       // covers [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8 bases whose modseq tail
       // image starts inside the window, deletions of <= 12 (the largest read, the tail image at
       // r_trloc + deletion, ends by rloc + 25)
-      const int rlc = event_rloc(r.L, rev, typ, h.qp, n);
+      const int rlc = event_rloc(r.L, rev, typ, hc.qp, n);
       const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
       // (and numbers below 10^8: emit_fast's decimal conversion)
-      const bool fast = r.acgt && rlc >= 8 && pre.qlo <= rlc - 8 && r.L < 100000000 && h.tloc < 99999999 &&
+      const bool fast = r.acgt && rlc >= 8 && qlo <= rlc - 8 && r.L < 100000000 && hc.tloc < 99999999 &&
                         (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L)
-                                          : (typ == PW_OP_INS ? (n <= 8 && rt - pre.qlo >= n) : n <= 12));
+                                          : (typ == PW_OP_INS ? (n <= 8 && rt - qlo >= n) : n <= 12));
       int merr;
       if (__ballot(!fast) == 0) {
         DLine dl;
         dl.buf = my_line;
         dl.pos = 0;
-        merr = emit_fast(dl, my_qw, pre.qlo, tp, in, rev, r.L, h.l0, h.l1, r.NS, skip, rel);
+        merr = emit_fast(dl, my_qw, qlo, tp, in, rev, r.L, hc.l0, hc.l1, r.NS, skip, rel);
         linelen = dl.pos;
       } else {
         merr = emit_event(k, r, in, skip, rel);
@@ -2308,15 +2316,16 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
     const uint32_t B = wave_last(incl);
     const uint32_t my_off = incl - (uint32_t)linelen;
-    // the page: in place, or an arena allocation when the lines do not fit
+    // the page: in place, or an arena allocation when the lines (+ kPageSlack) do not fit
     uint64_t P = c * (uint64_t)PW_PAGE_BYTES;
     bool ok = true;
-    if (B > (uint32_t)PW_PAGE_BYTES) {
+    if (B > (uint32_t)PW_PAGE_BYTES - kPageSlack) {
+      const uint32_t need = ((B + 15u) & ~15u) + kPageSlack;
       unsigned long long a = 0;
-      if (lane == 0) a = atomicAdd(W.arena_used, (unsigned long long)((B + 15u) & ~15u));
+      if (lane == 0) a = atomicAdd(W.arena_used, (unsigned long long)need);
       a = __shfl(a, 0, kWave);
       P = W.arena0 + a;
-      if (P + B > A.text_total) {  // capacity violated: report, never write outside
+      if (P + need > A.text_total) {  // capacity violated: report, never write outside
         ok = false;
         if (lane == 0) atomicOr(&W.ctr[2], 1u);
       }
@@ -2354,69 +2363,54 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         f.dst = g0;
         W.fix[s] = f;
       }
-      // the page's non-empty lines in order (k -> start, lane) and the chunk map: 16-byte block ci
-      // of the page -> k of the line holding its first byte (P is 16-byte aligned: pages are
-      // PW_PAGE_BYTES apart, arena allocations 16-byte multiples)
+      // copy-out: every lane stores its own line at page offset my_off (a long line: its first
+      // kLine bytes, fixup_kernel rewrites it) as dwords realigned to the page, 16 bytes per store,
+      // its last group first.  A store's dwords past the line's end are overwritten later by the
+      // next line's first group (written in the last round), and that group's first dword is the
+      // shared one: the next line ORs this line's tail bytes into it (shuffled from the previous
+      // non-empty lane).  The page's last line may store up to 12 bytes past B: the page keeps
+      // kPageSlack bytes free.
       uint8_t* const gb = A.text + P;
       const uint64_t ne = __ballot(linelen > 0);
-      const int nl = __popcll(ne);
-      const int kme = __popcll(ne & ((1ull << lane) - 1ull));
-      if (linelen > 0) {
-        w->ostart[kme] = my_off;
-        st8(&w->olane[kme], (uint8_t)lane);
-        const uint32_t c1 = (my_off + (uint32_t)linelen + 15) >> 4;
-        // (byte stores: a vectorised fill would be unaligned ds_write_b128)
-        for (uint32_t ci = (my_off + 15) >> 4; ci < c1 && ci < (uint32_t)kMap; ci++) st8(&w->cmap[ci], (uint8_t)kme);
-        if (my_off == 0) st8(&w->cmap[0], (uint8_t)kme);
+      const int ln = linelen > kLine ? kLine : linelen;
+      const uint32_t sh = my_off & 3u, a0 = my_off & ~3u;
+      // this line's bytes in the dword at floor4(my_off + linelen): [linelen - t, linelen), t of them
+      const uint32_t t = (my_off + (uint32_t)linelen) & 3u;
+      uint32_t tail;
+      {
+        const int tb = min(linelen - (int)t, kLine);
+        const LDS uint32_t* tp4 = reinterpret_cast<const LDS uint32_t*>(my_line + (tb & ~3));
+        tail = __builtin_amdgcn_alignbyte(tp4[1], tp4[0], (uint32_t)tb & 3u) & (uint32_t)((1ull << (8 * t)) - 1ull);
       }
-      if (lane == 0) w->ostart[nl] = B;
-      wave_sync();
-      // gather: a 16-byte output block holds the tail of one line (A) and at most the head of the
-      // next (B): lines are >= 40 bytes.  Both are read as 16-byte images (aligned dword reads +
-      // byte-align shifts; B's image starts before its line — those bytes are masked off), merged
-      // by a byte mask, then one 16-byte store.
-      for (uint32_t cc = (uint32_t)lane * 16; cc < B; cc += kWave * 16) {
-        int k;
-        if ((cc >> 4) < (uint32_t)kMap) {
-          k = w->cmap[cc >> 4];
-        } else {  // past the map (pages with long lines): last line starting at or before cc
-          k = 0;
+      const uint64_t below = ne & ((1ull << lane) - 1ull);
+      const int prev = below ? 63 - __builtin_clzll(below) : lane;
+      const uint32_t ptail = (uint32_t)__shfl((int)tail, prev, kWave) & (uint32_t)((1ull << (8 * sh)) - 1ull);
+      uint32_t Lw[24];
+      {
+        const LDS v4u* lp4 = reinterpret_cast<const LDS v4u*>(my_line);
 #pragma unroll
-          for (int step = 32; step >= 1; step >>= 1)
-            if (k + step < nl && w->ostart[k + step] <= cc) k += step;
+        for (int q = 0; q < 6; q++) {
+          const v4u v = lp4[q];
+          Lw[4 * q] = v.x, Lw[4 * q + 1] = v.y, Lw[4 * q + 2] = v.z, Lw[4 * q + 3] = v.w;
         }
-        const uint32_t s0 = w->ostart[k], s1 = w->ostart[k + 1];
-        const int la = w->olane[k], lb = w->olane[k + 1 < nl ? k + 1 : k];
-        int xa = (int)cc - (int)s0;  // >= 0
-        if (xa > kLine) xa = kLine;  // long line: garbage here, fixup_kernel rewrites it
-        int xb = (int)cc - (int)s1;  // < 0 while the block starts in line A
-        if (xb < -16) xb = -16;
-        const int aa = la * kLStride + xa, ab = lb * kLStride + xb;  // (ab >= 0: lb >= 1 when it is used)
-        const LDS uint32_t* pa = reinterpret_cast<const LDS uint32_t*>(w->line + (aa & ~3));
-        const LDS uint32_t* pb = reinterpret_cast<const LDS uint32_t*>(w->line + (ab > 0 ? (ab & ~3) : 0));
-        uint32_t da[5], db[5];
+      }
+      const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);
+      const int kmax = linelen > 0 ? ((int)sh + ln - 1) >> 2 : -1;  // last dword (from a0) holding a line byte
+      const int jmax = kmax >> 2;
+      PW_GLOBAL uint32_t* gd = (PW_GLOBAL uint32_t*)(gb + a0);
 #pragma unroll
-        for (int i = 0; i < 5; i++) {
-          da[i] = pa[i];
-          db[i] = pb[i];
-        }
-        const uint32_t sa = (uint32_t)aa & 3u, sb = (uint32_t)ab & 3u;
-        const int nka = (int)(s1 - cc);  // bytes of the block from line A (>= 16: all)
-        uint32_t v[4];
+      for (int j = 5; j >= 0; j--) {
+        if (j <= jmax) {
+          uint32_t v[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          int n = nka - 4 * i;
-          n = n < 0 ? 0 : (n > 4 ? 4 : n);
-          const uint32_t m = (uint32_t)((1ull << (8 * n)) - 1ull);
-          v[i] = (__builtin_amdgcn_alignbyte(da[i + 1], da[i], sa) & m) |
-                 (__builtin_amdgcn_alignbyte(db[i + 1], db[i], sb) & ~m);
+          for (int i = 0; i < 4; i++) {
+            const int k = 4 * j + i;
+            const uint32_t cur = k < 24 ? Lw[k] : 0u, prv = k == 0 ? 0u : Lw[k - 1];
+            v[i] = __builtin_amdgcn_perm(cur, prv, sel);
+          }
+          if (j == 0) v[0] |= ptail;
+          *reinterpret_cast<PW_GLOBAL v4u*>(gd + 4 * j) = (v4u){v[0], v[1], v[2], v[3]};
         }
-        v4u vv;
-        vv.x = v[0];
-        vv.y = v[1];
-        vv.z = v[2];
-        vv.w = v[3];
-        *reinterpret_cast<v4u*>(gb + cc) = vv;  // (bytes past B are page slack)
       }
     }
     wave_sync();
@@ -2855,7 +2849,8 @@ extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_
 }
 extern "C" uint64_t pw_report_page_count(uint64_t n_ev_slots) { return (n_ev_slots + PW_PAGE_EVENTS - 1) / PW_PAGE_EVENTS; }
 extern "C" uint64_t pw_report_text_bytes(uint64_t n_ev_slots, uint64_t text_bound) {
-  return pw_report_page_count(n_ev_slots) * PW_PAGE_BYTES + pw::align_up(text_bound, 16) + 16;
+  // (an arena allocation is its text rounded to 16 bytes + kPageSlack: at most one per page)
+  return pw_report_page_count(n_ev_slots) * (PW_PAGE_BYTES + pw::kPageSlack) + pw::align_up(text_bound, 16) + 16;
 }
 
 extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, void* next_stop_ready);

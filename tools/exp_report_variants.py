@@ -1,0 +1,58 @@
+"""Experiment variants of pw_report.hip (never shipped; timing only unless noted) linked into
+tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
+  cur      the working copy
+  allgen   every render wave takes the general emit_event path (same bytes)
+  allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
+  noline   no line is built (every line 78 bytes of whatever the buffer holds: timing only)
+  nowin    the per-lane query window is not loaded (constant bytes: timing only)
+  nohot    the Hot records are replaced by synthetic insertions after the load (timing only)
+  nocopy   render's copy-out stores skipped (timing only)
+Usage: python tools/exp_report_variants.py [names...]"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "pwasm_amd/csrc/pw_report.hip")
+OUT = os.path.join(REPO, "tools/abl_build")
+TMP = os.path.join(REPO, "build_exp")
+
+PATCHES = {
+    "cur": [],
+    "allgen": [("      if (__ballot(!fast) == 0) {\n        DLine dl;", "      if (false) {\n        DLine dl;")],
+    "allfast": [("      if (__ballot(!fast) == 0) {\n        DLine dl;", "      if (true) {\n        DLine dl;")],
+    "noline": [("      if (__ballot(!fast) == 0) {\n        DLine dl;",
+                "      if (A.n_alns != 0) {\n        merr = -1;\n        linelen = 78;\n      } else if (__ballot(!fast) == 0) {\n        DLine dl;")],
+    "nowin": [("  for (int q = 0; q < kQWin / 16; q++) p.q[q] = a0[q];\n  p.qlo = x0a;",
+               "  for (int q = 0; q < kQWin / 16; q++) p.q[q] = (v4u){0x41434741u, 0x54414341u, 0x47544341u, 0x41434741u};\n  p.qlo = x0a;")],
+    "nohot": [("  r.a = p[0];\n  r.b = p[1];\n  return r;", "  r.a = p[0];\n  r.b = p[1];\n  if (cc > 60000000) return r;\n  r.a = (v4u){0u, 2000u, 100u + 64u * (uint32_t)(cc & 15u) + lane, 50u};\n  r.b = (v4u){0u, (uint32_t)(PW_OP_INS << 30) | (1u << 28) | kFnAcgt | 2u, 0x41414141u, 0x41414141u};\n  return r;")],
+    "nocopy": [("      for (int j = 5; j >= 0; j--) {\n        if (j <= jmax) {",
+                "      for (int j = 5; j >= 0; j--) {\n        if (j <= jmax && A.n_alns == 0) {")],
+}
+
+
+def build(name):
+    s = open(SRC).read()
+    for a, b in PATCHES[name]:
+        assert a in s, (name, a)
+        s = s.replace(a, b)
+    os.makedirs(TMP, exist_ok=True)
+    src = os.path.join(TMP, f"report_{name}.hip")
+    open(src, "w").write(s)
+    d = os.path.join(OUT, name)
+    os.makedirs(os.path.join(d, "lib"), exist_ok=True)
+    o = os.path.join(d, "pw_report.o")
+    inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
+                    "-Wno-unused-function", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause", *inc, "-c", src,
+                    "-o", o], check=True)
+    bdir = os.path.join(REPO, "pwasm_amd/build")
+    objs = [os.path.join(bdir, f) for f in sorted(os.listdir(bdir)) if f.endswith(".o") and f != "pw_report.o"]
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
+                    os.path.join(d, "lib", "libpwasm_amd.so"), o, *objs, "-ldl"], check=True)
+    print("built", name, flush=True)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(PATCHES):
+        build(n)

@@ -4,7 +4,7 @@
 set -uo pipefail
 TAG=${1:-x}; shift
 mkdir -p gpurun_out
-export TMPDIR=/tmp
+export TMPDIR=/tmp PW_BENCH_NOCHECK=1
 VS="$*"
 [ -z "$VS" ] && VS=$(ls tools/abl_build)
 for v in $VS; do
@@ -13,5 +13,5 @@ for v in $VS; do
   f=$(find gpurun_out/sw_$TAG/$v -name "*kernel_stats.csv" | head -1)
   par=$(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d.get('parity'), round(d['roofline']['kernel_ms'],4))" gpurun_out/sw_${TAG}_$v.json)
   echo "== $v parity/kernel_ms: $par"
-  grep "pw::" "$f" | awk -F, '{printf "   %-24s %8.1f us\n", substr($1,2,24), $4/1000}'
+  python3 tools/kstat.py "$f"
 done
