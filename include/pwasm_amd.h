@@ -121,7 +121,8 @@ typedef struct pw_report_args {
                                than PW_BLOCK_OPS ops are decoded as blocks of PW_BLOCK_OPS ops by
                                several wavefronts (block carries from a pre-pass); a value
                                <= PW_BLOCK_OPS lets the pass skip that pre-pass. */
-  uint32_t reserved;        /* 0 */
+  uint32_t n_short;         /* records of at most 64 ops, or 0 = unknown: when they are most of the
+                               batch, index decoding takes two records per wavefront */
 } pw_report_args;
 #define PW_BLOCK_OPS 2048
 

@@ -69,7 +69,7 @@ class ReportArgs(ctypes.Structure):
                 ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
                 ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p), ("max_rec_ops", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("n_short", ctypes.c_uint32)]
 
 
 class CsTotals(ctypes.Structure):
@@ -371,7 +371,13 @@ class HostBatch:
         if getattr(self, "_max_ops", None) is None:
             d = self.array("desc").view(np.uint32).reshape(-1, 8)
             self._max_ops = int(d[:, 1].max()) if d.size else 0
+            self._n_short = int((d[:, 1] <= 64).sum()) if d.size else 0
         return self._max_ops
+
+    def n_short(self) -> int:
+        """Records of at most 64 ops (pw_report_args.n_short)."""
+        self.max_rec_ops()
+        return self._n_short
 
     def write_report(self, text_host, results_host, pages_host, path: str) -> int:
         """Headers + event text for a finished batch (numpy arrays on the host)."""
@@ -445,6 +451,7 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     a.n_ev_slots = int(v.n_events_max)
     a.pages = dev["pages"].data_ptr()
     a.max_rec_ops = batch.max_rec_ops()
+    a.n_short = 0 if os.environ.get("PW_NO_PAIRS") else batch.n_short()
     return a
 
 

@@ -1390,8 +1390,12 @@ struct Device {
     a.n_ev_slots = b.n_events_max;
     a.pages = pages.p;
     a.max_rec_ops = 0;
-    for (const pw_aln_desc& d : b.desc) a.max_rec_ops = d.n_ops > a.max_rec_ops ? d.n_ops : a.max_rec_ops;
-    a.reserved = 0;
+    a.n_short = 0;
+    for (const pw_aln_desc& d : b.desc) {
+      a.max_rec_ops = d.n_ops > a.max_rec_ops ? d.n_ops : a.max_rec_ops;
+      a.n_short += d.n_ops <= 64 ? 1u : 0u;
+    }
+    if (getenv("PW_NO_PAIRS") && atoi(getenv("PW_NO_PAIRS")) != 0) a.n_short = 0;  // (tests: one record per wave)
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
       return false;

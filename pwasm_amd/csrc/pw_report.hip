@@ -43,6 +43,7 @@
 // The text is one contiguous stream of event lines in record order; record headers are
 // formatted by the host (the only floating-point value, coverage:%.2f).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <limits.h>
 #include <stdint.h>
 
@@ -1515,7 +1516,7 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
 // ------------------------------------------------------------------ index_kernel
 constexpr int kOpWin = kSegOps + 2 * kOpHalo;
 struct IndexWave {
-  uint32_t opw[kOpWin];            // op words of the segment + halo
+  uint32_t opw[kOpWin + 8];        // op words of the segment + halo (index_pair_kernel: two records' ops)
 };
 
 __device__ __forceinline__ int ndigits(uint32_t v) {
@@ -1939,6 +1940,33 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   }
 }
 
+// index_kernel's (and index_pair_kernel's) end: blocks 1.. of the long records, spread over all
+// wavefronts (a record of 1-5 Mb walked by one wave would be the whole kernel's critical path), and
+// the padding slots of the last chunk (empty)
+__device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
+                                                  LDS IndexWave* w, int lane, int wv, uint32_t stride, bool planned) {
+  if (planned) {
+    const uint32_t nbl = W.ctr[3] < W.blk_cap ? W.ctr[3] : W.blk_cap;
+    for (uint32_t i = blockIdx.x * kWaves + wv; i < nbl; i += stride) {
+      const uint64_t e = W.blist[i];
+      const uint32_t bai = (uint32_t)(e >> 32), k = (uint32_t)e;
+      if (k == 0) continue;
+      RecPre p;
+      rec_pre(A, bai, A.desc[bai], lane, p);
+      rec_pre_ready(A, p, lane);
+      IdxBlk B = block_of(W, p.d, i - k, (p.d.n_ops + kBlkOps - 1) / kBlkOps, k, lane);
+      B.prev_sub = (A.ops[p.d.op_begin + B.sb0 - 1] >> 30) == PW_OP_SUB;
+      index_record(A, W, tp, w, bai, lane, p, B);
+    }
+  }
+  const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
+  if (blockIdx.x == 0)
+    for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) {
+      W.hot[s].fn = kNoEv;
+      W.sflag[s] = 0;
+    }
+}
+
 __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
@@ -1982,29 +2010,289 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
       dn = dnn;
     }
   }
-  // blocks 1.. of the long records, spread over all wavefronts (a record of 1-5 Mb walked by one
-  // wave would be the whole kernel's critical path)
-  if (planned) {
-    const uint32_t nbl = W.ctr[3] < W.blk_cap ? W.ctr[3] : W.blk_cap;
-    for (uint32_t i = blockIdx.x * kWaves + wv; i < nbl; i += stride) {
-      const uint64_t e = W.blist[i];
-      const uint32_t bai = (uint32_t)(e >> 32), k = (uint32_t)e;
-      if (k == 0) continue;
-      RecPre p;
-      rec_pre(A, bai, A.desc[bai], lane, p);
-      rec_pre_ready(A, p, lane);
-      IdxBlk B = block_of(W, p.d, i - k, (p.d.n_ops + kBlkOps - 1) / kBlkOps, k, lane);
-      B.prev_sub = (A.ops[p.d.op_begin + B.sb0 - 1] >> 30) == PW_OP_SUB;
-      index_record(A, W, tp, w, bai, lane, p, B);
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned);
+}
+
+// ------------------------------------------------------------------ index_kernel, two short records per wave
+// Records of at most kPairOps ops (most of a gene panel's — cfg3 averages ~40 — where one record
+// per wavefront left the wave's fixed per-record work, not the ops, as index_kernel's cost) go two
+// to a wavefront, one per 32-lane half, every op at once (2 per lane).  The per-op work is
+// index_record's for a record that fits one segment; the scans stop at the half (no row_bcast:31
+// step), the ballots are read per half and the record fields are per lane.
+constexpr uint32_t kPairOps = 64;
+__device__ __forceinline__ uint32_t half_scan_incl(uint32_t v) {
+  v += dpp_or_zero<0x111>(v);       // row_shr:1
+  v += dpp_or_zero<0x112>(v);       // row_shr:2
+  v += dpp_or_zero<0x114>(v);       // row_shr:4
+  v += dpp_or_zero<0x118>(v);       // row_shr:8
+  v += dpp_or_zero<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3: each half's second row
+  return v;
+}
+__device__ __forceinline__ uint32_t half_last(uint32_t v, int lane) {  // lane 31's / lane 63's value
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 31), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  return lane < 32 ? a : b;
+}
+__device__ __forceinline__ uint32_t half_bits(uint64_t m, int lane) { return (uint32_t)(m >> (lane & 32)); }
+
+// the head of a pair unit's record ri (valid: ri < n_alns), every value per lane
+struct PairHead {
+  pw_aln_desc d;
+  uint64_t qb, ev_next;
+  int L;
+  uint32_t w0, w1;
+};
+__device__ __forceinline__ void pair_head(const pw_report_args& A, uint32_t ri, int hl, PairHead& p) {
+  const uint32_t r = ri < A.n_alns ? ri : A.n_alns - 1;
+  p.d = A.desc[r];
+  const uint32_t qi = p.d.ref & PW_REF_QMASK;
+  p.qb = A.qoff[qi];
+  p.L = A.qlen[qi];
+  p.ev_next = r + 1 < A.n_alns ? A.desc[r + 1].ev_begin : A.n_ev_slots;
+  const uint32_t* ops = A.ops + p.d.op_begin;
+  const uint32_t n = p.d.n_ops;
+  const uint32_t* dummy = reinterpret_cast<const uint32_t*>(A.desc);  // (a readable word for lanes past the ops)
+  p.w0 = *((uint32_t)hl < n ? ops + hl : dummy);
+  p.w1 = *((uint32_t)(hl + 32) < n ? ops + hl + 32 : dummy);
+  if ((uint32_t)hl >= n) p.w0 = 0u;
+  if ((uint32_t)(hl + 32) >= n) p.w1 = 0u;
+}
+
+// the two records of a pair unit (record ri of this lane's half; valid = it exists)
+__device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
+                                           LDS IndexWave* w, uint32_t ai, bool valid, int lane, const PairHead& P) {
+  const int hl = lane & 31, half = lane >> 5;
+  const pw_aln_desc& d = P.d;
+  const uint64_t qb = P.qb;
+  const uint8_t* R = A.qseq + qb;
+  const bool layout_ok = (qb & 15u) == 0 && (qb >> 36) == 0 && P.ev_next >= d.ev_begin && P.ev_next <= A.n_ev_slots;
+  const int L = P.L;
+  const bool rev = (d.ref & PW_REF_REVERSE) != 0;
+  const int T = d.t_len;
+  const uint32_t n_ops = valid && layout_ok ? d.n_ops : 0u;
+  const uint64_t evb = d.ev_begin;
+  const uint32_t nmax = layout_ok ? (uint32_t)(P.ev_next - evb) : 0u;
+  const uint32_t* lits32 = reinterpret_cast<const uint32_t*>(A.lits);
+  LDS uint32_t* opw = w->opw + kOpHalo + 80 * half;  // this half's op words (opw[-1] and opw[64]: 0)
+  // ---- op words + half scans of the query / target / literal advances
+  uint32_t wd[2];
+  int qs[2], ts[2];
+  uint32_t ls[2];
+  uint32_t qtot = 0, ttot = 0, ltot = 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const uint32_t idx = 32 * k + hl;
+    wd[k] = idx < n_ops ? (k == 0 ? P.w0 : P.w1) : 0u;
+    const uint32_t qa = op_qadv(wd[k]), ta = op_tadv(wd[k]), la = op_ladv(wd[k]);  // (0 for a 0 word... see below)
+    const uint32_t qa_ = idx < n_ops ? qa : 0u, ta_ = idx < n_ops ? ta : 0u, la_ = idx < n_ops ? la : 0u;
+    const uint32_t qi_ = half_scan_incl(qa_), ti_ = half_scan_incl(ta_), li_ = half_scan_incl(la_);
+    qs[k] = (int)(qtot + qi_ - qa_);
+    ts[k] = (int)(ttot + ti_ - ta_);
+    ls[k] = d.lit_begin + ltot + li_ - la_;
+    qtot += half_last(qi_, lane);
+    ttot += half_last(ti_, lane);
+    ltot += half_last(li_, lane);
+    opw[idx] = wd[k];
+  }
+  if (hl == 0) {
+    opw[-1] = 0u;
+    opw[64] = 0u;
+  }
+  // ---- per op: query base, cs query base of a '*' op, the first 8 literal bytes of an event head
+  uint8_t qlit[2], qref[2];
+  uint32_t lw[2][3];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int qp = d.offset + qs[k];
+    const int qc = qp < 0 ? 0 : (qp >= L ? (L > 0 ? L - 1 : 0) : qp);
+    qref[k] = R[rev ? (L > 0 ? L - 1 - qc : 0) : qc];
+    qlit[k] = A.lits[ls[k] + 1];
+    const uint32_t la = ls[k] >> 2;
+#pragma unroll
+    for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
+  }
+  // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads, per half
+  uint32_t subm[2], hm[2];
+  int bad_idx = INT_MAX;
+  int err_a = 0, err_b = 0, err_c = 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const uint32_t idx = 32 * k + hl;
+    const bool in = idx < n_ops;
+    const uint32_t typ = wd[k] >> 30;
+    const bool is_sub = in && typ == PW_OP_SUB;
+    subm[k] = half_bits(__ballot(is_sub), lane);
+    const bool prevsub = hl == 0 ? (k == 1 && ((subm[0] >> 31) & 1u) != 0) : ((subm[k] >> (hl - 1)) & 1u) != 0;
+    hm[k] = half_bits(__ballot(in && (typ == PW_OP_INS || typ == PW_OP_DEL || (is_sub && !prevsub))), lane);
+    const int qp = d.offset + qs[k];
+    const uint8_t rch = (unsigned)qp >= (unsigned)L ? (uint8_t)0 : (rev ? tab->comp[qref[k]] : qref[k]);
+    const uint8_t qch = qlit[k];
+    const bool bad = is_sub && qch != rch;
+    const uint32_t bm = half_bits(__ballot(bad), lane);
+    const int fl = __builtin_ctz(bm | 0x80000000u);  // (31 when none: a lane in range)
+    const int src = (lane & 32) + fl;
+    const int ea = __shfl(qp, src, kWave), eb = __shfl((int)qch, src, kWave), ec = __shfl((int)rch, src, kWave);
+    if (bm && bad_idx == INT_MAX) {
+      bad_idx = 32 * k + fl;
+      err_a = ea;
+      err_b = eb;
+      err_c = ec;
     }
   }
-  // the padding slots of the last chunk are empty
-  const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
-  if (blockIdx.x == 0)
-    for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) {
-      W.hot[s].fn = kNoEv;
-      W.sflag[s] = 0;
+  wave_sync();
+  uint32_t hl0[2], hl1[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const uint32_t sh = ls[k] & 3u;
+    hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
+    hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
+  }
+  // ---- events (none after a mismatch: the record ends at its first one)
+  const bool ok = bad_idx == INT_MAX;
+  const uint32_t n0 = (uint32_t)__popc(hm[0]);
+  const uint32_t nev = ok ? n0 + (uint32_t)__popc(hm[1]) : 0u;
+  const uint32_t lt = (1u << hl) - 1u;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const uint32_t idx = 32 * k + hl;
+    const uint32_t typ = wd[k] >> 30;
+    if (ok && ((hm[k] >> hl) & 1u)) {
+      uint32_t n;
+      if (typ != PW_OP_SUB) {
+        n = wd[k] & 0x3FFFFFFFu;
+      } else {  // run of '*' ops from idx: first non-'*' op at or after it (ops past the record are not '*')
+        const uint32_t ns0 = ~subm[0], ns1 = ~subm[1];
+        uint32_t end;
+        const uint32_t r0 = k == 0 ? (ns0 >> hl) : 0u;
+        if (k == 0 && r0) end = (uint32_t)hl + (uint32_t)__builtin_ctz(r0);
+        else {
+          const uint32_t r1 = k == 0 ? ns1 : (ns1 >> hl);
+          end = r1 ? (k == 0 ? 32u + (uint32_t)__builtin_ctz(r1) : 32u + (uint32_t)hl + (uint32_t)__builtin_ctz(r1)) : 64u;
+        }
+        n = end - idx;
+      }
+      const TGeom g = tgeom(T, typ, (int)n, ts[k]);
+      const uint32_t pw = opw[(int)idx - 1], aw = opw[idx + 1];
+      const bool fast = tctx_fast(g, typ, (int)n, pw, idx > 0, aw, idx + 1 < n_ops);
+      const uint32_t kidx = k == 0 ? (uint32_t)__popc(hm[0] & lt) : n0 + (uint32_t)__popc(hm[1] & lt);
+      if (kidx < nmax) {
+        const uint64_t s = rev ? evb + nmax - 1 - kidx : evb + kidx;
+        const bool lastc = kidx + 1 == nev;
+        const bool first = rev ? lastc : kidx == 0, last = rev ? kidx == 0 : lastc;
+        Hot hh;
+        hh.qb = (uint32_t)(qb >> 4);
+        hh.L = L;
+        hh.qp = d.offset + qs[k];
+        hh.tloc = rev ? T - ts[k] : ts[k];
+        hh.ls = ls[k];
+        hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, (d.ref & PW_REF_ACGT) != 0, n);
+        hh.l0 = hl0[k];
+        hh.l1 = hl1[k];
+        W.hot[s] = hh;
+        W.sflag[s] = fast ? (uint8_t)0 : (uint8_t)1;
+        if (kidx == 0 || lastc || n >= kNBig) {
+          Cold cd;
+          cd.ai = ai;
+          cd.j = idx;
+          cd.qs = qs[k];
+          cd.ts = ts[k];
+          W.cold[s] = cd;
+        }
+        if (!fast) {  // tctx_kernel's walk start
+          v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
+          dtx[0] = (v4u){d.op_begin, idx, n_ops, (uint32_t)qs[k]};
+          dtx[1] = (v4u){(uint32_t)ts[k], (uint32_t)T, (uint32_t)d.offset, 0u};
+        }
+      }
     }
+  }
+  // ---- empty slots, results
+  int err = !layout_ok ? PW_REC_LAYOUT : (ok ? PW_REC_OK : PW_REC_MISMATCH);
+  uint32_t ev = nev;
+  if (ev > nmax) {  // host event bound violated (cannot happen: every head is a counted op)
+    err = PW_REC_OVERFLOW;
+    ev = nmax;
+  }
+  if (valid) {
+    if (!layout_ok) {
+      if (P.ev_next >= evb && P.ev_next <= A.n_ev_slots)
+        for (uint64_t s = evb + (uint64_t)hl; s < P.ev_next; s += 32) {
+          W.hot[s].fn = kNoEv;
+          W.sflag[s] = 0;
+        }
+    } else {
+      const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;
+      for (uint64_t s = h0 + (uint64_t)hl; s < h1; s += 32) {
+        W.hot[s].fn = kNoEv;
+        W.sflag[s] = 0;
+      }
+    }
+    if (hl == 0) {
+      pw_aln_result res;
+      res.text_off = res.text_end = 0;
+      res.page_first = res.page_last = 0;
+      res.text_len = 0;
+      res.n_events = ev;
+      res.err = err;
+      res.err_a = err_a;
+      res.err_b = err_b;
+      res.err_c = err_c;
+      A.results[ai] = res;
+      W.rec_mod[ai] = ~0ull;
+    }
+  }
+  wave_sync();
+}
+
+// one record of a unit that is not a pair (index_kernel's per-record step, without its prefetch)
+__device__ __forceinline__ void index_one(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
+                                          LDS IndexWave* w, uint32_t ai, int lane, bool planned) {
+  RecPre p;
+  rec_pre(A, ai, A.desc[ai], lane, p);
+  rec_pre_ready(A, p, lane);
+  IdxBlk B = whole_record(p.d);
+  if (planned && p.d.n_ops > (uint32_t)kBlkOps) {
+    const uint32_t base = W.rec_blk[ai];
+    if (base != kNoBlk) B = block_of(W, p.d, base, (p.d.n_ops + kBlkOps - 1) / kBlkOps, 0u, lane);
+  }
+  index_record(A, W, tab, w, ai, lane, p, B);
+}
+
+__global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_pair_kernel(pw_report_args A, Work W) {
+  __shared__ SmallTables tab;
+  __shared__ IndexWave iw[kWaves];
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, kWave * kWaves);
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int hl = lane & 31;
+  LDS IndexWave* w = (LDS IndexWave*)&iw[wv];
+  const uint32_t stride = gridDim.x * kWaves;
+  const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;
+  const uint32_t nu = (A.n_alns + 1) / 2;  // units of two records
+  uint32_t u = blockIdx.x * kWaves + wv;
+  if (u < nu) {
+    // the next unit's heads are loaded while this one is processed
+    PairHead cur;
+    pair_head(A, 2 * u + (uint32_t)(lane >> 5), hl, cur);
+    for (; u < nu; u += stride) {
+      const uint32_t un = u + stride;
+      PairHead nxt;
+      pair_head(A, 2 * (un < nu ? un : u) + (uint32_t)(lane >> 5), hl, nxt);
+      const uint32_t ai = 2 * u + (uint32_t)(lane >> 5);
+      const bool valid = ai < A.n_alns;
+      const uint32_t n_a = (uint32_t)__builtin_amdgcn_readlane((int)cur.d.n_ops, 0);
+      const uint32_t n_b = (uint32_t)__builtin_amdgcn_readlane((int)cur.d.n_ops, 32);
+      const bool b_ok = 2 * u + 1 < A.n_alns;
+      if (n_a <= kPairOps && (!b_ok || n_b <= kPairOps)) {
+        index_pair(A, W, tp, w, ai, valid, lane, cur);
+      } else {
+        index_one(A, W, tp, w, 2 * u, lane, planned);
+        if (b_ok) index_one(A, W, tp, w, 2 * u + 1, lane, planned);
+      }
+      cur = nxt;
+    }
+  }
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned);
 }
 
 // ------------------------------------------------------------------ long records: plan + carries
@@ -2893,7 +3181,13 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     hipLaunchKernelGGL(pw::plan_kernel, dim3((args->n_alns + 255) / 256), dim3(256), 0, st, *args, W);
     hipLaunchKernelGGL(pw::carry_kernel, dim3((uint32_t)ncu * 8u), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   }
-  hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+  // mostly short records (a gene panel): two per wavefront (index_pair_kernel)
+  if (args->n_short && (uint64_t)args->n_short * 4 >= (uint64_t)args->n_alns * 3)
+    hipLaunchKernelGGL(pw::index_pair_kernel,
+                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 10u)),
+                       dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+  else
+    hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
     uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;

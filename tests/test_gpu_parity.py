@@ -651,3 +651,32 @@ def test_gapassem_driver_rccl_world1(built, tmp_path):
     p.join(timeout=60)
     assert p.exitcode == 0
     assert res == _ga_cli(lay, tmp_path, True)
+
+
+def _short_fraction(paf):
+    """Records whose cs string packs to at most 64 ops (index_pair_kernel's records)."""
+    import re
+    n = short = 0
+    for ln in open(paf):
+        if ln.startswith("#"):
+            continue
+        cs = next((x[5:] for x in ln.rstrip("\n").split("\t")[12:] if x.startswith("cs:Z:")), None)
+        if cs is None:
+            continue
+        n += 1
+        short += len(re.findall(r"[:*+-]", cs)) <= 64
+    return short / max(n, 1)
+
+
+@pytest.mark.parametrize("seed,extra", [(51, []), (52, ["--subrun", 0.6, "--rev", 0.8]), (53, ["--longindel", 0.4])])
+def test_pair_index_short_records(built, tmp_path, seed, extra, monkeypatch):
+    """Mostly short records: index_pair_kernel decodes two per wavefront (one per 32-lane half);
+    the same bytes with PW_NO_PAIRS=1 (one record per wavefront) and from the oracle — odd record
+    counts, a mismatch injected into a short record, reverse strands, S runs, long indels."""
+    fa, paf = synth_paf(tmp_path, 0, seed=seed, extra=["--len-min", 90, "--len-max", 700, "--ncds", 31, "--recs", 9, *extra])
+    assert _short_fraction(paf) >= 0.8
+    same(["-r", fa, paf])
+    bad = _inject(paf, tmp_path, "mismatch", seed=seed)
+    same(["-r", fa, bad])
+    monkeypatch.setenv("PW_NO_PAIRS", "1")
+    same(["-r", fa, paf])
