@@ -90,16 +90,17 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // K0: the row of every slot (slot_row) and K1's chunk descriptor (sdesc: the chunk's first ofs
-// element | its base count << 48 | 16-byte aligned << 63), one workgroup per row, coalesced
+// element | its base count << 48 | 16-byte aligned << 63), gridDim.y workgroups per row (a few
+// long rows still fill the chip), coalesced
 constexpr uint64_t kDescVec = 1ull << 63;
 __global__ __launch_bounds__(256) void slot_rows(const pw_msa_args A, int32_t* slot_row, uint64_t* sdesc) {
-  if (blockIdx.x == 0 && threadIdx.x < 4)  // minmax sentinels (no host copy on the stream)
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4)  // minmax sentinels (no host copy on the stream)
     A.minmax[threadIdx.x] = threadIdx.x == 1 ? -1 : INT_MAX;
   for (uint32_t r = blockIdx.x; r < A.n_rows; r += gridDim.x) {
     const int64_t b = A.slot_base[r], e = A.slot_base[r + 1];
     const uint64_t roff = A.row_off[r];
     const int len = A.row_len[r];
-    for (int64_t k = b + threadIdx.x; k < e; k += 256) {
+    for (int64_t k = b + (int64_t)blockIdx.y * 256 + threadIdx.x; k < e; k += (int64_t)gridDim.y * 256) {
       slot_row[k] = (int32_t)r;
       const int i0 = (int)(k - b) * kChunk;
       const uint64_t nv = (uint64_t)min(max(len - i0, 0), kChunk);
@@ -990,6 +991,20 @@ __global__ __launch_bounds__(256) void gap_scan(const pw_msa_args A, pw_msa_refi
   }
 }
 
+// K6' (refineMSA without removeConsGaps, GapAssem.cpp:1143-1162): no column moves, so no G(c) —
+// the consensus string is the called columns [mincol, maxcol] with '-' printed as '*', one
+// elementwise pass (K6 + K7 are two launches and a scan for the same bytes)
+__global__ __launch_bounds__(256) void cons_mark(const pw_msa_args A, pw_msa_refine_args R) {
+  const int lo = A.minmax[0], hi = A.minmax[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // (= K7: set when maxcol is a column of the layout)
+    *R.cons_len = hi >= 0 && hi < A.n_cols && hi >= lo ? hi - lo + 1 : 0;
+  const int a = max(lo, 0), z = min(hi, A.n_cols - 1);
+  for (int c = a + (int)(blockIdx.x * 256 + threadIdx.x); c <= z; c += (int)(gridDim.x * 256)) {
+    const uint8_t ch = A.consensus[c];
+    R.cons_out[c - lo] = ch == '-' ? (uint8_t)'*' : ch;
+  }
+}
+
 __device__ __forceinline__ int gx(const pw_msa_refine_args& R, int n_cols, int c) {
   return c < 0 ? 0 : R.gap_prefix[c < n_cols ? c : n_cols - 1];
 }
@@ -1107,7 +1122,8 @@ static int msa_count(const pw_msa_args* a, void* stream, bool call) {
   int32_t* tstart = a->scratch + pw::tstart_word(a->n_slots);
   int32_t* rinfo = a->scratch + pw::rinfo_word(a->n_slots);
   uint64_t* sdesc = reinterpret_cast<uint64_t*>(tstart);  // (K1's input; K2 then writes the tile starts there)
-  hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192), dim3(256), 0, s, *a, slot_row, sdesc);
+  const unsigned sy = a->n_rows >= 2048 ? 1u : (2048u / a->n_rows < 64u ? 2048u / a->n_rows : 64u);
+  hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192, sy), dim3(256), 0, s, *a, slot_row, sdesc);
   const uint64_t nb1 = ((a->n_slots + 3) / 4 + 3) / 4;  // 4 slots per wave, 4 waves per workgroup
   // (persistent: ~2 rounds of resident waves, each streaming many groups)
   hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 2048 ? nb1 : 2048)), dim3(256), 0, s, *a,
@@ -1150,6 +1166,11 @@ extern "C" int pw_msa_refine(const pw_msa_args* a, const pw_msa_refine_args* r, 
   if (r->remove_gaps && (!r->row_offset || !r->ofs_out || !r->offset_out || !r->numgaps_out)) return PW_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const unsigned ntiles = (unsigned)pw_msa_refine_tiles(a->n_cols);
+  if (!r->remove_gaps) {  // (gap_prefix / tile_gaps are not written: nothing reads them)
+    const unsigned nb = (unsigned)(((uint64_t)a->n_cols + 255) / 256);
+    hipLaunchKernelGGL(pw::cons_mark, dim3(nb < 4096 ? nb : 4096), dim3(256), 0, s, *a, *r);
+    return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+  }
   hipLaunchKernelGGL(pw::gap_tiles, dim3(ntiles), dim3(256), 0, s, *a, *r);
   hipLaunchKernelGGL(pw::gap_scan, dim3(ntiles), dim3(256), 0, s, *a, *r);
   if (r->remove_gaps) {

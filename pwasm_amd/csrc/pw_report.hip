@@ -79,6 +79,7 @@ constexpr uint32_t kNBig = (1u << 19) - 1;  // evtbases length field saturates h
 constexpr uint32_t kFnAcgt = 1u << 19;      // query + record literals all A/C/G/T (PW_REF_ACGT)
 constexpr int kTx = 32;         // pre-rendered target-context record (length byte + field)
 constexpr int kIndexOcc = 5;    // index_kernel: waves per SIMD the register budget is sized for
+constexpr int kPairOcc = 4;     // index_pair_kernel: (two records per wave hold more live state: 128 VGPRs)
 constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)
 
 // Render record of one event (index_kernel -> render_kernel), 32 bytes.
@@ -2257,7 +2258,7 @@ __device__ __forceinline__ void index_one(const pw_report_args& A, const Work& W
   index_record(A, W, tab, w, ai, lane, p, B);
 }
 
-__global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_pair_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves, kPairOcc) void index_pair_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
@@ -2276,20 +2277,22 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_pair_kernel(pw
     pair_head(A, 2 * u + (uint32_t)(lane >> 5), hl, cur);
     for (; u < nu; u += stride) {
       const uint32_t un = u + stride;
-      PairHead nxt;
-      pair_head(A, 2 * (un < nu ? un : u) + (uint32_t)(lane >> 5), hl, nxt);
+      const uint32_t nx = 2 * (un < nu ? un : u) + (uint32_t)(lane >> 5);
       const uint32_t ai = 2 * u + (uint32_t)(lane >> 5);
       const bool valid = ai < A.n_alns;
       const uint32_t n_a = (uint32_t)__builtin_amdgcn_readlane((int)cur.d.n_ops, 0);
       const uint32_t n_b = (uint32_t)__builtin_amdgcn_readlane((int)cur.d.n_ops, 32);
       const bool b_ok = 2 * u + 1 < A.n_alns;
       if (n_a <= kPairOps && (!b_ok || n_b <= kPairOps)) {
+        PairHead nxt;  // (the next unit's heads in flight while this pair is decoded)
+        pair_head(A, nx, hl, nxt);
         index_pair(A, W, tp, w, ai, valid, lane, cur);
-      } else {
-        index_one(A, W, tp, w, 2 * u, lane, planned);
-        if (b_ok) index_one(A, W, tp, w, 2 * u + 1, lane, planned);
+        cur = nxt;
+      } else {  // (no head prefetch across the single-record path: it holds index_record's registers)
+#pragma unroll 1
+        for (uint32_t x = 2 * u; x < 2 * u + (b_ok ? 2u : 1u); x++) index_one(A, W, tp, w, x, lane, planned);
+        pair_head(A, nx, hl, cur);
       }
-      cur = nxt;
     }
   }
   index_long_blocks(A, W, tp, w, lane, wv, stride, planned);

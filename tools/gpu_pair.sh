@@ -5,7 +5,7 @@ set -uo pipefail
 TAG=${1:-pair}
 mkdir -p gpurun_out/pair_$TAG
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -x -q --timeout 120 --timeout-method thread -k "pair or cfg3 or kat or edge_mix or error_midway or cfg2 or long" > gpurun_out/pair_$TAG/pytest.log 2>&1 || { echo "pytest failed: $?"; grep -E "FAIL|Error|error|first difference|oracle:|hip:" gpurun_out/pair_$TAG/pytest.log | head -30; tail -5 gpurun_out/pair_$TAG/pytest.log; exit 1; }
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gapassem_refine.py tests/test_gapassem_kat.py tests/test_gapassem_shard.py -m gpu -x -q --timeout 120 --timeout-method thread -k "gapassem or refine or msa or pair or cfg3 or kat or edge_mix or error_midway or cfg2 or long" > gpurun_out/pair_$TAG/pytest.log 2>&1 || { echo "pytest failed: $?"; grep -E "FAIL|Error|error|first difference|oracle:|hip:" gpurun_out/pair_$TAG/pytest.log | head -30; tail -5 gpurun_out/pair_$TAG/pytest.log; exit 1; }
 tail -2 gpurun_out/pair_$TAG/pytest.log
 for mode in pairs single; do
   if [ $mode = single ]; then export PW_NO_PAIRS=1; else unset PW_NO_PAIRS; fi
