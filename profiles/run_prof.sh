@@ -14,7 +14,8 @@ i=0
 for G in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
          "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT" \
-         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA"; do
+         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA" \
+         "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 5 120 rocprofv3 --pmc $G --kernel-include-regex "pw::" -d "$OUT/pmc_$i" -o run --output-format csv -- python3 $B > /dev/null 2> "$OUT/pmc_$i.err" || { echo "pmc pass $i failed"; tail -5 "$OUT/pmc_$i.err"; exit 1; }
 done

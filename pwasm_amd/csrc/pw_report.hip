@@ -58,6 +58,7 @@ namespace pw {
 #define LDS __attribute__((address_space(3)))
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));  // 16-byte copies
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+typedef unsigned int v4a4 __attribute__((ext_vector_type(4), aligned(4)));  // 16 bytes at a dword address
 
 __constant__ Tables c_tables = build_tables();
 
@@ -71,6 +72,7 @@ constexpr int kLine = 92;       // render_kernel: report lines up to this long a
 constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
 static_assert(kLine + kLSlack <= 144, "line buffer stride");
+constexpr uint32_t kDropOff = 0xFFFFFF00u;  // a buffer-store offset past any range: the store is dropped
 constexpr int kLStride = 144;  // line buffer stride (16-byte aligned for the copy-out reads)
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
@@ -2393,18 +2395,27 @@ __device__ __forceinline__ HotRaw load_hot(const Work& W, uint64_t c, int lane) 
   r.b = p[1];
   return r;
 }
-__device__ __forceinline__ Hot decode_hot(HotRaw r, bool valid) {
-  pin(r.a);
-  pin(r.b);
+// The record is copied out of the load's registers here, before the next prefetch is issued (an
+// explicit move into other registers, ordered as memory): left to hipcc, the copy sinks to the
+// loop latch, after the next load, whose result then needs other registers and a move of its own
+// at the latch — which waits for that load and exposes the prefetch's whole latency.
+__device__ __forceinline__ Hot decode_hot(const HotRaw& r, bool valid) {
   Hot h;
-  h.qb = r.a.x;
-  h.L = (int32_t)r.a.y;
-  h.qp = (int32_t)r.a.z;
-  h.tloc = (int32_t)r.a.w;
-  h.ls = r.b.x;
-  h.fn = valid ? r.b.y : kNoEv;
-  h.l0 = r.b.z;
-  h.l1 = r.b.w;
+  uint32_t qb, L, qp, tl, ls, fn, l0, l1;
+  asm volatile(
+      "v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"
+      "v_mov_b32 %4, %12\n\tv_mov_b32 %5, %13\n\tv_mov_b32 %6, %14\n\tv_mov_b32 %7, %15"
+      : "=&v"(qb), "=&v"(L), "=&v"(qp), "=&v"(tl), "=&v"(ls), "=&v"(fn), "=&v"(l0), "=&v"(l1)
+      : "v"(r.a.x), "v"(r.a.y), "v"(r.a.z), "v"(r.a.w), "v"(r.b.x), "v"(r.b.y), "v"(r.b.z), "v"(r.b.w)
+      : "memory");
+  h.qb = qb;
+  h.L = (int32_t)L;
+  h.qp = (int32_t)qp;
+  h.tloc = (int32_t)tl;
+  h.ls = ls;
+  h.fn = valid ? fn : kNoEv;
+  h.l0 = l0;
+  h.l1 = l1;
   return h;
 }
 
@@ -2505,6 +2516,12 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
   HotRaw hn = load_hot(W, c + nw, lane);
   RenderPre pre;
   render_pre(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
+  {  // (six dropped stores: the loop is entered with the same count of memory operations after the
+     // render_pre loads as each iteration leaves — hipcc's wait at the loop head takes the smaller)
+    const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)A.text, (short)0, 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 6; j++) __builtin_amdgcn_raw_buffer_store_b32(0u, rs0, kDropOff + 16u * (uint32_t)j, 0, 0);
+  }
   for (; c < W.n_chunks; c += nw) {
     const uint64_t s = c * kWave + (uint64_t)lane;
     const bool act = h.fn != kNoEv;
@@ -2614,7 +2631,8 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       const uint32_t need = ((B + 15u) & ~15u) + kPageSlack;
       unsigned long long a = 0;
       if (lane == 0) a = atomicAdd(W.arena_used, (unsigned long long)need);
-      a = __shfl(a, 0, kWave);
+      a = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, 0) |
+          (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), 0) << 32;  // (uniform: SGPRs)
       P = W.arena0 + a;
       if (P + need > A.text_total) {  // capacity violated: report, never write outside
         ok = false;
@@ -2646,22 +2664,34 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         A.results[ai].page_last = (uint32_t)c;
       }
     }
-    if (ok && B > 0) {
-      if (need_fix) {  // the line's destination for fixup_kernel
-        Fixup f;
-        f.s = (uint32_t)s;
-        f.pad = 0;
-        f.dst = g0;
-        W.fix[s] = f;
-      }
-      // copy-out: every lane stores its own line at page offset my_off (a long line: its first
-      // kLine bytes, fixup_kernel rewrites it) as dwords realigned to the page, 16 bytes per store,
-      // its last group first.  A store's dwords past the line's end are overwritten later by the
+    if (need_fix) {  // the line's destination for fixup_kernel
+      Fixup f;
+      f.s = (uint32_t)s;
+      f.pad = 0;
+      f.dst = g0;
+      W.fix[s] = f;
+    }
+    {
+      // copy-out: every lane places its own line at page offset my_off (a long line: its first
+      // kLine bytes, fixup_kernel rewrites it) as dwords realigned to the page, 16 bytes per group,
+      // its last group first.  A group's dwords past the line's end are overwritten later by the
       // next line's first group (written in the last round), and that group's first dword is the
       // shared one: the next line ORs this line's tail bytes into it (shuffled from the previous
-      // non-empty lane).  The page's last line may store up to 12 bytes past B: the page keeps
-      // kPageSlack bytes free.
-      uint8_t* const gb = A.text + P;
+      // non-empty lane).  The page's last line may write up to 12 bytes past B: the page keeps
+      // kPageSlack bytes free.  The groups go to an LDS image of the page (then stored as
+      // contiguous 1 KB rows), or, for an arena page, straight to global memory.
+      // Every global store here is a buffer store issued by every lane: one with no bytes to write
+      // gets an offset past the buffer's range and the hardware drops it (as branches, the next
+      // iteration's first wait — for the render_pre loads, which precede these stores — would count
+      // them as possibly absent and wait for them too: vmcnt is in order).
+      const bool wr = ok && B > 0;  // (uniform)
+      // (the descriptor's fields through readfirstlane: hipcc otherwise treats the arena path's
+      // values as divergent and wraps each store in a waterfall loop)
+      const uint64_t pa = (uint64_t)A.text + (wr ? P : 0ull);
+      const uint64_t Pu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32)) << 32;
+      const int nrec = __builtin_amdgcn_readfirstlane(wr ? (int)(B + (uint32_t)kPageSlack) : 0);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)Pu, (short)0, nrec, 0x00020000);
       const uint64_t ne = __ballot(linelen > 0);
       const int ln = linelen > kLine ? kLine : linelen;
       const uint32_t sh = my_off & 3u, a0 = my_off & ~3u;
@@ -2688,20 +2718,36 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);
       const int kmax = linelen > 0 ? ((int)sh + ln - 1) >> 2 : -1;  // last dword (from a0) holding a line byte
       const int jmax = kmax >> 2;
-      PW_GLOBAL uint32_t* gd = (PW_GLOBAL uint32_t*)(gb + a0);
+      auto group = [&](int j) -> v4u {  // the line's dwords [4j, 4j + 4) realigned to the page
+        uint32_t v[4];
 #pragma unroll
-      for (int j = 5; j >= 0; j--) {
-        if (j <= jmax) {
-          uint32_t v[4];
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int k = 4 * j + i;
-            const uint32_t cur = k < 24 ? Lw[k] : 0u, prv = k == 0 ? 0u : Lw[k - 1];
-            v[i] = __builtin_amdgcn_perm(cur, prv, sel);
-          }
-          if (j == 0) v[0] |= ptail;
-          *reinterpret_cast<PW_GLOBAL v4u*>(gd + 4 * j) = (v4u){v[0], v[1], v[2], v[3]};
+        for (int i = 0; i < 4; i++) {
+          const int k = 4 * j + i;
+          const uint32_t cur = k < 24 ? Lw[k] : 0u, prv = k == 0 ? 0u : Lw[k - 1];
+          v[i] = __builtin_amdgcn_perm(cur, prv, sel);
         }
+        if (j == 0) v[0] |= ptail;
+        return (v4u){v[0], v[1], v[2], v[3]};
+      };
+      if (B + (uint32_t)kPageSlack <= (uint32_t)PW_PAGE_BYTES) {  // (uniform) the page in place:
+        // every lane writes its groups into the wave's line buffer at its page offset (the page
+        // image; the lines are in Lw already), then the image goes out as contiguous 1 KB stores —
+        // one cache line per 8 lanes instead of one or two per lane
+        wave_sync();
+        LDS uint8_t* img = w->line;
+#pragma unroll
+        for (int j = 5; j >= 0; j--)
+          if (j <= jmax) *reinterpret_cast<LDS v4a4*>(img + a0 + 16u * (uint32_t)j) = group(j);
+        wave_sync();
+#pragma unroll
+        for (int q = 0; q < 8; q++) {  // (PW_PAGE_BYTES / 1024 rows; rows past B are dropped)
+          const uint32_t o = 1024u * (uint32_t)q + 16u * (uint32_t)lane;
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const LDS v4u*>(img + o), rs, o < B ? o : kDropOff, 0, 0);
+        }
+      } else {  // an arena page: every lane stores its own groups
+#pragma unroll
+        for (int j = 5; j >= 0; j--)
+          __builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, 0);
       }
     }
     wave_sync();
