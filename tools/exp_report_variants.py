@@ -6,7 +6,9 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   noline   no line is built (every line 78 bytes of whatever the buffer holds: timing only)
   nowin    the per-lane query window is not loaded (constant bytes: timing only)
   nohot    the Hot records are replaced by synthetic insertions after the load (timing only)
-  nocopy   render's copy-out stores skipped (timing only)
+  nocopy   render's copy-out (LDS page image + stores) skipped (timing only)
+  fx_inline  fixup_kernel reads outside its windows inline (no out-of-line call per byte)
+  fx_bigwin  fixup_kernel stages 128 query bytes and 64 literal bytes per line
 Usage: python tools/exp_report_variants.py [names...]"""
 import os
 import subprocess
@@ -26,8 +28,26 @@ PATCHES = {
     "nowin": [("  for (int q = 0; q < kQWin / 16; q++) p.q[q] = a0[q];\n  p.qlo = x0a;",
                "  for (int q = 0; q < kQWin / 16; q++) p.q[q] = (v4u){0x41434741u, 0x54414341u, 0x47544341u, 0x41434741u};\n  p.qlo = x0a;")],
     "nohot": [("  r.a = p[0];\n  r.b = p[1];\n  return r;", "  r.a = p[0];\n  r.b = p[1];\n  if (cc > 60000000) return r;\n  r.a = (v4u){0u, 2000u, 100u + 64u * (uint32_t)(cc & 15u) + lane, 50u};\n  r.b = (v4u){0u, (uint32_t)(PW_OP_INS << 30) | (1u << 28) | kFnAcgt | 2u, 0x41414141u, 0x41414141u};\n  return r;")],
-    "nocopy": [("      for (int j = 5; j >= 0; j--) {\n        if (j <= jmax) {",
-                "      for (int j = 5; j >= 0; j--) {\n        if (j <= jmax && A.n_alns == 0) {")],
+    "nocopy": [("      if (B + (uint32_t)kPageSlack <= (uint32_t)PW_PAGE_BYTES) {  // (uniform) the page in place:",
+                "      if (A.n_alns != 0) {\n      } else if (B + (uint32_t)kPageSlack <= (uint32_t)PW_PAGE_BYTES) {")],
+    # fixup_kernel: the global fallbacks of its Rec inline (RecFix), or 128-byte query / 64-byte
+    # literal windows instead of 48 / 32
+    "fx_inline": [("struct RecFast : Rec {\n  static constexpr bool kFast = true;\n};",
+                   "struct RecFast : Rec {\n  static constexpr bool kFast = true;\n};\nstruct RecFix : Rec {};"),
+                  ("__device__ __forceinline__ uint8_t Rc(const RecFast& r, int x) { return r.qw[x - r.qlo]; }",
+                   "__device__ __forceinline__ uint8_t Rc(const RecFast& r, int x) { return r.qw[x - r.qlo]; }\n"
+                   "__device__ __forceinline__ uint8_t Rc(const RecFix& r, int x) {\n  const unsigned o = (unsigned)(x - r.qlo);\n"
+                   "  if (o < (unsigned)r.qn) return r.qw[o];\n  return (unsigned)x < (unsigned)r.L ? r.R[x] : (uint8_t)0;\n}\n"
+                   "__device__ __forceinline__ uint8_t litb(const RecFix& r, uint32_t i) {\n  const uint32_t o = i - r.ls0;\n"
+                   "  if (o < r.ln) return (uint8_t)((o < 4 ? r.lit0 : r.lit1) >> (8 * (o & 3)));\n  const uint32_t ow = i - r.l_lo;\n"
+                   "  if (ow < r.l_n) return r.lw[ow];\n  return r.lits[i];\n}"),
+                  ("    Rec r;\n    r.lits = A.lits;\n    r.R = A.qseq + ((uint64_t)h.qb << 4);\n    r.L = h.L;\n    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;\n    r.tab = tp;",
+                   "    RecFix r;\n    r.lits = A.lits;\n    r.R = A.qseq + ((uint64_t)h.qb << 4);\n    r.L = h.L;\n    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;\n    r.tab = tp;")],
+    "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
+                  ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
+                  ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
+                   "    for (int q = 0; q < kFxQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];"),
+                  ("    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kQWin;", "    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kFxQ;")],
 }
 
 
