@@ -71,9 +71,9 @@ constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dw
 constexpr int kLine = 92;       // render_kernel: report lines up to this long are built in LDS (99.94 % at cfg2)
 constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
-static_assert(kLine + kLSlack <= 144, "line buffer stride");
+static_assert(kLine + kLSlack <= 148, "line buffer stride");
 constexpr uint32_t kDropOff = 0xFFFFFF00u;  // a buffer-store offset past any range: the store is dropped
-constexpr int kLStride = 144;  // line buffer stride (16-byte aligned for the copy-out reads)
+constexpr int kLStride = 148;  // line buffer stride (37 dwords, odd: lanes at the same line position hit 32 banks)
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
 constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, failed records)
@@ -2708,7 +2708,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       const uint32_t ptail = (uint32_t)__shfl((int)tail, prev, kWave) & (uint32_t)((1ull << (8 * sh)) - 1ull);
       uint32_t Lw[24];
       {
-        const LDS v4u* lp4 = reinterpret_cast<const LDS v4u*>(my_line);
+        const LDS v4a4* lp4 = reinterpret_cast<const LDS v4a4*>(my_line);  // (4-byte aligned: 148-byte stride)
 #pragma unroll
         for (int q = 0; q < 6; q++) {
           const v4u v = lp4[q];

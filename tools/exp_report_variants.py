@@ -9,6 +9,8 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   nocopy   render's copy-out (LDS page image + stores) skipped (timing only)
   fx_inline  fixup_kernel reads outside its windows inline (no out-of-line call per byte)
   fx_bigwin  fixup_kernel stages 128 query bytes and 64 literal bytes per line
+  tc_nowalk  tctx_kernel skips the op walk (timing only)
+  ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
 Usage: python tools/exp_report_variants.py [names...]"""
 import os
 import subprocess
@@ -43,6 +45,14 @@ PATCHES = {
                    "  if (ow < r.l_n) return r.lw[ow];\n  return r.lits[i];\n}"),
                   ("    Rec r;\n    r.lits = A.lits;\n    r.R = A.qseq + ((uint64_t)h.qb << 4);\n    r.L = h.L;\n    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;\n    r.tab = tp;",
                    "    RecFix r;\n    r.lits = A.lits;\n    r.R = A.qseq + ((uint64_t)h.qb << 4);\n    r.L = h.L;\n    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;\n    r.tab = tp;")],
+    # line buffers at an odd dword stride (148 bytes: lanes at the same line position hit 32 distinct
+    # banks instead of 16), the copy-out then reading each line with 4-byte-aligned loads
+    "ls148": [("constexpr int kLStride = 144;", "constexpr int kLStride = 148;"),
+              ("        const LDS v4u* lp4 = reinterpret_cast<const LDS v4u*>(my_line);",
+               "        const LDS v4a4* lp4 = reinterpret_cast<const LDS v4a4*>(my_line);")],
+    # tctx_kernel without the op walk (an 11-byte record of whatever the buffer holds: timing only)
+    "tc_nowalk": [("      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);",
+                   "      if (A.n_alns == 0) emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);\n      else ks.pos = 11;")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
