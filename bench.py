@@ -9,8 +9,9 @@ errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard
 seed = different target genomes; weak scaling, no data-path collective); the timed region is
 bracketed by barrier + synchronize, the max over ranks is reported.
 
-Also reported (rank 0): roofline of the dominant kernel (algorithmic bytes / its average HIP-
-event duration vs 8 TB/s) and the CPU baseline: the single-threaded oracle restatement
+Also reported (rank 0): roofline of the dominant kernel sequence (algorithmic bytes / the pass's
+average GPU time — HIP events around the K timed passes, divided by K — vs 8 TB/s) and the CPU
+baseline: the single-threaded oracle restatement
 (oracle/pafreport_oracle, kind "port") on a bounded sample of the same workload, 1 core.
 """
 import argparse
@@ -143,7 +144,7 @@ def main():
     side = torch.cuda.Stream()
     ns_ready, pass_done = torch.cuda.Event(), torch.cuda.Event()
 
-    def step(ev=None):
+    def step():
         ready = None
         if not v.skip_codan:
             side.wait_event(pass_done)
@@ -153,12 +154,8 @@ def main():
             ns_ready.record(side)
             ready = ns_ready.cuda_event
         a = pw.report_args(batch, dev)
-        if ev is not None:
-            ev[0].record(stream)
         rc = pw.lib().pw_report_events_after(pw.ctypes.byref(a), sp, ready)
         assert rc == 0
-        if ev is not None:
-            ev[1].record(stream)
         pass_done.record(stream)
         if gtab is not None:
             mg, rows, gt, padded, gathered = gtab
@@ -182,18 +179,22 @@ def main():
     ctr = dev["work"][:16].cpu().numpy().view(np.uint32)
     log(f"[rank {rank}] {n_events} events, {text_bytes} text bytes; long lines {int(ctr[1])}")
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events around the K passes as a whole (an event pair per pass would put two timestamp
+    # packets, ~5 us of GPU time, between consecutive passes)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step()
+    ev1.record(stream)
     torch.cuda.synchronize()
     t_el = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     tot_events = n_events
     tot_records = int(v.n_alns)
@@ -347,7 +348,8 @@ def main():
 def bench_gapassem(args, world, rank, dev_name):
     """BASELINE.json configs[4]: GapAssem consensus of one 200-row, ~1M-column layout (pwsynth
     cfg5, seed 5), rows sharded over the ranks (strong scaling).  A step on one GPU =
-    pw_msa_columns (count and bestChar in one pass) + pw_msa_refine; on N > 1 = pw_msa_count on the
+    pw_msa_columns_refine (count, bestChar and, without removeConsGaps, the consensus string in
+    one counting pass; with --remove-gaps + the pw_msa_refine kernels); on N > 1 = pw_msa_count on the
     rank's rows + pw_msa_call_sharded (RCCL reduce-scatter of the [n_cols x 6] histograms by
     column range + bounds, bestChar of the rank's columns, all-gather of the consensus) +
     pw_msa_refine (consensus string; with --remove-gaps also the removeConsGaps row edits).  Default removeConsGaps=false: pafreport's setting (pafreport.cpp:31,203), which is
@@ -379,9 +381,8 @@ def bench_gapassem(args, world, rank, dev_name):
     red = torch.empty(2, dtype=torch.int32, device=dev_name)
 
     def step():
-        if world == 1:  # one shard: count + call in one pass (pw_msa_columns), then refine
-            eng.columns(st)
-            eng.refine(st, remove)
+        if world == 1:  # one shard: count + call (+ the consensus string) in one pass, then refine
+            eng.columns_refine(st, remove)
             return
         counts, _ = eng.count(st)
         if rccl:  # column-sharded: reduce-scatter by column range, own-range bestChar, all-gather
@@ -405,20 +406,20 @@ def bench_gapassem(args, world, rank, dev_name):
     if not os.environ.get("PW_BENCH_NOCHECK"):  # (set by attribution sweeps of variants that count wrong)
         assert zero == 2 ** 31 - 1 and int(mm[2].item()) == 2 ** 31 - 1, "layout errors"
     stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)  # (around all K steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        evs[k][0].record(stream)
         step()
-        evs[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     t_el = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     max_el = t_el
     if world > 1:
         t = torch.tensor([t_el], dtype=torch.float64, device=dev_name)
@@ -472,7 +473,7 @@ def bench_gapassem(args, world, rank, dev_name):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": prof.get("hbm_bytes_per_launch"),
-                         "kernel": ("pw_msa_columns+pw_msa_refine" if world == 1 else "pw_msa_count+pw_msa_call+pw_msa_refine") + " (rank 0)", "kernel_ms": round(kern_ms, 4),
+                         "kernel": ("pw_msa_columns_refine" if world == 1 else "pw_msa_count+pw_msa_call+pw_msa_refine") + " (rank 0)", "kernel_ms": round(kern_ms, 4),
                          "alg_bytes_per_launch": alg,
                          "alg_formula": "SURVEY 8(d): sum_rows(16 + 3*seqlen) + 25*n_cols",
                          "occupancy_waves_per_simd": prof.get("occupancy_waves_per_simd"),

@@ -224,6 +224,10 @@ typedef struct pw_msa_refine_args {
 } pw_msa_refine_args;
 uint64_t pw_msa_refine_tiles(int32_t n_cols);
 int pw_msa_refine(const pw_msa_args* args, const pw_msa_refine_args* refine, void* stream);
+/* buildMSA + refineMSA of one shard holding every row (GapAssem.cpp:1088-1106, 1143-1181):
+ * = pw_msa_columns then pw_msa_refine, the same results; without remove_gaps the consensus string
+ * and its length are written by the counting pass itself (gap_prefix / tile_gaps untouched). */
+int pw_msa_columns_refine(const pw_msa_args* args, const pw_msa_refine_args* refine, void* stream);
 
 /* ---------------------------------------------------------------- GapAssem over RCCL
  * One process per GPU; the 128-byte id travels over any side channel (torch.distributed in

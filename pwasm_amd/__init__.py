@@ -124,6 +124,7 @@ _SIGS = {
                                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_msa_refine_tiles": (ctypes.c_uint64, [ctypes.c_int32]),
     "pw_msa_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
+    "pw_msa_columns_refine": (ctypes.c_int, [ctypes.POINTER(MsaArgs), ctypes.POINTER(MsaRefineArgs), ctypes.c_void_p]),
     "pw_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "pw_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_void_p, ctypes.c_int]),
     "pw_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),

@@ -706,7 +706,8 @@ __device__ __forceinline__ uint8_t best_char(const int (&v)[6]) {
 __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_args A, const int32_t* __restrict__ ckpt,
                                                               const uint16_t* __restrict__ runs,
                                                               const int32_t* __restrict__ rinfo,
-                                                              const int32_t* __restrict__ tstart, int call) {
+                                                              const int32_t* __restrict__ tstart, int call,
+                                                              uint8_t* __restrict__ cons_star, int32_t* cons_len) {
   __shared__ __attribute__((aligned(16))) TileLds L;
   LDS TileLds* lp = (LDS TileLds*)&L;
   const int tid = threadIdx.x, lane0 = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -895,12 +896,15 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
   }
   if (call) {  // pw_msa_columns (all rows in this launch): the call step from the same table
     const int zlo = A.minmax[0], zhi = A.minmax[1];
+    // (pw_msa_columns_refine without removeConsGaps: refineMSA's consensus string too, as K6')
+    if (cons_star && blockIdx.x == 0 && tid == 0) *cons_len = zhi >= 0 && zhi < A.n_cols && zhi >= zlo ? zhi - zlo + 1 : 0;
     for (int c = tid; c < cw; c += 64 * kCntWaves) {
       int v[6];
 #pragma unroll
       for (int f = 0; f < 6; f++) v[f] = (int)tab[f * kCntW + cnt_swz(c)];
       const uint8_t best = best_char(v);
       A.consensus[c0 + c] = best;
+      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) cons_star[c0 + c - zlo] = best == '-' ? (uint8_t)'*' : best;
       if (best == 0 && c0 + c >= zlo && c0 + c <= zhi) atomicMin(&A.minmax[3], c0 + c);
     }
   }
@@ -1109,7 +1113,8 @@ static bool msa_args_ok(const pw_msa_args* a) {
 }
 
 // count (+ with call, the bestChar step in tile_counts' epilogue: every row is in this launch)
-static int msa_count(const pw_msa_args* a, void* stream, bool call) {
+static int msa_count(const pw_msa_args* a, void* stream, bool call, uint8_t* cons_star = nullptr,
+                     int32_t* cons_len = nullptr) {
   if (!msa_args_ok(a)) return PW_E_ARG;
   if (a->n_slots >= (1ull << 27)) return PW_E_ARG;  // (K1's 32-bit buffer offsets: < 34 G bases)
   hipStream_t s = (hipStream_t)stream;
@@ -1132,7 +1137,7 @@ static int msa_count(const pw_msa_args* a, void* stream, bool call) {
                      rinfo, runs, tstart);
   const unsigned ntiles = (unsigned)((a->n_cols + pw::kCntW - 1) / pw::kCntW);
   hipLaunchKernelGGL(pw::tile_counts, dim3(ntiles), dim3(64 * pw::kCntWaves), 0, s, *a, ckpt, runs, rinfo, tstart,
-                     call ? 1 : 0);
+                     call ? 1 : 0, cons_star, cons_len);
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
@@ -1182,4 +1187,13 @@ extern "C" int pw_msa_refine(const pw_msa_args* a, const pw_msa_refine_args* r, 
     hipLaunchKernelGGL(pw::row_finish, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(64), 0, s, *a, *r);
   }
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
+}
+
+// pw_msa_columns + pw_msa_refine; without removeConsGaps the consensus string comes out of
+// tile_counts' call epilogue (no column moves: no G(c) scan, one launch less)
+extern "C" int pw_msa_columns_refine(const pw_msa_args* a, const pw_msa_refine_args* r, void* stream) {
+  if (!msa_args_ok(a) || !r || !r->cons_out || !r->cons_len) return PW_E_ARG;
+  if (!r->remove_gaps) return msa_count(a, stream, true, r->cons_out, r->cons_len);
+  const int rc = msa_count(a, stream, true);
+  return rc != PW_OK ? rc : pw_msa_refine(a, r, stream);
 }

@@ -2833,8 +2833,10 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
       for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
 #pragma unroll
       for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
-      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;  // forward position of the event
-      int x0 = fc - kTcQ / 2;
+      // forward query bytes of the context: [fc - 5, fc + n + 5) for a '+' record, [fc - n - 5,
+      // fc + 5] for a '-' record (n <= 12 unless abbreviated), fc = the event's forward position
+      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;
+      int x0 = fc - (r.rev ? kTcQ / 2 : 8);
       if (x0 < 0) x0 = 0;
       const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
       const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);

@@ -201,6 +201,17 @@ class HipEngine:
         self._rc("pw_msa_call", self.lib.pw_msa_call(ctypes.byref(st["args"]), self.stream.cuda_stream))
         return st["d"]["cons"], st["d"]["mm"]
 
+    def columns_refine(self, st, remove_gaps: bool):
+        """columns + refine of a single shard holding every row (pw_msa_columns_refine: without
+        removeConsGaps the consensus string comes out of the counting pass)."""
+        d, ra = st["d"], st["rargs"]
+        ra.remove_gaps = 1 if remove_gaps else 0
+        if remove_gaps:
+            d["ngo"].copy_(d["ng0"])
+        self._rc("pw_msa_columns_refine", self.lib.pw_msa_columns_refine(ctypes.byref(st["args"]), ctypes.byref(ra),
+                                                                         self.stream.cuda_stream))
+        return d["counts"], d["mm"]
+
     def refine(self, st, remove_gaps: bool):
         """Launch pw_msa_refine (device results stay in st["d"])."""
         d, ra = st["d"], st["rargs"]

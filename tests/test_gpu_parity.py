@@ -586,6 +586,47 @@ def test_msa_columns_fused_equals_count_call(built, tmp_path, zero):
     assert (int(mm[3]) != 2 ** 31 - 1) == zero  # (the zero-coverage column is found by both)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("remove", [False, True])
+def test_msa_columns_refine_equals_columns_then_refine(built, tmp_path, remove):
+    """pw_msa_columns_refine (without removeConsGaps: the consensus string written by tile_counts'
+    call epilogue) against pw_msa_columns + pw_msa_refine on the same staged layout: consensus
+    string, its length, minmax and (remove) every row's offset / numgaps / ofs identical."""
+    import torch
+    from pwasm_amd import gapassem
+    rng = random.Random(77 + remove)
+    rows = []
+    for r in range(40):
+        n = rng.randint(300, 5000)
+        seq = "".join(rng.choice("ACGTACGTNacgt-") for _ in range(n))
+        ofs = [0] + [rng.choice([0] * 40 + [1, 2, 7]) for _ in range(n - 1)]
+        rows.append((rng.randint(0, 6000), seq, ofs, rng.randint(0, 15), rng.randint(0, 15), r % 2))
+    lay_p = tmp_path / "cr.pwl"
+    write_pwl(lay_p, rows)
+    lay = gapassem.Layout(str(lay_p))
+    eng = gapassem.HipEngine("cuda:0")
+    st = eng.stage(lay, range(lay.n), lay.length)
+    d = st["d"]
+    eng.columns(st)
+    cons, rws = eng.refine_host(st, remove)
+    want_mm = d["mm"].clone()
+    d["cout"].fill_(7)
+    d["clen"].fill_(-5)
+    d["cons"].fill_(9)
+    eng.columns_refine(st, remove)
+    torch.cuda.synchronize()
+    clen = int(d["clen"].cpu().item())
+    assert clen == len(cons)
+    assert bytes(d["cout"][:clen].cpu().numpy()) == cons
+    assert d["mm"].tolist() == want_mm.tolist()
+    if remove:
+        offo, ngo, ofso = d["offo"].cpu().numpy(), d["ngo"].cpu().numpy(), d["ofso"].cpu().numpy()
+        for k, r in enumerate(st["rows"]):
+            o = int(st["row_off"][k])
+            assert (int(offo[k]), int(ngo[k])) == rws[r][:2]
+            assert (ofso[o:o + int(st["lens"][k])] == rws[r][2]).all()
+
+
 # ---------------------------------------------------------------- RCCL collectives C-ABI
 def test_msa_counts_allreduce_world1(built, tmp_path):
     """pw_comm_* + pw_msa_counts_allreduce / reduce_scatter on a one-rank RCCL communicator:
