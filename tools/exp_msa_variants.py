@@ -5,6 +5,8 @@
   nowin    the row window is not stored to LDS (loads kept, reads see a stale window)
   noruns   the gap-run ORs into the bitmap are skipped
   rp_lds   tools/variants/row_prefix_lds.patch (row_prefix stages the row's runs in LDS)
+  k1_3ahead  row_chunk_sums with three groups' loads in flight instead of two
+  k1_32b   tools/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
 Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
 import os
 import subprocess
@@ -46,6 +48,37 @@ def make(name):
         p = os.path.join(TMP, "rp_lds.hip")
         open(p, "w").write(s)
         subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_prefix_lds.patch")], check=True)
+        s = open(p).read()
+    elif name == "k1_3ahead":  # row_chunk_sums with three groups' loads in flight (unrolled by three)
+        s = sub(s, """  SumPre p0, p1;
+  sums_load(A, sums_desc(A, sdesc, g, lane), g, lane, p0);
+  sums_load(A, sums_desc(A, sdesc, g + nw, lane), g + nw, lane, p1);
+  uint64_t dn = sums_desc(A, sdesc, g + 2 * nw, lane);""", """  SumPre p0, p1, p2;
+  sums_load(A, sums_desc(A, sdesc, g, lane), g, lane, p0);
+  sums_load(A, sums_desc(A, sdesc, g + nw, lane), g + nw, lane, p1);
+  sums_load(A, sums_desc(A, sdesc, g + 2 * nw, lane), g + 2 * nw, lane, p2);
+  uint64_t dn = sums_desc(A, sdesc, g + 3 * nw, lane);""")
+        s = sub(s, """    const uint64_t dnn = sums_desc(A, sdesc, g + 3 * nw, lane);
+    asm volatile("" : "+v"(dn)::"memory");
+    sums_load(A, dn, g + 2 * nw, lane, p);""", """    const uint64_t dnn = sums_desc(A, sdesc, g + 4 * nw, lane);
+    asm volatile("" : "+v"(dn)::"memory");
+    sums_load(A, dn, g + 3 * nw, lane, p);""")
+        s = sub(s, """  for (uint32_t k = 2; k <= n_mine; k += 2) {
+    step(p0);
+    step(p1);
+  }
+  if (n_mine & 1) step(p0);""", """  for (uint32_t k = 3; k <= n_mine; k += 3) {
+    step(p0);
+    step(p1);
+    step(p2);
+  }
+  if (n_mine % 3 >= 1) step(p0);
+  if (n_mine % 3 == 2) step(p1);""")
+    elif name == "k1_32b":  # tools/variants/row_chunk_sums_32bases.patch
+        os.makedirs(TMP, exist_ok=True)
+        p = os.path.join(TMP, "k1_32b.hip")
+        open(p, "w").write(s)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_chunk_sums_32bases.patch")], check=True)
         s = open(p).read()
     elif name != "cur":
         raise SystemExit(f"unknown variant {name}")

@@ -7,7 +7,7 @@ RX=${2:-"pw::(render|index|tctx)_kernel"}
 O=gpurun_out/rpmc_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-gapassem"
+B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --no-gapassem ${BENCH_ARGS:-}"
 i=0
 for G in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
          "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT" \
