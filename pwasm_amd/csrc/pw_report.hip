@@ -74,6 +74,8 @@ constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 
 static_assert(kLine + kLSlack <= 148, "line buffer stride");
 constexpr uint32_t kDropOff = 0xFFFFFF00u;  // a buffer-store offset past any range: the store is dropped
 constexpr int kLStride = 148;  // line buffer stride (37 dwords, odd: lanes at the same line position hit 32 banks)
+// (render's copy-out builds an in-place page, <= PW_PAGE_BYTES, over the wave's line buffers)
+static_assert(kWave * kLStride >= PW_PAGE_BYTES, "the LDS page image must fit the wave's line buffers");
 constexpr int kMaxEv = 12;      // MAX_EVLEN, pafreport.cpp:919
 constexpr int32_t kNoStop = INT32_MAX;
 constexpr uint32_t kNoEv = 0xFFFFFFFFu;  // empty event slot (merged '*' runs, failed records)

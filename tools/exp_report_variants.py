@@ -10,6 +10,8 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   fx_inline  fixup_kernel reads outside its windows inline (no out-of-line call per byte)
   fx_bigwin  fixup_kernel stages 128 query bytes and 64 literal bytes per line
   tc_nowalk  tctx_kernel skips the op walk (timing only)
+  rw2      render_kernel in 2-wave workgroups (6 per CU)
+  tw2      tctx_kernel in 2-wave workgroups (8 per CU)
   ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
 Usage: python tools/exp_report_variants.py [names...]"""
 import os
@@ -53,6 +55,27 @@ PATCHES = {
     # tctx_kernel without the op walk (an 11-byte record of whatever the buffer holds: timing only)
     "tc_nowalk": [("      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);",
                    "      if (A.n_alns == 0) emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);\n      else ks.pos = 11;")],
+    # render_kernel in 2-wave workgroups, 6 per CU (same 3 waves/SIMD; a workgroup's LDS frees
+    # when its slower wave ends, so smaller workgroups pack the CU more tightly)
+    "rw2": [("constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)",
+             "constexpr int kRenderOcc = 6;   // render_kernel: workgroups per CU (LDS-limited)\nconstexpr int kRenderWaves = 2;"),
+            ("__global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_report_args A, Work W) {\n  __shared__ SmallTables tab;\n  __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];\n  LDS SmallTables* tp = (LDS SmallTables*)&tab;\n  stage_small_tables(tp, threadIdx.x, kWave * kWaves);",
+             "__global__ __launch_bounds__(kWave* kRenderWaves, 3) void render_kernel(pw_report_args A, Work W) {\n  __shared__ SmallTables tab;\n  __shared__ __attribute__((aligned(16))) RenderWave rw[kRenderWaves];\n  LDS SmallTables* tp = (LDS SmallTables*)&tab;\n  stage_small_tables(tp, threadIdx.x, kWave * kRenderWaves);"),
+            ("  const uint64_t nw = (uint64_t)gridDim.x * kWaves;\n\n  uint64_t c = (uint64_t)blockIdx.x * kWaves + wv;\n  if (c >= W.n_chunks) return;\n  Hot h = decode_hot(load_hot(W, c, lane), true);",
+             "  const uint64_t nw = (uint64_t)gridDim.x * kRenderWaves;\n\n  uint64_t c = (uint64_t)blockIdx.x * kRenderWaves + wv;\n  if (c >= W.n_chunks) return;\n  Hot h = decode_hot(load_hot(W, c, lane), true);"),
+            ("    uint64_t rg = (W.n_chunks + nwave - 1) / nwave;", "    uint64_t rg = (W.n_chunks + pw::kRenderWaves - 1) / pw::kRenderWaves;"),
+            ("    hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);",
+             "    hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kRenderWaves), 0, st, *args, W);")],
+    # tctx_kernel in 2-wave workgroups, 8 per CU (same 4 waves/SIMD, finer packing)
+    "tw2": [("__global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, Work W) {",
+             "constexpr int kTctxWaves = 2;\n__global__ __launch_bounds__(kWave* kTctxWaves) void tctx_kernel(pw_report_args A, Work W) {"),
+            ("  __shared__ __attribute__((aligned(16))) TctxWave tw[kWaves];", "  __shared__ __attribute__((aligned(16))) TctxWave tw[kTctxWaves];"),
+            ("  stage_small_tables(tp, threadIdx.x, kWave * kWaves);\n  __syncthreads();\n  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  LDS TctxWave* w",
+             "  stage_small_tables(tp, threadIdx.x, kWave * kTctxWaves);\n  __syncthreads();\n  const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);\n  LDS TctxWave* w"),
+            ("  const uint64_t gstride = (uint64_t)gridDim.x * kWaves;\n  uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv;",
+             "  const uint64_t gstride = (uint64_t)gridDim.x * kTctxWaves;\n  uint64_t gi = (uint64_t)blockIdx.x * kTctxWaves + wv;"),
+            ("    uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;\n    if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;\n    hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);",
+             "    uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kTctxWaves + 1;\n    if (tg > (uint64_t)ncu * 8u) tg = (uint64_t)ncu * 8u;\n    hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kTctxWaves), 0, st, *args, W);")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
