@@ -78,9 +78,10 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane l gets lane
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// A record's head in two prefetch stages (vector loads, so each wait is a vmcnt wait in issue
-// order): its extent, offset and query length two records ahead, then its first window's two
-// aligned dwords per lane one record ahead.  Addresses past the record are clamped to its last
+// A record's head in two prefetch stages: its extent, offset and query length two records ahead
+// (uniform: scalar loads — as per-lane vector loads every lane's copy went through the texture
+// units: 4 of a record's 7 vector reads), then its first window's two aligned dwords per lane one
+// record ahead (vector loads).  Addresses past the record are clamped to its last
 // dword (the caller's text is only readable up to the last record's end + 16 bytes).
 struct PkHead {
   uint64_t base, end;
@@ -103,11 +104,11 @@ __device__ __forceinline__ void pk_head(const uint64_t* cs_off, const int32_t* o
   h.ql = qlen[ri];
 }
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
-__device__ __forceinline__ void pin(PkHead& h) { asm volatile("" : "+v"(h.base), "+v"(h.end), "+v"(h.off), "+v"(h.ql)); }
 
-__global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const uint64_t* cs_off, const int32_t* offset,
-                                                      const int32_t* qlen, uint32_t n, uint32_t* ops, uint8_t* lits,
-                                                      pw_cs_rec* out) {
+__global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const uint64_t* __restrict__ cs_off,
+                                                      const int32_t* __restrict__ offset,
+                                                      const int32_t* __restrict__ qlen, uint32_t n, uint32_t* ops,
+                                                      uint8_t* lits, pw_cs_rec* out) {
   __shared__ uint32_t win[4][kPackWin / 4 + 4];  // the window's characters, zeros past its end (lanes read 3 dwords on)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: scalar loop)
   LDS uint32_t* w = (LDS uint32_t*)win[wv];
@@ -124,12 +125,10 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
   for (; ri < n; ri += nw) {
     // this record's head (two stages loaded ahead); the next record's first window words and the
     // one after's head are issued before this record is decoded
-    pin(h1);
     pin(d0n);
     pin(d1n);
     const PkHead cur = h1;
     const uint32_t w0 = d0n, w1 = d1n;
-    pin(h2);
     pk_words(text, h2.base, pk_last(h2), lane, d0n, d1n);
     h1 = h2;
     pk_head(cs_off, offset, qlen, ri + 2 * nw < n ? ri + 2 * nw : nl1, h2);
