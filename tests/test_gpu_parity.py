@@ -95,6 +95,16 @@ def test_long_indels_and_runs(built, tmp_path):
     same(["-r", fa, paf])
 
 
+def test_arena_pages(built, tmp_path):
+    """Records of nothing but long '*' runs: every line is kilobytes (fixup_kernel) and chunks reserve
+    up to ~150 KB, far past a page (PW_PAGE_BYTES - kPageSlack): render's arena pages and their
+    per-lane copy-out (the in-place pages go through the LDS page image instead)."""
+    for seed in (21, 22):
+        fa, paf = synth_paf(tmp_path, 0, seed=seed, extra=["--subrun", 1.0, "--psub", 1.0, "--pdel", 0, "--pins", 0,
+                                                           "--err", 0.2, "--rev", 0.5])
+        same(["-r", fa, paf])
+
+
 def test_reverse_only_and_forward_only(built, tmp_path):
     for rev in (0.0, 1.0):
         fa, paf = synth_paf(tmp_path, 0, seed=31, extra=["--rev", rev])
