@@ -176,8 +176,9 @@ def main():
     text_bytes = int(res["text_len"].astype(np.int64).sum())
     if not os.environ.get("PW_BENCH_NOCHECK"):  # (set by attribution sweeps of variants that render wrong)
         assert errs == 0, f"{errs} records reported errors"
-    ctr = dev["work"][:16].cpu().numpy().view(np.uint32)
-    log(f"[rank {rank}] {n_events} events, {text_bytes} text bytes; long lines {int(ctr[1])}")
+    ctr = dev["work"][:64].cpu().numpy().view(np.uint32)
+    log(f"[rank {rank}] {n_events} events, {text_bytes} text bytes; long lines {int(ctr[1])}; "
+        f"ctr[7:16] {ctr[7:16].tolist()}")  # (ctr[7:16]: zeros unless an experiment build counts there)
 
     # HIP events around the K passes as a whole (an event pair per pass would put two timestamp
     # packets, ~5 us of GPU time, between consecutive passes)

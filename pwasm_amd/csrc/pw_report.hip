@@ -1150,7 +1150,7 @@ __device__ __forceinline__ int emit_fast(DLine& L, const LDS uint8_t* qw, int ql
   const bool isS = typ == PW_OP_SUB, isI = typ == PW_OP_INS, isD = typ == PW_OP_DEL;
   const int rloc = event_rloc(Lq, rev, typ, in.qp, n);
   const int aap0 = rloc / 3;
-  const int rt = 3 * (aap0 - 1);  // r_trloc (rloc >= 8 here)
+  const int rt = 3 * (aap0 - 1);  // r_trloc (rloc >= 4 here)
   rel = rloc - rt;
   const uint64_t l64 = (uint64_t)l1 << 32 | l0;
   const LDS uint8_t* c64 = tab->codon64;
@@ -2584,16 +2584,17 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       k.pos = 0;
       int rel = 0;
       // the fast instantiation when every active lane's reads are in its registers / window: A/C/G/T,
-      // at least 8 query bytes before the event (the window starts at or before rloc - 8, so it
-      // covers [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8 bases whose modseq tail
-      // image starts inside the window, deletions of <= 12 (the largest read, the tail image at
-      // r_trloc + deletion, ends by rloc + 25)
+      // rloc >= 4 (r_trloc = 3 * (rloc / 3 - 1) >= 0 with rloc - r_trloc in 3..5, and the RCTX
+      // window rloc - 4 unclipped; the window starts at max(rloc - 8, 0) rounded down to 16, so it
+      // covers every query byte in [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8
+      // bases, deletions of <= 12 (the largest read, the tail image at r_trloc + deletion, ends by
+      // rloc + 25).  (An insertion's modseq tail image starts at r_trloc - n, up to 8 bytes before
+      // the lane's window: those bytes are LDS of the wave's line buffers, read and masked off.)
       const int rlc = event_rloc(r.L, rev, typ, hc.qp, n);
       const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
       // (and numbers below 10^8: emit_fast's decimal conversion)
-      const bool fast = r.acgt && rlc >= 8 && qlo <= rlc - 8 && r.L < 100000000 && hc.tloc < 99999999 &&
-                        (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L)
-                                          : (typ == PW_OP_INS ? (n <= 8 && rt - qlo >= n) : n <= 12));
+      const bool fast = r.acgt && rlc >= 4 && r.L >= 9 && r.L < 100000000 && hc.tloc < 99999999 &&
+                        (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L) : n <= (typ == PW_OP_INS ? 8 : 12));
       int merr;
       if (__ballot(!fast) == 0) {
         DLine dl;

@@ -11,6 +11,8 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   fx_bigwin  fixup_kernel stages 128 query bytes and 64 literal bytes per line
   tc_nowalk  tctx_kernel skips the op walk (timing only)
   rw2      render_kernel in 2-wave workgroups (6 per CU)
+  idx_scalar index_kernel record heads through scalar loads
+  why      render counts its non-fast lanes by reason into Work.ctr[8..15] (ctr[7]: general waves)
   tw2      tctx_kernel in 2-wave workgroups (8 per CU)
   ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
 Usage: python tools/exp_report_variants.py [names...]"""
@@ -76,6 +78,22 @@ PATCHES = {
              "  const uint64_t gstride = (uint64_t)gridDim.x * kTctxWaves;\n  uint64_t gi = (uint64_t)blockIdx.x * kTctxWaves + wv;"),
             ("    uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;\n    if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;\n    hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);",
              "    uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kTctxWaves + 1;\n    if (tg > (uint64_t)ncu * 8u) tg = (uint64_t)ncu * 8u;\n    hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kTctxWaves), 0, st, *args, W);")],
+    # index_kernel: the record heads (descriptor, query location, next event slot) as scalar loads
+    # instead of per-lane vector loads pinned in VGPRs
+    "idx_scalar": [('  asm volatile("" : "+v"(p.qb), "+v"(p.ev_next), "+v"(p.L), "+v"(p.w0), "+v"(p.w1));',
+                    '  asm volatile("" : "+v"(p.w0), "+v"(p.w1));'),
+                   ("    rec_pre_ready(A, cur, lane);\n    pin(dn.a);\n    pin(dn.b);", "    rec_pre_ready(A, cur, lane);"),
+                   ("      rec_pre_ready(A, nxt, lane);\n      pin(dnn.a);\n      pin(dnn.b);", "      rec_pre_ready(A, nxt, lane);")],
+    # render: why lanes miss the fast path — per reason an atomic into Work.ctr[8..14] (bench logs
+    # ctr[8:16]; timing meaningless)
+    "why": [("      int merr;\n      if (__ballot(!fast) == 0) {",
+             "      if (!fast) {\n        const int why = !r.acgt ? 8 : (rlc < 8 ? 9 : ((r.L >= 100000000 || hc.tloc >= 99999999) ? 10 : "
+             "(typ == PW_OP_SUB ? (n > 4 ? 11 : 12) : (typ == PW_OP_INS ? (n > 8 ? 13 : 14) : 15))));\n"
+             "        atomicAdd(&W.ctr[why], 1u);\n      }\n      if (__ballot(!fast) != 0 && lane == 0) atomicAdd(&W.ctr[7], 1u);\n"
+             "      int merr;\n      if (__ballot(!fast) == 0) {")],
+    # fixup_kernel's two halves timed apart (results wrong: timing only)
+    "fx_nofin": [("    if (ai < A.n_alns) finalize_record(A, W, ai);\n    return;", "    return;")],
+    "fx_nofix": [("  if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten", "  return;")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
