@@ -2654,6 +2654,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       pg.pad = 0;
       A.pages[c] = pg;
       W.lmask[c] = lm;
+      if (lm) atomicAdd(&W.ctr[1], (uint32_t)__popcll(lm));  // (no return value: no wait)
     }
     const uint64_t g0 = P + my_off;
     if (act && (fn_cur & (3u << 26))) {  // first / last line of a record
@@ -2945,6 +2946,9 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     if (ai < A.n_alns) finalize_record(A, W, ai);
     return;
   }
+  // no long lines (the common case): the workgroup ends here — before the table staging and the
+  // scan of every chunk's mask (25 us of this launch on cfg2 when it ran them for nothing)
+  if (W.ctr[1] == 0) return;
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, 256);
   __syncthreads();

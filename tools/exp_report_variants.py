@@ -94,6 +94,11 @@ PATCHES = {
     # fixup_kernel's two halves timed apart (results wrong: timing only)
     "fx_nofin": [("    if (ai < A.n_alns) finalize_record(A, W, ai);\n    return;", "    return;")],
     "fx_nofix": [("  if (W.ctr[2]) return;  // overflow: the results report it, nothing is rewritten", "  return;")],
+    # finalize as its own launch before the (then long-line only) fixup launch
+    "fx_sep": [("    if (ai < A.n_alns) finalize_record(A, W, ai);\n    return;", "    return;"),
+               ("    hipLaunchKernelGGL(pw::fixup_kernel, dim3(",
+                "    hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);\n"
+                "    hipLaunchKernelGGL(pw::fixup_kernel, dim3(")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
