@@ -512,9 +512,11 @@ __device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, 
   }
 }
 
-// "%d" of a non-negative int, digit by digit (numbers >= 10^8: rare, out of line)
+// "%d" of a non-negative int, digit by digit (numbers >= 10^8, abbreviation lengths: rare).  Inline:
+// an out-of-line call taking the sink by reference put the sink in scratch, and a kernel with a
+// scratch segment paid ~25 us per launch (fixup_kernel: 31 us for workgroups that return at once)
 template <class S>
-__device__ __noinline__ void wr_dig(S& k, uint32_t v) {
+__device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
   for (uint32_t P = 1000000000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
   k.put((uint8_t)('0' + v % 10u));
 }
@@ -2375,11 +2377,12 @@ struct RenderWave {
 };
 
 // the record owning event slot s: the last one whose first slot is <= s (error path only)
-__device__ __noinline__ uint32_t rec_of_slot(const pw_report_args& A, uint64_t s) {
-  uint32_t lo = 0, hi = A.n_alns - 1;
+// (arguments by value: a reference to the kernel arguments would put a copy of them in scratch)
+__device__ __noinline__ uint32_t rec_of_slot(const pw_aln_desc* desc, uint32_t n_alns, uint64_t s) {
+  uint32_t lo = 0, hi = n_alns - 1;
   while (lo < hi) {
     const uint32_t mid = lo + (hi - lo + 1) / 2;
-    if (A.desc[mid].ev_begin <= s) lo = mid;
+    if (desc[mid].ev_begin <= s) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -2607,7 +2610,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         linelen = k.pos;
       }
       if (merr >= 0) {  // modseq error: first failing event of the record in output order
-        const uint32_t ai = rec_of_slot(A, s);
+        const uint32_t ai = rec_of_slot(A.desc, A.n_alns, s);
         const pw_aln_desc d = A.desc[ai];
         const uint64_t evb = d.ev_begin;
         const uint64_t ev_next = (ai + 1 < A.n_alns) ? A.desc[ai + 1].ev_begin : A.n_ev_slots;

@@ -99,6 +99,13 @@ PATCHES = {
                ("    hipLaunchKernelGGL(pw::fixup_kernel, dim3(",
                 "    hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);\n"
                 "    hipLaunchKernelGGL(pw::fixup_kernel, dim3(")],
+    "fx_lds": [("  __shared__ __attribute__((aligned(16))) FixLane fl[256];", "  __shared__ __attribute__((aligned(16))) FixLane fl[4];"),
+               ("  LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x];", "  LDS FixLane* me = (LDS FixLane*)&fl[threadIdx.x & 3];")],
+    "fx_sep2": [("    if (ai < A.n_alns) finalize_record(A, W, ai);\n    return;", "    return;"),
+                ("    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,",
+                 "    hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);\n"
+                 "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0,"),
+                ("  const uint32_t fix_wg = gridDim.x - (A.n_alns + 255) / 256;", "  const uint32_t fix_wg = gridDim.x;")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
