@@ -513,8 +513,8 @@ __device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, 
 }
 
 // "%d" of a non-negative int, digit by digit (numbers >= 10^8, abbreviation lengths: rare).  Inline:
-// an out-of-line call taking the sink by reference put the sink in scratch, and a kernel with a
-// scratch segment paid ~25 us per launch (fixup_kernel: 31 us for workgroups that return at once)
+// an out-of-line call taking the sink by reference put the sink in a scratch segment (no report
+// kernel has one now)
 template <class S>
 __device__ __forceinline__ void wr_dig(S& k, uint32_t v) {
   for (uint32_t P = 1000000000u; P >= 10u; P /= 10u) k.put_if(v >= P, (uint8_t)('0' + (v / P) % 10u));
@@ -2949,8 +2949,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     if (ai < A.n_alns) finalize_record(A, W, ai);
     return;
   }
-  // no long lines (the common case): the workgroup ends here — before the table staging and the
-  // scan of every chunk's mask (25 us of this launch on cfg2 when it ran them for nothing)
+  // no long lines (inputs without S runs of many codons / long indels): the workgroup ends here
   if (W.ctr[1] == 0) return;
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, 256);

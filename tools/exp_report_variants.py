@@ -106,6 +106,11 @@ PATCHES = {
                  "    hipLaunchKernelGGL(pw::finalize_kernel, dim3((uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0, st, *args, W);\n"
                  "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu), dim3(256), 0,"),
                 ("  const uint32_t fix_wg = gridDim.x - (A.n_alns + 255) / 256;", "  const uint32_t fix_wg = gridDim.x;")],
+    # fixup_kernel timed on the long lines render's fast predicate accepts / rejects only
+    "fx_onlyfast": [("    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);",
+                     "    const bool fast_ = r.acgt && rl >= 4 && r.L >= 9 && r.L < 100000000 && h.tloc < 99999999 && (typ == PW_OP_SUB ? (ne <= 4 && 3 * (rl / 3 - 1) + 9 <= r.L) : ne <= (typ == PW_OP_INS ? 8 : 12));\n    if (!fast_) continue;\n    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);")],
+    "fx_onlyslow": [("    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);",
+                     "    const bool fast_ = r.acgt && rl >= 4 && r.L >= 9 && r.L < 100000000 && h.tloc < 99999999 && (typ == PW_OP_SUB ? (ne <= 4 && 3 * (rl / 3 - 1) + 9 <= r.L) : ne <= (typ == PW_OP_INS ? 8 : 12));\n    if (fast_) continue;\n    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
