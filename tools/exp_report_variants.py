@@ -111,6 +111,26 @@ PATCHES = {
                      "    const bool fast_ = r.acgt && rl >= 4 && r.L >= 9 && r.L < 100000000 && h.tloc < 99999999 && (typ == PW_OP_SUB ? (ne <= 4 && 3 * (rl / 3 - 1) + 9 <= r.L) : ne <= (typ == PW_OP_INS ? 8 : 12));\n    if (!fast_) continue;\n    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);")],
     "fx_onlyslow": [("    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);",
                      "    const bool fast_ = r.acgt && rl >= 4 && r.L >= 9 && r.L < 100000000 && h.tloc < 99999999 && (typ == PW_OP_SUB ? (ne <= 4 && 3 * (rl / 3 - 1) + 9 <= r.L) : ne <= (typ == PW_OP_INS ? 8 : 12));\n    if (fast_) continue;\n    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);")],
+    # fixup_kernel's long-line chain timed in stages (s_memtime after full waits): ctr[7] whole line,
+    # [8] mask -> Fixup -> Hot, [9] windows staged, [10] emit_event, [11] lines on one lane (maxima)
+    "fx_time": [("    const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];",
+                 "    __builtin_amdgcn_s_waitcnt(0);\n    const uint64_t TA = clock64();\n"
+                 "    const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];"),
+                ("    const int rl = event_rloc(r.L, rev, typ, h.qp, ne);\n    int x0 = rl - 8;\n    if (x0 < 0) x0 = 0;\n    const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)\n    const GV4* a0",
+                 "    __builtin_amdgcn_s_waitcnt(0);\n    const uint64_t TB = clock64();\n"
+                 "    const int rl = event_rloc(r.L, rev, typ, h.qp, ne);\n    int x0 = rl - 8;\n    if (x0 < 0) x0 = 0;\n    const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)\n    const GV4* a0"),
+                ("    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);",
+                 "    __builtin_amdgcn_s_waitcnt(0);\n    const uint64_t TC = clock64();\n"
+                 "    GlobalSink g;\n    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);"),
+                ("    emit_event(g, r, in, skip, rel);\n  }",
+                 "    emit_event(g, r, in, skip, rel);\n    __builtin_amdgcn_s_waitcnt(0);\n    const uint64_t TD = clock64();\n"
+                 "    atomicMax(&W.ctr[7], (uint32_t)(TD - TA));\n    atomicMax(&W.ctr[8], (uint32_t)(TB - TA));\n"
+                 "    atomicMax(&W.ctr[9], (uint32_t)(TC - TB));\n    atomicMax(&W.ctr[10], (uint32_t)(TD - TC));\n"
+                 "    atomicMax(&W.ctr[11], (T + 63u - (uint32_t)lane) / 64u);\n  }")],
+    # fixup_kernel launched twice per pass (idempotent): is the second, warm-cache launch faster?
+    "fx_twice": [("    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);",
+                  "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);\n"
+                  "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
