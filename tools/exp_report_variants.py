@@ -131,11 +131,25 @@ PATCHES = {
     "fx_twice": [("    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);",
                   "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);\n"
                   "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);")],
+    # the same source under other machine schedulers (FLAGS below)
+    "sch_ilp": [],
+    "sch_none": [],
+    "sch_iterilp": [],
+    "sch_minreg": [],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
                    "    for (int q = 0; q < kFxQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];"),
                   ("    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kQWin;", "    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kFxQ;")],
+}
+
+
+# scheduler flags per variant (default: the Makefile's max-memory-clause)
+FLAGS = {
+    "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "sch_none": [],
+    "sch_iterilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "sch_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
 }
 
 
@@ -152,7 +166,7 @@ def build(name):
     o = os.path.join(d, "pw_report.o")
     inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
-                    "-Wno-unused-function", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause", *inc, "-c", src,
+                    "-Wno-unused-function", *FLAGS.get(name, ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]), *inc, "-c", src,
                     "-o", o], check=True)
     bdir = os.path.join(REPO, "pwasm_amd/build")
     objs = [os.path.join(bdir, f) for f in sorted(os.listdir(bdir)) if f.endswith(".o") and f != "pw_report.o"]
