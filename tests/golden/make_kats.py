@@ -125,6 +125,49 @@ K6_MSA = (">qa\nAACC---GGTTAA-CC\n"
           ">t5:100-113+\nAACC---GGTTAAcCC\n")
 
 
+# kat7_near_start: events at rloc 4..7 (render's fast path since round 4: r_trloc = 3*(aapos-2)
+# = 0 or 3, the codon window from the query start, and insertions whose modseq tail starts before
+# rloc - 8), forward and reverse.  Derivation (Q = CDS, 0-based):
+#  asm7  ':5-gc:25'  I at q 5: tseq = Q[0:5]+gc+Q[5:]; tctx = tseq[0:12] (:120-128); aa = Q[3:6]
+#        AAA K, aapos 2 (:893-898); rctx Q[1:10] (:721-733); r_trloc 0, modseq = Q with GC at 5,
+#        no stop in ATG AAG CAC CCG GGT TTA AAC CCG GGT TTT -> frame shift aa4 KPGF / maa4 KHPG.
+#  asm8  ':6+cc:22'  D at q 6: tctx = tseq[1:11] (evt_len 0); aa = Q[6:9] CCC P, aapos 3; rctx
+#        Q[2:11]; r_trloc 3, modseq = Q[3:] cut at 3 len 2 = AAA CGG GTT TAA -> stop at i 9:
+#        AA 1+(9+3)/3 = 5.
+#  asm9  ':4*ga*ta:24' merged S (:556-560) AA->GT at q 4, evtlen stays 1 so tctx = tseq[0:10];
+#        aamods {1}: AAA K -> AGT S, AA 1+4/3 = 2.
+#  asm10 ':7-ttt:23' I at q 7: tctx tseq[2:15]; aa Q[6:9] P, aapos 3; rctx Q[3:12]; r_trloc 3,
+#        modseq = Q[3:] with TTT at 4 -> AAA CTT TCC GGG TTT AAA CCC GGG TTT TAA: stop at i 27, AA 11.
+#  asm11 '-' ':25-ga:5' on RC = revcomp(Q): I at aligned q 25, rloc = 30-25 = 5 (:597), evtbases
+#        revcomp(ga) = TC; tctx = tseq[20:31] (tc_end clipped to |tseq|-1) = CGGGTgaTTCA, revcomp
+#        TGAAtcACCCG; tloc = 32-25 = 7 (:633); modseq = Q with TC at 5 -> frame shift KPGF / NHPG.
+#  asm12 '-' ':21+ggg:6': D of RC[21:24] = GGG -> evtbases CCC, rloc = 30-21-3 = 6 (:615);
+#        tctx tseq[16:26] = AACCCTTTCA, revcomp TGAAAGGGTT; tloc 27-21 = 6; modseq = Q[3:] cut at
+#        3 len 3 = AAA GGG TTT AAA CCC GGG TTT TAA: stop at i 21, AA 9.
+K7 = (paf("cds", 30, 0, 30, "+", "asm7", 100, 10, 42, 30, 32, 60, "NM:i:2", "AS:i:50", "cg:Z:5M2D25M", "cs:Z::5-gc:25")
+      + paf("cds", 30, 0, 30, "+", "asm8", 100, 20, 48, 28, 30, 60, "NM:i:2", "AS:i:50", "cg:Z:6M2I22M", "cs:Z::6+cc:22")
+      + paf("cds", 30, 0, 30, "+", "asm9", 100, 30, 60, 28, 30, 60, "NM:i:2", "AS:i:50", "cg:Z:30M",
+            "cs:Z::4*ga*ta:24")
+      + paf("cds", 30, 0, 30, "+", "asm10", 100, 0, 33, 30, 33, 60, "NM:i:3", "AS:i:50", "cg:Z:7M3D23M",
+            "cs:Z::7-ttt:23")
+      + paf("cds", 30, 0, 30, "-", "asm11", 100, 5, 37, 30, 32, 60, "NM:i:2", "AS:i:50", "cg:Z:25M2D5M",
+            "cs:Z::25-ga:5")
+      + paf("cds", 30, 0, 30, "-", "asm12", 100, 40, 67, 27, 30, 60, "NM:i:3", "AS:i:40", "cg:Z:21M3I6M",
+            "cs:Z::21+ggg:6"))
+K7_OUT = (">asm7:10-42+ coverage:100.00 score=50 edit_distance=2\n"
+          "I\t6\t2(K)\t:GC\t6\tATGAAgcACCCG\tTGAAACCCG\t[unknown]\tframe shift KPGF+:KHPG+\n"
+          ">asm8:20-48+ coverage:100.00 score=50 edit_distance=2\n"
+          "D\t7\t3(P)\tCC:\t7\tTGAAACGGGT\tGAAACCCGG\t[unknown]\tpremature stop at AA5\n"
+          ">asm9:30-60+ coverage:100.00 score=50 edit_distance=2\n"
+          "S\t5\t2(K)\tAA:GT\t5\tATGAgtCCCG\tATGAAACCC\t[unknown]\tAA2|K:S\n"
+          ">asm10:0-33+ coverage:100.00 score=50 edit_distance=3\n"
+          "I\t8\t3(P)\t:TTT\t8\tGAAACtttCCGGG\tAAACCCGGG\t[unknown]\tpremature stop at AA11\n"
+          ">asm11:5-37- coverage:100.00 score=50 edit_distance=2\n"
+          "I\t6\t2(K)\t:TC\t8\tTGAAtcACCCG\tTGAAACCCG\t[unknown]\tframe shift KPGF+:NHPG+\n"
+          ">asm12:40-67- coverage:100.00 score=40 edit_distance=3\n"
+          "D\t7\t3(P)\tCCC:\t7\tTGAAAGGGTT\tGAAACCCGG\t[unknown]\tpremature stop at AA9\n")
+
+
 def line(s):
     return s.rstrip("\n")
 
@@ -135,6 +178,7 @@ CASES = {
     "kat2_reverse": (FA1, K2, ["-r", "q.fa", "in.paf"], 0, K2_OUT, ""),
     "kat3_status": (FA3, K3, ["-r", "q.fa", "in.paf"], 0, K3_OUT, K3_ERR),
     "kat4_fullgenome": (FA1, K1, ["-F", "-r", "q.fa", "in.paf"], 0, K4_OUT, ""),
+    "kat7_near_start": (FA1, K7, ["-r", "q.fa", "in.paf"], 0, K7_OUT, ""),
     "kat6_msa_w": (FA6, K6, ["-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", ""),
     "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
                        K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
