@@ -167,6 +167,37 @@ K7_OUT = (">asm7:10-42+ coverage:100.00 score=50 edit_distance=2\n"
           ">asm12:40-67- coverage:100.00 score=40 edit_distance=3\n"
           "D\t7\t3(P)\tCCC:\t7\tTGAAAGGGTT\tGAAACCCGG\t[unknown]\tpremature stop at AA9\n")
 
+# kat8_tctx_walk: four events within 5 target bases of each other, so every target context crosses
+# another event (tctx_kernel's op walk, not the query-copy fast form).  asm20 ':10*cg:1-tt:3+aa:2*gc:10'
+# tseq = Q[0:10] c G tt TTT AC g Q[20:] (30): S q10 tloc 10, I q12 tloc 12, D q15 tloc 17 (tpos after
+# ':3'), S q19 tloc 19 (the D in between: no merge, :556).  tctx (:120-128) = tseq[5:16], [7:19],
+# [12:22] (D: evt_len 0), [14:25].  Impacts (:801-883): S q10 r_trloc 6, codon 1 GGG G -> GCG A;
+# I q12 r_trloc 9, modseq GGG TT TTTAAA.. -> FKPG / FLNP, no stop; D q15 r_trloc 12, TTT + Q[17:] ->
+# KPGF / TRVL; S q19 r_trloc 15, CCC P -> CGC R.
+K8 = paf("cds", 30, 0, 30, "+", "asm20", 100, 50, 80, 24, 32, 60, "NM:i:6", "AS:i:30", "cg:Z:12M2D3M2I13M",
+         "cs:Z::10*cg:1-tt:3+aa:2*gc:10")
+K8_OUT = (">asm20:50-80+ coverage:100.00 score=30 edit_distance=6\n"
+          "S\t11\t4(G)\tG:C\t11\tACCCGcGttTT\tCCCGGGTTT\t[unknown]\tAA4|G:A\n"
+          "I\t13\t5(F)\t:TT\t13\tCCGcGttTTTAC\tCGGGTTTAA\t[unknown]\tframe shift FKPG+:FLNP+\n"
+          "D\t16\t6(K)\tAA:\t18\tttTTTACgCG\tGTTTAAACC\t[unknown]\tframe shift KPGF+:TRVL+\n"
+          "S\t20\t7(P)\tC:G\t20\tTTTACgCGGGT\tAAACCCGGG\t[unknown]\tAA7|P:R\n")
+
+# kat9_tctx_walk_reverse: the same pattern on the '-' strand, decoded on RC = revcomp(Q)
+# (:361-363): asm21 ':8*tc:2-gg:3+ta:3*ac:10', tseq = RC[0:8] t GG gg GTT AAC a RC[20:] (30).
+# Aligned events S q8 t8, I q11 t11, D q14 t16, S q19 t19; tctx = tseq[3:14], [6:18], [11:21],
+# [14:25], each reverse-complemented (:631), tloc = 30 - tloc (:633); S flipped after the contexts
+# (:634-640): rloc 30-8-1 = 21 and 30-19-1 = 10; I rloc 30-11 = 19 (:597), D 30-14-2 = 14
+# (:615); tdiffs reversed (:643).  Impacts on Q: S q10 G->T (GGG G -> GTG V, AA4); D q14 TA,
+# r_trloc 9 -> FKPG / LTRV; I q19 CC, r_trloc 15: aa4 ends in TAA = '.', modseq has no stop ->
+# frame shift PGF. / PPGF; S q21 G->A (GGG G -> AGG R, AA8).
+K9 = paf("cds", 30, 0, 30, "-", "asm21", 100, 60, 90, 24, 32, 60, "NM:i:6", "AS:i:30", "cg:Z:11M2D3M2I14M",
+         "cs:Z::8*tc:2-gg:3+ta:3*ac:10")
+K9_OUT = (">asm21:60-90- coverage:100.00 score=30 edit_distance=6\n"
+          "S\t11\t4(G)\tG:T\t12\tACCCGtGTTAA\tCCCGGGTTT\t[unknown]\tAA4|G:V\n"
+          "D\t15\t5(F)\tTA:\t15\tGtGTTAACcc\tGGTTTAAAC\t[unknown]\tframe shift FKPG+:LTRV+\n"
+          "I\t20\t7(P)\t:CC\t20\tTTAACccCCaGG\tAAACCCGGG\t[unknown]\tframe shift PGF.+:PPGF+\n"
+          "S\t22\t8(G)\tG:A\t23\tCccCCaGGTTT\tACCCGGGTT\t[unknown]\tAA8|G:R\n")
+
 
 def line(s):
     return s.rstrip("\n")
@@ -179,6 +210,8 @@ CASES = {
     "kat3_status": (FA3, K3, ["-r", "q.fa", "in.paf"], 0, K3_OUT, K3_ERR),
     "kat4_fullgenome": (FA1, K1, ["-F", "-r", "q.fa", "in.paf"], 0, K4_OUT, ""),
     "kat7_near_start": (FA1, K7, ["-r", "q.fa", "in.paf"], 0, K7_OUT, ""),
+    "kat8_tctx_walk": (FA1, K8, ["-r", "q.fa", "in.paf"], 0, K8_OUT, ""),
+    "kat9_tctx_walk_reverse": (FA1, K9, ["-r", "q.fa", "in.paf"], 0, K9_OUT, ""),
     "kat6_msa_w": (FA6, K6, ["-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", ""),
     "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
                        K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
