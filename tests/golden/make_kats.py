@@ -198,6 +198,27 @@ K9_OUT = (">asm21:60-90- coverage:100.00 score=30 edit_distance=6\n"
           "I\t20\t7(P)\t:CC\t20\tTTAACccCCaGG\tAAACCCGGG\t[unknown]\tframe shift PGF.+:PPGF+\n"
           "S\t22\t8(G)\tG:A\t23\tCccCCaGGTTT\tACCCGGGTT\t[unknown]\tAA8|G:R\n")
 
+# kat10_general: events outside render's fast path (emit_event's general instantiation).
+#  asm30 ':3*ta*ga*ga*tc*ac*ac:21' an S run of 6 (merged, :556-560; evtlen stays 1 so tctx =
+#        tseq[0:9]); rctx clipped at the query start (ctxstart -1 -> 0, :724); aamods {1, 2}:
+#        AAA K -> TGG W, CCC P -> TAA '.' (:826-837): "AA2|K:W, AA3|P:.|premature stop at AA3".
+#  asm31 ':9-acgtacgtac:21' a 10-base insertion: tctx tseq[4:24] (20 <= 22, not abbreviated);
+#        r_trloc 6, modseq CCC ACG TAC GTA CGG GTT TAA -> stop at i 18, AA 1+(18+6)/3 = 9.
+#  asm32 ':10+ggtttaaacccgg:7' a 13-base deletion: evtbases "[13]" (> MAX_EVLEN, :936-941),
+#        tctx tseq[5:15]; r_trloc 6, modseq CCCG + GTTTTAA: GGT G, TTT F, no stop -> GF / GF.
+K10 = (paf("cds", 30, 0, 30, "+", "asm30", 100, 0, 30, 24, 30, 60, "NM:i:6", "AS:i:20", "cg:Z:30M",
+           "cs:Z::3*ta*ga*ga*tc*ac*ac:21")
+       + paf("cds", 30, 0, 30, "+", "asm31", 100, 10, 50, 30, 40, 60, "NM:i:10", "AS:i:20", "cg:Z:9M10D21M",
+             "cs:Z::9-acgtacgtac:21")
+       + paf("cds", 30, 0, 30, "+", "asm32", 100, 20, 37, 17, 30, 60, "NM:i:13", "AS:i:10", "cg:Z:10M13I7M",
+             "cs:Z::10+ggtttaaacccgg:7"))
+K10_OUT = (">asm30:0-30+ coverage:100.00 score=20 edit_distance=6\n"
+           "S\t4\t2(K)\tAAACCC:TGGTAA\t4\tATGtggtaa\tATGAAACCC\t[unknown]\tAA2|K:W, AA3|P:.|premature stop at AA3\n"
+           ">asm31:10-50+ coverage:100.00 score=20 edit_distance=10\n"
+           "I\t10\t4(G)\t:ACGTACGTAC\t10\tAACCCacgtacgtacGGGTT\tACCCGGGTT\t[unknown]\tpremature stop at AA9\n"
+           ">asm32:20-37+ coverage:100.00 score=10 edit_distance=13\n"
+           "D\t11\t4(G)\t[13]:\t11\tACCCGGTTTT\tCCCGGGTTT\t[unknown]\tframe shift GF+:GF+\n")
+
 
 def line(s):
     return s.rstrip("\n")
@@ -212,6 +233,7 @@ CASES = {
     "kat7_near_start": (FA1, K7, ["-r", "q.fa", "in.paf"], 0, K7_OUT, ""),
     "kat8_tctx_walk": (FA1, K8, ["-r", "q.fa", "in.paf"], 0, K8_OUT, ""),
     "kat9_tctx_walk_reverse": (FA1, K9, ["-r", "q.fa", "in.paf"], 0, K9_OUT, ""),
+    "kat10_general": (FA1, K10, ["-r", "q.fa", "in.paf"], 0, K10_OUT, ""),
     "kat6_msa_w": (FA6, K6, ["-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", ""),
     "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
                        K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
