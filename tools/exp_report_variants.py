@@ -131,6 +131,9 @@ PATCHES = {
     "fx_twice": [("    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);",
                   "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);\n"
                   "    hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,\n                       st, *args, W);")],
+    # no next-stop table build (timing only: index without the side-stream kernel beside it)
+    "ns_skip": [("  const uint32_t grid = nq < 4096u ? nq : 4096u;\n  hipLaunchKernelGGL(pw::stop_table_kernel,",
+                 "  const uint32_t grid = nq < 4096u ? nq : 4096u;\n  if (grid) return PW_OK;\n  hipLaunchKernelGGL(pw::stop_table_kernel,")],
     # the same source under other machine schedulers (FLAGS below)
     "sch_ilp": [],
     "sch_none": [],
