@@ -134,6 +134,11 @@ PATCHES = {
     # no next-stop table build (timing only: index without the side-stream kernel beside it)
     "ns_skip": [("  const uint32_t grid = nq < 4096u ? nq : 4096u;\n  hipLaunchKernelGGL(pw::stop_table_kernel,",
                  "  const uint32_t grid = nq < 4096u ? nq : 4096u;\n  if (grid) return PW_OK;\n  hipLaunchKernelGGL(pw::stop_table_kernel,")],
+    # index_kernel at 6 waves/SIMD (<= 80 VGPRs), grid two rounds of that
+    "idx6": [("constexpr int kIndexOcc = 5;", "constexpr int kIndexOcc = 6;"),
+             ("  if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;",
+              "  if (ig > (uint64_t)ncu * 12u || planned) ig = (uint64_t)ncu * 12u;")],
+    "idx6g10": [("constexpr int kIndexOcc = 5;", "constexpr int kIndexOcc = 6;")],
     # the same source under other machine schedulers (FLAGS below)
     "sch_ilp": [],
     "sch_none": [],
