@@ -139,6 +139,8 @@ PATCHES = {
              ("  if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;",
               "  if (ig > (uint64_t)ncu * 12u || planned) ig = (uint64_t)ncu * 12u;")],
     "idx6g10": [("constexpr int kIndexOcc = 5;", "constexpr int kIndexOcc = 6;")],
+    # no counter memset before index (timing only: cfg2 uses no counter that carries over harmfully)
+    "nomemset": [("  if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;", "")],
     # the same source under other machine schedulers (FLAGS below)
     "sch_ilp": [],
     "sch_none": [],
