@@ -68,7 +68,7 @@ constexpr int kSegOps = 128;    // index_kernel: ops per segment (2 per lane)
 constexpr int kOpHalo = 16;     // index_kernel: op words staged before / after a segment
 constexpr int kQWin = 48;       // render_kernel: forward-query window per lane (bytes)
 constexpr int kQStride = 56;    // ... its LDS stride (14 dwords: same-offset dword reads at most 2-way)
-constexpr int kLine = 92;       // render_kernel: report lines up to this long are built in LDS (99.94 % at cfg2)
+constexpr int kLine = 108;      // render_kernel: report lines up to this long are built in LDS (all but ~1 in 10^4 at cfg2)
 constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
 static_assert(kLine + kLSlack <= 148, "line buffer stride");
@@ -2713,11 +2713,11 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       const uint64_t below = ne & ((1ull << lane) - 1ull);
       const int prev = below ? 63 - __builtin_clzll(below) : lane;
       const uint32_t ptail = (uint32_t)__shfl((int)tail, prev, kWave) & (uint32_t)((1ull << (8 * sh)) - 1ull);
-      uint32_t Lw[24];
+      uint32_t Lw[28];
       {
         const LDS v4a4* lp4 = reinterpret_cast<const LDS v4a4*>(my_line);  // (4-byte aligned: 148-byte stride)
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
+        for (int q = 0; q < 7; q++) {
           const v4u v = lp4[q];
           Lw[4 * q] = v.x, Lw[4 * q + 1] = v.y, Lw[4 * q + 2] = v.z, Lw[4 * q + 3] = v.w;
         }
@@ -2730,7 +2730,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int k = 4 * j + i;
-          const uint32_t cur = k < 24 ? Lw[k] : 0u, prv = k == 0 ? 0u : Lw[k - 1];
+          const uint32_t cur = k < 28 ? Lw[k] : 0u, prv = k == 0 ? 0u : Lw[k - 1];
           v[i] = __builtin_amdgcn_perm(cur, prv, sel);
         }
         if (j == 0) v[0] |= ptail;
@@ -2743,7 +2743,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         wave_sync();
         LDS uint8_t* img = w->line;
 #pragma unroll
-        for (int j = 5; j >= 0; j--)
+        for (int j = 6; j >= 0; j--)
           if (j <= jmax) *reinterpret_cast<LDS v4a4*>(img + a0 + 16u * (uint32_t)j) = group(j);
         wave_sync();
 #pragma unroll
@@ -2753,7 +2753,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         }
       } else {  // an arena page: every lane stores its own groups
 #pragma unroll
-        for (int j = 5; j >= 0; j--)
+        for (int j = 6; j >= 0; j--)
           __builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, 0);
       }
     }

@@ -15,6 +15,8 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   why      render counts its non-fast lanes by reason into Work.ctr[8..15] (ctr[7]: general waves)
   tw2      tctx_kernel in 2-wave workgroups (8 per CU)
   ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
+  kl108    lines up to 108 bytes built in render (kLine 92 -> 108: the whole 40-byte slack of the
+           148-byte stride; copy-out over 28 dwords / 7 groups), so fewer lines go to fixup_kernel
 Usage: python tools/exp_report_variants.py [names...]"""
 import os
 import subprocess
@@ -151,6 +153,15 @@ PATCHES = {
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
                    "    for (int q = 0; q < kFxQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];"),
                   ("    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kQWin;", "    r.qw = me->qw;\n    r.qlo = x0a;\n    r.qn = kFxQ;")],
+    "kl108": [("constexpr int kLine = 92; ", "constexpr int kLine = 108;"),
+              ("      uint32_t Lw[24];", "      uint32_t Lw[28];"),
+              ("        for (int q = 0; q < 6; q++) {\n          const v4u v = lp4[q];",
+               "        for (int q = 0; q < 7; q++) {\n          const v4u v = lp4[q];"),
+              ("          const uint32_t cur = k < 24 ? Lw[k] : 0u,", "          const uint32_t cur = k < 28 ? Lw[k] : 0u,"),
+              ("        for (int j = 5; j >= 0; j--)\n          if (j <= jmax) *reinterpret_cast<LDS v4a4*>",
+               "        for (int j = 6; j >= 0; j--)\n          if (j <= jmax) *reinterpret_cast<LDS v4a4*>"),
+              ("        for (int j = 5; j >= 0; j--)\n          __builtin_amdgcn_raw_buffer_store_b128(group(j)",
+               "        for (int j = 6; j >= 0; j--)\n          __builtin_amdgcn_raw_buffer_store_b128(group(j)")],
 }
 
 
