@@ -148,6 +148,14 @@ PATCHES = {
     "sch_none": [],
     "sch_iterilp": [],
     "sch_minreg": [],
+    # fixup_kernel: the Hot / Cold / tx records by the line's slot (the lane-mask position) in
+    # parallel with its Fixup entry, whose `s` is the same slot (one dependent load less per line)
+    "fx_par": [("    const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];\n    const Hot h = W.hot[f.s];",
+                "    const uint64_t sl = (c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm);  // (= f.s)\n"
+                "    const uint64_t fdst = W.fix[sl].dst;\n    const Hot h = W.hot[sl];"),
+               ("const Cold cd = W.cold[f.s];", "const Cold cd = W.cold[sl];"),
+               ("W.tx + (uint64_t)kTx * f.s);\n      t0 = tp4[0];", "W.tx + (uint64_t)kTx * sl);\n      t0 = tp4[0];"),
+               ("g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);", "g.p = (PW_GLOBAL uint8_t*)(A.text + fdst);")],
     "fx_bigwin": [("constexpr int kFxLit = 32;", "constexpr int kFxLit = 64;\nconstexpr int kFxQ = 128;"),
                   ("  uint8_t qw[kQWin];\n  uint8_t lw[kFxLit];", "  uint8_t qw[kFxQ];\n  uint8_t lw[kFxLit];"),
                   ("    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];",
@@ -164,6 +172,7 @@ PATCHES = {
                "        for (int j = 6; j >= 0; j--)\n          __builtin_amdgcn_raw_buffer_store_b128(group(j)")],
 }
 
+PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
