@@ -1,6 +1,7 @@
 """Experiment variants of pw_report.hip (never shipped; timing only unless noted) linked into
 tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   cur      the working copy
+  head     pw_report.hip at git HEAD
   allgen   every render wave takes the general emit_event path (same bytes)
   allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
   noline   no line is built (every line 78 bytes of whatever the buffer holds: timing only)
@@ -185,7 +186,10 @@ FLAGS = {
 
 def build(name):
     s = open(SRC).read()
-    for a, b in PATCHES[name]:
+    if name == "head":  # pw_report.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
+        s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_report.hip"], check=True,
+                           capture_output=True, text=True).stdout
+    for a, b in PATCHES.get(name, []):
         assert a in s, (name, a)
         s = s.replace(a, b)
     os.makedirs(TMP, exist_ok=True)
