@@ -3241,10 +3241,12 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     hipLaunchKernelGGL(pw::plan_kernel, dim3((args->n_alns + 255) / 256), dim3(256), 0, st, *args, W);
     hipLaunchKernelGGL(pw::carry_kernel, dim3((uint32_t)ncu * 8u), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   }
-  // mostly short records (a gene panel): two per wavefront (index_pair_kernel)
+  // mostly short records (a gene panel): two per wavefront (index_pair_kernel); its grid is two
+  // full rounds at the 4 waves/SIMD it runs at (sweep on cfg3 at 0.2: 8 per CU 1,421-1,436 us,
+  // 4 / 12 1,427 / 1,421, 10 — index_kernel's, 2.5 rounds here — 1,474-1,481, 16 1,458)
   if (args->n_short && (uint64_t)args->n_short * 4 >= (uint64_t)args->n_alns * 3)
     hipLaunchKernelGGL(pw::index_pair_kernel,
-                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 10u)),
+                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 8u)),
                        dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   else
     hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);

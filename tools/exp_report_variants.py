@@ -2,6 +2,7 @@
 tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   cur      the working copy
   head     pw_report.hip at git HEAD
+  pg4..pg16  index_pair_kernel grid of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
   allgen   every render wave takes the general emit_event path (same bytes)
   allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
   noline   no line is built (every line 78 bytes of whatever the buffer holds: timing only)
@@ -173,6 +174,10 @@ PATCHES = {
                "        for (int j = 6; j >= 0; j--)\n          __builtin_amdgcn_raw_buffer_store_b128(group(j)")],
 }
 
+# index_pair_kernel grid (workgroups per CU; the product's 10 was swept for index_kernel at 5
+# waves/SIMD, the pair kernel runs at 4)
+for _g in (4, 8, 12, 16):
+    PATCHES[f"pg{_g}"] = [("nwave - 1) / nwave, (uint64_t)ncu * 10u)),", f"nwave - 1) / nwave, (uint64_t)ncu * {_g}u)),")]
 PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
