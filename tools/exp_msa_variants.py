@@ -7,6 +7,7 @@
   rp_lds   tools/variants/row_prefix_lds.patch (row_prefix stages the row's runs in LDS)
   k1_3ahead  row_chunk_sums with three groups' loads in flight instead of two
   k1_32b   tools/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
+  k1g<N>   row_chunk_sums with a grid of N workgroups (product: 2048)
   head     pw_msa.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
 Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
 import os
@@ -81,6 +82,9 @@ def make(name):
         open(p, "w").write(s)
         subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_chunk_sums_32bases.patch")], check=True)
         s = open(p).read()
+    elif name.startswith("k1g"):  # row_chunk_sums grid of N workgroups (product: 2048)
+        n = int(name[3:])
+        s = sub(s, "(nb1 < 2048 ? nb1 : 2048)", f"(nb1 < {n} ? nb1 : {n})")
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout
