@@ -1130,8 +1130,10 @@ static int msa_count(const pw_msa_args* a, void* stream, bool call, uint8_t* con
   const unsigned sy = a->n_rows >= 2048 ? 1u : (2048u / a->n_rows < 64u ? 2048u / a->n_rows : 64u);
   hipLaunchKernelGGL(pw::slot_rows, dim3(a->n_rows < 8192 ? a->n_rows : 8192, sy), dim3(256), 0, s, *a, slot_row, sdesc);
   const uint64_t nb1 = ((a->n_slots + 3) / 4 + 3) / 4;  // 4 slots per wave, 4 waves per workgroup
-  // (persistent: ~2 rounds of resident waves, each streaming many groups)
-  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 2048 ? nb1 : 2048)), dim3(256), 0, s, *a,
+  // (persistent: 8192 workgroups, ~4 rounds of resident waves, each streaming a few groups — the
+  // round-4 sweep on cfg5: 2048 68.6-69.2 us, 4096 65.3-65.5, 6144 63.8, 8192 62.1-62.3, uncapped
+  // (36 k) 62.6: fewer groups per wave end the kernel with less of a tail)
+  hipLaunchKernelGGL(pw::row_chunk_sums, dim3((unsigned)(nb1 < 8192 ? nb1 : 8192)), dim3(256), 0, s, *a,
                      chunk_sum, sdesc, runs);
   hipLaunchKernelGGL(pw::row_prefix, dim3(a->n_rows < 4096 ? a->n_rows : 4096), dim3(1024), 0, s, *a, chunk_sum, ckpt,
                      rinfo, runs, tstart);
