@@ -325,8 +325,10 @@ extern "C" int pw_pack_cs_batch(const uint8_t* cs_text, const uint64_t* cs_off, 
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
   }
-  // persistent wavefronts, two rounds of 8 resident workgroups per CU
-  const uint32_t cap = (uint32_t)ncu * 16u;
+  // persistent wavefronts, 64 workgroups per CU (~8 rounds of resident workgroups: fewer records
+  // per wave, a shorter tail — round-4 sweep on cfg2's 100k records: 8 / 16 / 32 / 64 / 1000 per CU
+  // 145.9 / 132.0 / 124.7-125.4 / 123.1-123.8 / 126.0 us)
+  const uint32_t cap = (uint32_t)ncu * 64u;
   const uint32_t grid = (n + 3) / 4 < cap ? (n + 3) / 4 : cap;
   hipLaunchKernelGGL(pw::pack_cs_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, cs_text, cs_off, offset, qlen,
                      n, ops, lits, out);

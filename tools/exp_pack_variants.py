@@ -1,0 +1,47 @@
+"""Experiment builds of pw_pack.hip (never shipped), linked with the other product objects into
+tools/abl_build/<name>/lib for tools/pk_sweep.sh (PWASM_LIB):
+  cur      the working copy
+  pkg<N>   pack_cs_kernel grid capped at N workgroups per CU (product: 16)
+Usage: python tools/exp_pack_variants.py [names...]"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "pwasm_amd/csrc/pw_pack.hip")
+OUT = os.path.join(REPO, "tools/abl_build")
+TMP = os.path.join(REPO, "build_exp")
+
+
+def make(name):
+    s = open(SRC).read()
+    if name.startswith("pkg"):
+        old = "const uint32_t cap = (uint32_t)ncu * 16u;"
+        assert old in s
+        s = s.replace(old, f"const uint32_t cap = (uint32_t)ncu * {int(name[3:])}u;")
+    elif name != "cur":
+        raise SystemExit(f"unknown variant {name}")
+    os.makedirs(TMP, exist_ok=True)
+    p = os.path.join(TMP, f"pack_{name}.hip")
+    open(p, "w").write(s)
+    return p
+
+
+def build(name):
+    src = make(name)
+    bdir = os.path.join(REPO, "pwasm_amd/build")
+    objs = [os.path.join(bdir, f) for f in sorted(os.listdir(bdir)) if f.endswith(".o") and f != "pw_pack.o"]
+    inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "pwasm_amd/csrc")]
+    d = os.path.join(OUT, name)
+    os.makedirs(os.path.join(d, "lib"), exist_ok=True)
+    o = os.path.join(d, "pw_pack.o")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall",
+                    "-Wno-unused-function", *inc, "-c", src, "-o", o], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950", "-o",
+                    os.path.join(d, "lib", "libpwasm_amd.so"), o, *objs, "-ldl"], check=True)
+    print("built", name, flush=True)
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or ["cur"]:
+        build(n)
