@@ -3234,9 +3234,12 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   // the counters (a memset launch: without it index_kernel starts at once and the next-stop table
   // built beside it on a side stream slows it down — index 127 -> 143 us, table 29 -> 66 us)
   if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;
-  // (two rounds at 5 waves/SIMD; sweep: 16 -> 10 per CU saved ~10 us of index + tctx); with long
-  // records the blocks of 1.. are spread over the full grid whatever the record count
-  if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;
+  // (four rounds at 5 waves/SIMD — round-4 sweep on cfg2, same-box pairs: 10 / 15 / 20 / 30 per
+  // CU 127.9-128.8 / 128.3 / 125.9-126.1 / 128.7 us; round 2 found 16 worse than 10 before the
+  // segment and prefetch changes); with long records (planned) the blocks of 1.. are spread over a
+  // grid of 10 per CU whatever the record count (the grid that was measured for cfg4)
+  if (planned) ig = (uint64_t)ncu * 10u;
+  else if (ig > (uint64_t)ncu * 20u) ig = (uint64_t)ncu * 20u;
   if (planned) {  // records of more than PW_BLOCK_OPS ops
     hipLaunchKernelGGL(pw::plan_kernel, dim3((args->n_alns + 255) / 256), dim3(256), 0, st, *args, W);
     hipLaunchKernelGGL(pw::carry_kernel, dim3((uint32_t)ncu * 8u), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);

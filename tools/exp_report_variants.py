@@ -2,6 +2,8 @@
 tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   cur      the working copy
   head     pw_report.hip at git HEAD
+  tg8..tg16  tctx_kernel grid of 8 / 12 / 16 workgroups per CU (product: 4)
+  ig15..ig30 index_kernel grid of 15 / 20 / 30 workgroups per CU (product: 10)
   pg4..pg16  index_pair_kernel grid of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
   allgen   every render wave takes the general emit_event path (same bytes)
   allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
@@ -178,6 +180,12 @@ PATCHES = {
 # waves/SIMD, the pair kernel runs at 4)
 for _g in (4, 8, 12, 16):
     PATCHES[f"pg{_g}"] = [("nwave - 1) / nwave, (uint64_t)ncu * 10u)),", f"nwave - 1) / nwave, (uint64_t)ncu * {_g}u)),")]
+# tctx_kernel grid (workgroups per CU; product 4) and index_kernel grid (product 10)
+for _g in (8, 12, 16):
+    PATCHES[f"tg{_g}"] = [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", f"if (tg > (uint64_t)ncu * {_g}u) tg = (uint64_t)ncu * {_g}u;")]
+for _g in (15, 20, 30):
+    PATCHES[f"ig{_g}"] = [("if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;",
+                           f"if (ig > (uint64_t)ncu * {_g}u || planned) ig = (uint64_t)ncu * {_g}u;")]
 PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
