@@ -8,6 +8,7 @@
   k1_3ahead  row_chunk_sums with three groups' loads in flight instead of two
   k1_32b   tools/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
   k1g<N>   row_chunk_sums with a grid of N workgroups (product: 2048)
+  sy<N>    slot_rows with N workgroups per row (product: 2048 / rows)
   head     pw_msa.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
 Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
 import os
@@ -85,6 +86,9 @@ def make(name):
     elif name.startswith("k1g"):  # row_chunk_sums grid of N workgroups (product: 2048)
         n = int(name[3:])
         s = sub(s, "(nb1 < 2048 ? nb1 : 2048)", f"(nb1 < {n} ? nb1 : {n})")
+    elif name.startswith("sy"):  # slot_rows with N workgroups per row (product: 2048 / rows, <= 64)
+        s = sub(s, "const unsigned sy = a->n_rows >= 2048 ? 1u : (2048u / a->n_rows < 64u ? 2048u / a->n_rows : 64u);",
+                f"const unsigned sy = {int(name[2:])}u;")
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout
