@@ -3258,9 +3258,10 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
     hipLaunchKernelGGL(pw::tctx_kernel, dim3((uint32_t)tg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     uint64_t rg = (W.n_chunks + nwave - 1) / nwave;
-    // two rounds of the kRenderOcc resident workgroups per CU (sweep: render 286.5 vs 288-290 us
-    // at one round — the second round fills the CUs whose first workgroups finish early)
-    if (rg > (uint64_t)ncu * 2u * pw::kRenderOcc) rg = (uint64_t)ncu * 2u * pw::kRenderOcc;
+    // four rounds of the kRenderOcc resident workgroups per CU: later rounds fill the CUs whose
+    // first workgroups finish early (round 2: 2 rounds 286.5 vs 288-290 us at one; round 4,
+    // same-call pairs on cfg2: 4 rounds 214.1-216.3 us, 8 rounds 215.2, 2 rounds 220.8-221.5)
+    if (rg > (uint64_t)ncu * 4u * pw::kRenderOcc) rg = (uint64_t)ncu * 4u * pw::kRenderOcc;
     // (render is the first kernel that reads next_stop)
     if (next_stop_ready && hipStreamWaitEvent(st, (hipEvent_t)next_stop_ready, 0) != hipSuccess) return PW_E_HIP;
     hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);

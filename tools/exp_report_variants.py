@@ -4,6 +4,9 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   head     pw_report.hip at git HEAD
   tg8..tg16  tctx_kernel grid of 8 / 12 / 16 workgroups per CU (product: 4)
   ig15..ig30 index_kernel grid of 15 / 20 / 30 workgroups per CU (product: 10)
+  rr4 / rr8  render grid of 4 / 8 rounds of resident workgroups (product: 2)
+  igp20      index_kernel grid of 20 per CU for long-record (planned) batches (product: 10)
+  cg4 / cg16 carry_kernel grid of 4 / 16 per CU (product: 8)
   pg4..pg16  index_pair_kernel grid of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
   allgen   every render wave takes the general emit_event path (same bytes)
   allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
@@ -186,6 +189,14 @@ for _g in (8, 12, 16):
 for _g in (15, 20, 30):
     PATCHES[f"ig{_g}"] = [("if (ig > (uint64_t)ncu * 10u || planned) ig = (uint64_t)ncu * 10u;",
                            f"if (ig > (uint64_t)ncu * {_g}u || planned) ig = (uint64_t)ncu * {_g}u;")]
+# render grid in rounds of the resident workgroups (product: 2), long-record (planned) index grid
+# and carry_kernel grid (product: 10 / 8 per CU)
+for _g in (4, 8):
+    PATCHES[f"rr{_g}"] = [("if (rg > (uint64_t)ncu * 2u * pw::kRenderOcc) rg = (uint64_t)ncu * 2u * pw::kRenderOcc;",
+                           f"if (rg > (uint64_t)ncu * {_g}u * pw::kRenderOcc) rg = (uint64_t)ncu * {_g}u * pw::kRenderOcc;")]
+PATCHES["igp20"] = [("if (planned) ig = (uint64_t)ncu * 10u;", "if (planned) ig = (uint64_t)ncu * 20u;")]
+PATCHES["cg16"] = [("pw::carry_kernel, dim3((uint32_t)ncu * 8u)", "pw::carry_kernel, dim3((uint32_t)ncu * 16u)")]
+PATCHES["cg4"] = [("pw::carry_kernel, dim3((uint32_t)ncu * 8u)", "pw::carry_kernel, dim3((uint32_t)ncu * 4u)")]
 PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
