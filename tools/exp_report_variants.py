@@ -7,7 +7,7 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   rr4 / rr8  render grid of 4 / 8 rounds of resident workgroups (product: 2)
   igp20      index_kernel grid of 20 per CU for long-record (planned) batches (product: 10)
   cg4 / cg16 carry_kernel grid of 4 / 16 per CU (product: 8)
-  pg4..pg16  index_pair_kernel grid of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
+  pg4..pg16  index_pair_kernel grid (pg10: the pre-round-4-end 10) of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
   allgen   every render wave takes the general emit_event path (same bytes)
   allfast  every render wave takes emit_fast (wrong bytes where a lane is not fast: timing only)
   noline   no line is built (every line 78 bytes of whatever the buffer holds: timing only)
@@ -181,8 +181,8 @@ PATCHES = {
 
 # index_pair_kernel grid (workgroups per CU; the product's 10 was swept for index_kernel at 5
 # waves/SIMD, the pair kernel runs at 4)
-for _g in (4, 8, 12, 16):
-    PATCHES[f"pg{_g}"] = [("nwave - 1) / nwave, (uint64_t)ncu * 10u)),", f"nwave - 1) / nwave, (uint64_t)ncu * {_g}u)),")]
+for _g in (4, 10, 12, 16):  # (the product took 8 in round 4)
+    PATCHES[f"pg{_g}"] = [("nwave - 1) / nwave, (uint64_t)ncu * 8u)),", f"nwave - 1) / nwave, (uint64_t)ncu * {_g}u)),")]
 # tctx_kernel grid (workgroups per CU; product 4) and index_kernel grid (product 10)
 for _g in (8, 12, 16):
     PATCHES[f"tg{_g}"] = [("if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;", f"if (tg > (uint64_t)ncu * {_g}u) tg = (uint64_t)ncu * {_g}u;")]
