@@ -6,6 +6,7 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   ig15..ig30 index_kernel grid of 15 / 20 / 30 workgroups per CU (product: 10)
   rr4 / rr8  render grid of 4 / 8 rounds of resident workgroups (product: 2)
   igp20      index_kernel grid of 20 per CU for long-record (planned) batches (product: 10)
+  ns256 / ns1024 next-stop table grid capped at 256 / 1024 workgroups (product: 4096)
   cg4 / cg16 carry_kernel grid of 4 / 16 per CU (product: 8)
   pg4..pg16  index_pair_kernel grid (pg10: the pre-round-4-end 10) of 4 / 8 / 12 / 16 workgroups per CU (product: 10)
   allgen   every render wave takes the general emit_event path (same bytes)
@@ -197,6 +198,9 @@ for _g in (4, 8):
 PATCHES["igp20"] = [("if (planned) ig = (uint64_t)ncu * 10u;", "if (planned) ig = (uint64_t)ncu * 20u;")]
 PATCHES["cg16"] = [("pw::carry_kernel, dim3((uint32_t)ncu * 8u)", "pw::carry_kernel, dim3((uint32_t)ncu * 16u)")]
 PATCHES["cg4"] = [("pw::carry_kernel, dim3((uint32_t)ncu * 8u)", "pw::carry_kernel, dim3((uint32_t)ncu * 4u)")]
+# next-stop table grid (product: min(queries, 4096) workgroups, one query each at a time)
+for _g in (256, 1024):
+    PATCHES[f"ns{_g}"] = [("  const uint32_t grid = nq < 4096u ? nq : 4096u;", f"  const uint32_t grid = nq < {_g}u ? nq : {_g}u;")]
 PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
