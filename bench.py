@@ -6,8 +6,16 @@ table build (pw_stop_table_build, on a side stream overlapping the decode kernel
 decode/classify/codon/render kernels (pw_report_events_after) over every record of the batch.  At N=1 the batch is BASELINE.json
 configs[1] (cfg2: 100k synthetic minimap2-style records, 1,000 CDS of 1-5 kb, ~1% ONT-style
 errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard (different
-seed = different target genomes; weak scaling, no data-path collective); the timed region is
-bracketed by barrier + synchronize, the max over ranks is reported.
+seed = different target genomes; weak scaling, no data-path collective; the per-genome tables
+are all-gathered over RCCL every step); the timed region is bracketed by barrier + synchronize,
+the max over ranks is reported.  Beside it at N>1 (sub-object "cfg3"): BASELINE configs[2], the
+one 10M-record set sharded by target genome over the N ranks (strong scaling), and the node's
+end-to-end run of it (pwasm_amd.mgpu).
+
+`python3 bench.py --gpus N` with no WORLD_SIZE in the environment launches the N ranks itself
+(one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
+as torchrun sets them) before anything touches the GPU; under torchrun WORLD_SIZE must equal
+--gpus.
 
 Also reported (rank 0): roofline of the dominant kernel sequence (algorithmic bytes / the pass's
 average GPU time — HIP events around the K timed passes, divided by K — vs 8 TB/s) and the CPU
@@ -37,7 +45,8 @@ def log(*a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=None,
@@ -53,12 +62,20 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="N > 1: skip the end-to-end pwasm_amd.mgpu leg")
     ap.add_argument("--no-gapassem", action="store_true", help="N = 1, cfg2: skip the cfg5 (GapAssem) sub-object")
     ap.add_argument("--e2e-parity", action="store_true", help="N > 1: CRC the end-to-end report against the oracle")
+    ap.add_argument("--no-cfg3", action="store_true", help="N > 1: skip the cfg3 (10M records sharded) sub-object")
+    ap.add_argument("--cfg3-scale", type=float, default=1.0, help="N > 1: scale of the cfg3 sub-object's record set")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
+    plan = launch_plan(args.gpus, sys.argv[1:], os.environ)
+    if isinstance(plan, str):
+        log(f"bench.py: {plan}")
+        sys.exit(2)
+    if plan:  # python3 bench.py --gpus N: start the N ranks (nothing here has touched torch / HIP)
+        sys.exit(run_ranks(plan))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.config is None:
-        args.config = 2 if world == 1 else 3
+        args.config = 2
     if args.traffic_json is None:  # the newest committed profile of the same command (profiles/run_prof.sh)
         args.traffic_json = latest_profile(args.config)
 
@@ -85,11 +102,48 @@ def main():
             dist.destroy_process_group()
         return
 
+    out = report_leg(args, args.config, world, rank, dev_name)
+    if world > 1 and args.config == 2 and not args.no_cfg3:
+        # BASELINE configs[2] beside the weak-scaled line: the one 10M-record set sharded by target
+        # genome over the N ranks (strong scaling) + the node's end-to-end run of it
+        torch.cuda.empty_cache()
+        c3 = argparse.Namespace(**{**vars(args), "scale": args.cfg3_scale, "traffic_json": None})
+        sub = report_leg(c3, 3, world, rank, dev_name)
+        if rank == 0:
+            out["cfg3"] = {k: sub[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config",
+                                               "roofline", "e2e")}
+    if rank == 0:
+        out["config"]["ranks"] = world
+        out["config"]["backend"] = dist.get_backend() if dist.is_initialized() else "none"
+        out["config"]["launcher"] = os.environ.get("PW_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process")
+        if world == 1 and args.config == 2 and not args.no_gapassem:
+            # BASELINE configs[4] beside it, timed in its own region after the cfg2 one (cfg2's
+            # device buffers released first): the GapAssem step, its roofline, parity, CPU baseline
+            torch.cuda.empty_cache()
+            ga = argparse.Namespace(**{**vars(args), "config": 5, "scale": 1.0, "remove_gaps": False,
+                                       "traffic_json": latest_profile(5)})
+            g = bench_gapassem(ga, 1, 0, dev_name)
+            out["gapassem"] = {k: g[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
+                                                 "config", "parity", "roofline", "cpu_baseline")}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def report_leg(args, config, world, rank, dev_name):
+    """One pafreport pass benchmark (config 2 weak / 3 sharded by target genome); the JSON object
+    on rank 0, None elsewhere."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pwasm_amd as pw
+
     # ---- data (synthetic, seeded; generated outside the timed region).  cfg3 is ONE 10M-record
     # set: rank r generates exactly the lines of its target-genome shard (crc32(target) % N == r,
     # the rule of pw_batch_from_files_shard / pwasm_amd.mgpu) — strong scaling.  Other configs
     # at N > 1: one independent batch per rank (weak scaling).
-    sharded = args.config == 3
+    sharded = config == 3
     tmp = tempfile.mkdtemp(prefix=f"pwbench{rank}_")
     if sharded and world > 1:  # one 10M-record file for the node (rank 0 writes it; ranks share it)
         box = [tmp if rank == 0 else None]
@@ -98,18 +152,18 @@ def main():
     else:
         shared = tmp
     fa, paf = os.path.join(shared, "q.fa"), os.path.join(shared, "a.paf")
-    seed = 3 if sharded else (2 + 1000 * rank if args.config == 2 else args.config + 1000 * rank)
+    seed = 3 if sharded else (2 + 1000 * rank if config == 2 else config + 1000 * rank)
     t0 = time.time()
-    cmd = [str(REPO / "synth/build/pwsynth"), "paf", "--config", str(args.config), "--scale", str(args.scale),
+    cmd = [str(REPO / "synth/build/pwsynth"), "paf", "--config", str(config), "--scale", str(args.scale),
            "--seed", str(seed), "--fa", fa, "--paf", paf]
-    if args.config in (3, 4):
+    if config in (3, 4):
         cmd += ["--threads", str(host_threads())]
     if not (sharded and world > 1 and rank != 0):
         subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
     if sharded and world > 1:
         dist.barrier()
     t_gen = time.time() - t0
-    flags = pw.FLAG_G | pw.FLAG_C if args.config in (1, 2, 3) else 0
+    flags = pw.FLAG_G | pw.FLAG_C if config in (1, 2, 3) else 0
     # cfg3 over N ranks: rank r packs the lines of its target-genome shard (crc32 of PAF column 6)
     batch = pw.HostBatch(fa, paf, flags, rank, world) if sharded else pw.HostBatch(fa, paf, flags)
     v = batch.view
@@ -214,7 +268,7 @@ def main():
         # end to end over the node: pwasm_amd.mgpu (every rank reads 1/N of the PAF, exchanges lines
         # by target genome, packs / runs / writes its own records at their offsets of one report)
         from pwasm_amd import mgpu
-        del dev
+        dev = None
         torch.cuda.empty_cache()
         out_path = os.path.join(shared, "report_e2e.txt")
         dist.barrier()
@@ -250,12 +304,12 @@ def main():
         alg_text = int(v.alg_bytes_in) + text_bytes
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         prof = {}
-        if args.config == 2 and args.scale == 1.0 and args.traffic_json and os.path.exists(args.traffic_json):
+        if config == 2 and args.scale == 1.0 and args.traffic_json and os.path.exists(args.traffic_json):
             prof = json.load(open(args.traffic_json))
         traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
         flags_cli = ["-G", "-C"] if flags else []
         parity, cpu, e2e, gpack = None, None, None, None
-        big = args.config == 4 or v.n_alns > 200000
+        big = config == 4 or v.n_alns > 200000
         if not args.no_parity and world == 1 and big:
             # too large for files on both sides: the report of the benchmarked batch and the
             # CLI's stdout streamed through CRC-32, against the oracle run over byte ranges of
@@ -292,7 +346,7 @@ def main():
             gpack = gpu_pack_check(pw, paf)
         if cpu is None and not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(flags_cli, fa, paf, args.cpu_sample if args.cpu_sample else
-                               (10 if args.config == 4 else 100000), tmp)
+                               (10 if config == 4 else 100000), tmp)
         if cpu is not None:
             cpu.update(host_cpu())
         out = {
@@ -311,7 +365,7 @@ def main():
             "config": {"workload": (f"cfg3: {tot_records} PAF records (gene panel of {v.n_queries} CDS x assemblies, "
                                     f"-G -C) sharded by target genome over {world} GPU(s), {tot_events} events"
                                     if sharded else
-                                    f"cfg{args.config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
+                                    f"cfg{config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
                                     f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU"),
                        "records_per_gpu": int(v.n_alns), "events_per_gpu": n_events, "scale": args.scale,
                        "parallelism": (f"shard-by-target x{world} + RCCL all-gather of per-genome tables"
@@ -331,19 +385,11 @@ def main():
             "e2e": e2e if e2e is not None else e2e_node,
             "gpu_pack": gpack,
         }
-        if world == 1 and args.config == 2 and not args.no_gapassem:
-            # BASELINE configs[4] beside it, timed in its own region after the cfg2 one (cfg2's
-            # device buffers released first): the GapAssem step, its roofline, parity, CPU baseline
-            del dev
-            torch.cuda.empty_cache()
-            ga = argparse.Namespace(**{**vars(args), "config": 5, "scale": 1.0, "remove_gaps": False,
-                                       "traffic_json": latest_profile(5)})
-            g = bench_gapassem(ga, 1, 0, dev_name)
-            out["gapassem"] = {k: g[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype",
-                                                 "config", "parity", "roofline", "cpu_baseline")}
-        print(json.dumps(out), flush=True)
+    dev = None
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    shutil.rmtree(tmp, ignore_errors=True)  # (rank 0's is the shared one at cfg3: ~4 GB of PAF + report)
+    return out if rank == 0 else None
 
 
 def bench_gapassem(args, world, rank, dev_name):
@@ -483,6 +529,60 @@ def bench_gapassem(args, world, rank, dev_name):
         }
         return out
     return None
+
+
+def launch_plan(gpus, argv, env, port=None):
+    """What `bench.py --gpus N` starts: [] when this process is the (only) rank itself; a list of
+    (argv, env) pairs, one per rank, when it must launch N > 1 ranks (no WORLD_SIZE in the
+    environment); an error string when WORLD_SIZE contradicts --gpus.  Pure: nothing is started and
+    no GPU is touched (tests/test_bench_launch.py)."""
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if gpus is not None and int(world) != gpus:
+            return f"WORLD_SIZE={world} but --gpus {gpus}: run one rank per GPU (torchrun --nproc-per-node {gpus})"
+        return []
+    if gpus is None or gpus <= 1:
+        return []
+    if port is None:
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+    plan = []
+    for r in range(gpus):
+        e = dict(env)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(gpus), "LOCAL_WORLD_SIZE": str(gpus),
+                  "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                  "PW_BENCH_LAUNCHER": "bench.py --gpus"})
+        plan.append(([sys.executable, str(REPO / "bench.py"), *argv], e))
+    return plan
+
+
+def run_ranks(plan, poll_s=0.5):
+    """Start every rank of the plan as a child process (same process group, inherited stdout /
+    stderr: rank 0 prints the JSON line) and wait; the first rank that fails ends the others.
+    Returns the exit code: 0, or the first failing rank's."""
+    procs = [subprocess.Popen(cmd, env=env) for cmd, env in plan]
+    code = 0
+    try:
+        while procs:
+            for p in list(procs):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                procs.remove(p)
+                if rc != 0 and code == 0:
+                    code = rc if rc > 0 else 128 - rc
+                    log(f"bench.py: a rank exited with {rc}; stopping the others")
+                    for q in procs:
+                        q.terminate()
+            time.sleep(poll_s)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    return code
 
 
 def host_cpu():

@@ -566,8 +566,8 @@ static void msa_add_align(gsalign* m, gaseq* seq, gsalign* om, gaseq* oseq) {
   free(om->rows);
   free(om);
 }
-/* writeMSA :1039-1046 -> finalize -> prepSeq (revcompl) -> printMFasta :482-520 */
-static void msa_write(gsalign* m, FILE* f) {
+/* finalize :1006-1012 -> prepSeq :89-101 (no deletions in pafreport: only the revcompl) */
+static void msa_finalize(gsalign* m) {
   for (int i = 0; i < m->n; i++) {
     gaseq* s = m->rows[i];
     if (s->len == 0) gerror("Error: sequence for %s not loaded!\n", s->id);
@@ -581,6 +581,40 @@ static void msa_write(gsalign* m, FILE* f) {
       s->prepped = 1;
     }
   }
+}
+/* GSeqAlign::print(f, 'v') :1013-1037 -> GASeq::printGappedSeq(f, minoffset) :412-440, the -D dump
+ * of pafreport.cpp:443-446.  gclib's FastaSeq::getNameLen() is taken to be strlen(name) (gclib is
+ * absent: an assumption).  Rows are never clipped in pafreport (clp5 = clp3 = 0), so
+ * no base is lower-cased by the clip rule; tseq's own lower-case bases print as they are. */
+static void msa_print(gsalign* m, FILE* f, char c) {
+  msa_finalize(m);
+  int max = 0;
+  for (int i = 0; i < m->n; i++) {
+    const int n = (int)strlen(m->rows[i]->id);
+    if (n > max) max = n;
+  }
+  if (c != 0) {
+    fprintf(f, "%*s %c ", max, " ", ' ');
+    for (int k = 0; k < m->length; k++) fputc(c, f);
+    fputc('\n', f);
+  }
+  for (int i = 0; i < m->n; i++) {
+    gaseq* s = m->rows[i];
+    fprintf(f, "%*s %c ", max, s->id, s->revcompl == 1 ? '-' : '+');
+    if (s->len == 0 || s->len != s->seqlen)
+      gerror("GASeq print Error: invalid sequence data '%s' (len=%d, seqlen=%d)\n", s->id, s->len, s->seqlen);
+    for (int k = 0; k < s->offset - m->minoffset; k++) fputc(' ', f);
+    for (int k = 0; k < s->seqlen; k++) {
+      if (s->ofs[k] < 0) continue; /* deleted base */
+      for (int j = 0; j < s->ofs[k]; j++) fputc('-', f);
+      fputc(s->seq[k], f);
+    }
+    fputc('\n', f);
+  }
+}
+/* writeMSA :1039-1046 -> finalize -> prepSeq (revcompl) -> printMFasta :482-520 */
+static void msa_write(gsalign* m, FILE* f) {
+  msa_finalize(m);
   for (int i = 0; i < m->n; i++) {
     gaseq* s = m->rows[i];
     const int llen = 60;
@@ -1352,6 +1386,12 @@ int main(int argc, char* argv[]) {
         ref_msa = ga_ref->msa;
       }
     }
+  }
+  /* :443-446 -D: the MSA dump on stderr before it is written (without -w, or with no alignment,
+   * refMSA is NULL and the reference dereferences it: nothing is printed here, D7 / D10) */
+  if (debug_mode && ref_msa) {
+    fprintf(g_errf, ">MSA (%d)\n", ref_msa->n);
+    msa_print(ref_msa, g_errf, 'v');
   }
   if (fmsa) { /* :447-450 (no alignment at all: the reference dereferences NULL; here: empty file, D10) */
     if (ref_msa) msa_write(ref_msa, fmsa);

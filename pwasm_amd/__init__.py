@@ -431,6 +431,14 @@ class HostBatch:
             pass
 
 
+def _env_flag(name):
+    """An integer switch read as the C host reads it (atoi(getenv(name)) != 0): unset, empty, "0"
+    or a non-number are off."""
+    import re
+    m = re.match(r"\s*[+-]?\d+", os.environ.get(name, ""))
+    return m is not None and int(m.group(0)) != 0
+
+
 def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     """pw_report_args over the device tensors of stage_batch()."""
     v = batch.view
@@ -452,7 +460,7 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     a.n_ev_slots = int(v.n_events_max)
     a.pages = dev["pages"].data_ptr()
     a.max_rec_ops = batch.max_rec_ops()
-    a.n_short = 0 if os.environ.get("PW_NO_PAIRS") else batch.n_short()
+    a.n_short = 0 if _env_flag("PW_NO_PAIRS") else batch.n_short()
     return a
 
 

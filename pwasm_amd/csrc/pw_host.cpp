@@ -2006,9 +2006,11 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   }
   fflush(out.f);
   if (prof) fprintf(stderr, "[cli] total %.3f s\n", now() - t_start);
+  // -D dumps refMSA on stderr first (pafreport.cpp:443-446; without -w refMSA is NULL there, D7)
   if (fmsa.f && pk.run.qi >= 0) {  // refMSA->writeMSA(fmsa), pafreport.cpp:447-450
     const int qi = pk.run.qi;
-    const int rc = pw::write_run_msa(fmsa.f, qdb.ids[(size_t)qi].c_str(), qdb.seq.data() + qdb.off[(size_t)qi],
+    fflush(stderr);
+    const int rc = pw::write_run_msa(fmsa.f, debug ? stderr : nullptr, qdb.ids[(size_t)qi].c_str(), qdb.seq.data() + qdb.off[(size_t)qi],
                                  qdb.len[(size_t)qi], pk.run);
     if (rc != 0) return rc;
   }
@@ -2160,7 +2162,7 @@ extern "C" int pw_batch_write_msa(const pw_batch* bt, const char* path) {
   int rc = 0;
   const pw::MsaRun& run = bt->pk.run;
   if (run.qi >= 0)
-    rc = pw::write_run_msa(f, bt->q.ids[(size_t)run.qi].c_str(), bt->q.seq.data() + bt->q.off[(size_t)run.qi],
+    rc = pw::write_run_msa(f, nullptr, bt->q.ids[(size_t)run.qi].c_str(), bt->q.seq.data() + bt->q.off[(size_t)run.qi],
                            bt->q.len[(size_t)run.qi], run);
   if (fclose(f) != 0 && rc == 0) rc = PW_E_IO;
   return rc;

@@ -138,7 +138,7 @@ bool closed_form_ok(const MsaRun& run) {
 // pafreport's own construction (pafreport.cpp:382-421) through the GapAssem C++ API: the first
 // alignment's GSeqAlign(refseq, taseq) becomes refMSA, every later one is a GSeqAlign(rseq,
 // taseq) merged into it by addAlign (injectGap both ways, addSeq), then writeMSA.
-int replay(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& run) {
+int replay(FILE* f, FILE* dbg, const char* qid, const uint8_t* q, int qlen, const MsaRun& run) {
   GASeq* refseq = new GASeq(qid, nullptr, (const char*)q, qlen);  // (upper case already: allupper)
   refseq->setFlag(GA_FLAG_IS_REF);
   GSeqAlign* refMSA = nullptr;
@@ -162,6 +162,10 @@ int replay(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& r
       delete newmsa;  // its rows now belong to refMSA (addAlign cleared its free flag)
     }
   }
+  if (refMSA && dbg) {  // -D (pafreport.cpp:443-446)
+    fprintf(dbg, ">MSA (%d)\n", refMSA->Count());
+    refMSA->print(dbg, 'v');
+  }
   if (refMSA) refMSA->writeMSA(f);
   delete refMSA;  // frees refseq and every taseq
   return 0;
@@ -169,7 +173,7 @@ int replay(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& r
 
 }  // namespace
 
-int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& run) {
+int write_run_msa(FILE* f, FILE* dbg, const char* qid, const uint8_t* q, int qlen, const MsaRun& run) {
   if (run.recs.empty()) return 0;  // no alignment: the reference dereferences NULL
   // PW_MSA_PATH (tests): "replay" forces the literal merge, "closed" refuses to fall back to it
   const char* path = getenv("PW_MSA_PATH");
@@ -179,9 +183,9 @@ int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const Ms
       fprintf(stderr, "pw msa: the closed form does not apply to this run (PW_MSA_PATH=closed)\n");
       return 2;
     }
-    return replay(f, qid, q, qlen, run);
+    return replay(f, dbg, qid, q, qlen, run);
   };
-  if (force_replay) return replay(f, qid, q, qlen, run);
+  if (force_replay) return replay(f, dbg, qid, q, qlen, run);
   if (!closed_form_ok(run)) return fallback();
   // G = elementwise max of the alignments' query gaps (setGap semantics per alignment)
   std::vector<int32_t> G((size_t)qlen, 0);
@@ -197,10 +201,14 @@ int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const Ms
     if (g > 32767) return fallback();
   std::string tseq;
   std::vector<int32_t> ofs, extra;
+  long shift = 0;  // columns injected before the row's offset (injectGap moves the offset itself)
   // The row of alignment r in the final layout: its pairwise gaps plus, for every query gap
   // column i where the query row gained G[i] - R_a[i] columns, that many before the first target
-  // base b placed at or after column i (injectGap, GapAssem.cpp:720-753).  False: a gap length
-  // outside the 16-bit range the reference stores (the literal merge handles that).
+  // base b placed at or after column i (injectGap, GapAssem.cpp:720-753) — or, when the row starts
+  // at or after that column (`salpos >= alpos`, :733-737), added to the row's offset instead.  The
+  // relation "row offset >= column of query base i" never changes under injections, so it is
+  // decided on the pairwise layout.  False: a gap length outside the 16-bit range the reference
+  // stores (the literal merge handles that).
   auto row_layout = [&](const MsaRec& r) {
     build_tseq(q, qlen, run, r, tseq);
     const int tl = (int)tseq.size();
@@ -216,12 +224,17 @@ int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const Ms
     int b = 0;
     long pc = tl > 0 ? r.r_alnstart + ofs[0] : 0;  // column of base b (pairwise: own gaps only)
     extra.clear();
+    shift = 0;
     for (int i : gpos) {
       while (ri < rg.size() && rg[ri].first <= i) rsum += rg[ri++].second;
       const int Ra = (ri > 0 && rg[ri - 1].first == i) ? rg[ri - 1].second : 0;
       const int d = G[(size_t)i] - Ra;
       if (d <= 0) continue;
       const long rc = (long)i + rsum;
+      if (r.r_alnstart >= rc) {  // the row starts at or after the column: its offset moves
+        shift += d;
+        continue;
+      }
       while (b < tl && pc < rc) {
         b++;
         if (b < tl) pc += 1 + ofs[(size_t)b];
@@ -239,16 +252,62 @@ int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const Ms
   };
   for (const MsaRec& r : run.recs)  // decide before anything is printed
     if (!row_layout(r)) return fallback();
-  Printer pr;
-  pr.row(f, qid, (const char*)q, qlen, 0, G.data());
   const uint8_t* cm = comp().c;
-  for (const MsaRec& r : run.recs) {
-    row_layout(r);
-    if (r.reverse) {  // prepSeq reverse-complements the sequence, not its gaps
+  auto prepped = [&](const MsaRec& r) {  // finalize -> prepSeq: the sequence, not its gaps
+    if (r.reverse) {
       std::reverse(tseq.begin(), tseq.end());
       for (char& c : tseq) c = (char)cm[(uint8_t)c];
     }
-    pr.row(f, run.labels.substr(r.lab_off, r.lab_len), tseq.data(), (int)tseq.size(), r.r_alnstart, ofs.data());
+  };
+  if (dbg) {  // -D: refMSA->print(stderr, 'v') (pafreport.cpp:443-446, GapAssem.cpp:1013-1037)
+    // minoffset / length as GSeqAlign keeps them: the smallest row offset, the largest row end
+    long minoff = 0, end = (long)qlen;
+    size_t namew = strlen(qid);
+    for (int32_t g : G) end += g;
+    for (const MsaRec& r : run.recs) {
+      row_layout(r);
+      long e = r.r_alnstart + shift + (long)tseq.size();
+      for (int32_t o : ofs) e += o;
+      minoff = std::min(minoff, (long)r.r_alnstart + shift);
+      end = std::max(end, e);
+      namew = std::max(namew, (size_t)r.lab_len);
+    }
+    const int w = (int)namew;
+    std::string out;
+    auto row = [&](const char* name, size_t nlen, char orient, long offset, const char* seq, int n, const int32_t* o) {
+      out.assign((size_t)w - std::min(nlen, (size_t)w), ' ');
+      out.append(name, nlen);
+      out.push_back(' ');
+      out.push_back(orient);
+      out.push_back(' ');
+      out.append((size_t)std::max(0L, offset - minoff), ' ');
+      for (int k = 0; k < n; k++) {
+        if (o[k] < 0) continue;
+        out.append((size_t)o[k], '-');
+        out.push_back(seq[k]);
+      }
+      out.push_back('\n');
+      fwrite(out.data(), 1, out.size(), dbg);
+    };
+    fprintf(dbg, ">MSA (%d)\n", (int)run.recs.size() + 1);
+    out.assign((size_t)w + 3, ' ');
+    out.append((size_t)(end - minoff), 'v');
+    out.push_back('\n');
+    fwrite(out.data(), 1, out.size(), dbg);
+    row(qid, strlen(qid), '+', 0, (const char*)q, qlen, G.data());
+    for (const MsaRec& r : run.recs) {
+      row_layout(r);
+      prepped(r);
+      row(run.labels.data() + r.lab_off, r.lab_len, r.reverse ? '-' : '+', r.r_alnstart + shift, tseq.data(),
+          (int)tseq.size(), ofs.data());
+    }
+  }
+  Printer pr;
+  pr.row(f, qid, (const char*)q, qlen, 0, G.data());
+  for (const MsaRec& r : run.recs) {
+    row_layout(r);
+    prepped(r);
+    pr.row(f, run.labels.substr(r.lab_off, r.lab_len), tseq.data(), (int)tseq.size(), r.r_alnstart + shift, ofs.data());
   }
   return 0;
 }

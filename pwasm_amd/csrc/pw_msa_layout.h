@@ -43,6 +43,6 @@ struct MsaRun {
 // Write refMSA->writeMSA(f) (GapAssem.cpp:1039-1046) for the run: the query row then every
 // target row in input order, 60 columns per line.  q / qlen: the forward upper-case query.
 // Returns 0, or 1 after printing the reference's message for an error (stderr).
-int write_run_msa(FILE* f, const char* qid, const uint8_t* q, int qlen, const MsaRun& run);
+int write_run_msa(FILE* f, FILE* dbg, const char* qid, const uint8_t* q, int qlen, const MsaRun& run);
 
 }  // namespace pw

@@ -199,7 +199,10 @@ class OffsetWriter:
     any rank ends the run too), the per-line stdout byte counts of the window (one owner per line;
     all-reduce SUM of W int64) exclusive-scanned into file offsets after the previous windows, each
     rank's pwrite of its own items there (pw_batch_write_range), stderr gathered to rank 0 only and
-    written in line order.  Batches are released once their last item is written.  stdout without
+    written in line order.  A batch is released once its last item is written: a rank holds every
+    batch with a line in the current window or a later one (a batch whose lines reach into later
+    windows stays pending until those are written), and each window's collectives make a rank wait
+    for the slowest rank to cover that window.  stdout without
     -o: the file is assembled in a temporary file and rank 0 streams each window out after it."""
 
     BIG = np.iinfo(np.int64).max
@@ -210,6 +213,7 @@ class OffsetWriter:
         self.W = max(1, int(window or os.environ.get("PW_WINDOW_LINES", str(1 << 21))))
         self.nwin = -(-self.n_total // self.W)
         self.j, self.base, self.code, self.done, self.err = 0, 0, 0, False, None
+        self.failed = False  # an input error of some rank, all-reduced: the same on every rank
         self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item], ...] in line order
         self.tmp_out = None
         if out_path is None:  # stdout: assembled in a file, streamed out by rank 0 window by window
@@ -264,7 +268,7 @@ class OffsetWriter:
                 e = next(x for x in errs if x)
                 sys.stderr.write(e.split(": ", 1)[-1] if e.startswith("pw_batch_from_buffer") else e)
                 sys.stderr.flush()
-            self.code, self.done = 1, True
+            self.code, self.done, self.failed = 1, True, True
             return
         lens = np.zeros(hi - lo, dtype=np.int64)
         spans, owner = [], -1
@@ -442,12 +446,25 @@ def main(argv=None) -> int:
             break
         # ---- 3. the windows this rank's lines so far complete: offsets, pwrites, stderr
         writer.advance(int(line_no[cuts[k + 1][2]]) if k + 1 < len(cuts) else n_total)
+        if writer.done:  # the run ended at a window every rank has processed: nothing later is written
+            break
     if th is not None and th.is_alive():
         th.join()
     made.clear()
+    return finish_run(writer, err, gtabs, extra, world, rank, device)
+
+
+def finish_run(writer, err, gtabs, extra, world, rank, device):
+    """The end of main() on every rank: the remaining windows, then (unless an input error ended
+    the run) the per-genome table all-gather and the final barrier.  The early return keys on
+    writer.failed — the error all-reduced over the ranks inside the windows — not on this rank's
+    own `err`, so a rank without lines (or whose batches all read fine) takes the same path as the
+    rank that failed and no collective is left waiting (tests/test_mgpu_cpu.py)."""
+    import torch
+    import torch.distributed as dist
     writer.err = err
     code = writer.close()
-    if err:
+    if writer.failed:
         return code
     if "genome-table" in extra:
         names = list(gtabs.keys())

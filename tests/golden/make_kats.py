@@ -34,6 +34,30 @@ here as a literal.  Derivations (line refs into /root/reference/pafreport.cpp):
                     -> t3.addGap(12,1); t4 to spos 12 (gap at 11) -> t4.addGap(12,1); t5 added.
                   Rows (all offset 0, forward; finalize changes nothing): qa gaps {4:3, 10:1},
                   t3 {6:1, 12:1}, t4 {11:1, 12:1}, t5 {4:3}; printMFasta prints '-' per gap.
+  kat11_debug_msa - kat6 with -D (:443-446 -> GSeqAlign::print(stderr,'v') GapAssem.cpp:1013-1037 ->
+                  printGappedSeq :412-440): ">MSA (4)", a separator of 14 blanks (the "%11s %c " format
+                  of " ", ' ': 11 = the longest row name) and 16 'v' (MSA length), then per row the name
+                  right-aligned to 11, ' ', '+', ' ', the offset in blanks (all 0) and the gapped row.
+  kat13_debug_msa_offsets - -D -w with a self alignment (-D sets verbose: :198-201, :315), a row that
+                  starts inside the query (t2, r_alnstart 9) and a '-' row.  Derivation, qa =
+                  AACCGGTTAACC:  t1 ":4-tt:8" / 4M2D8M: qa.setGap(4,2), GSeqAlign(qa,t1) length 14.
+                  t2 ":3" / 3M at qa 9-12, offset 9: addAlign i=4 d=2 -> omsa.injectGap(rseq,4,2):
+                    alpos 4, t2's offset 9 >= 4 so only its offset moves (:733-737) -> 11; addSeq(t2, 11).
+                  t3 '-' ":3*ct:8" / 12M on RC = GGTTAACCGGTT, offset 12-12 = 0, tseq GGTcAACCGGTT:
+                    i=4 d=2 -> t3.addGap(4,2) (first base at column >= 4).
+                  t4 ":8-g:4" / 8M1D4M: rseq.setGap(8,1); i=4 d=2 -> t4.addGap(4,2); i=8 d=-1 ->
+                    injectGap(qa,8,1) in refMSA: alpos = 8+2 = 10; qa.addGap(8,1); t1 (no gaps) walks to
+                    base 10 -> addGap(10,1); t2's offset 11 >= 10 -> 12; t3 (gap 2 at 4) walks to base 8
+                    -> addGap(8,1); length 15; addSeq(t4, 0).
+                  print: finalize reverse-complements t3's bases, not its gaps (prepSeq :89-101):
+                    AACCGGTTgACC with {4:2, 8:1}; t2 is printed after 12 blanks (offset - minoffset 0),
+                    and writeMSA prints those 12 columns as '-'.
+  kat14_debug_no_w - -D without -w: verbose messages only (the reference then dereferences the NULL
+                  refMSA at :444 — DESIGN.md D7: nothing more is printed here).
+  kat12_*       - -v / -c (:217-240): "Max clipping set to 5 bases", "Percentual max clipping set to
+                  5%" (iround(100*0.05f) = 5), each before the self-alignment message (:315); without
+                  -v neither prints.  -s/-p/-m/-d take a value and are never used (-s's file is never
+                  created, :274).  err_clip_*: -c 0 and -c 100% (:220-225), exit 1.
   err_*         - the reference's error messages (format strings copied from the source
                   lines cited in each case), exit code 1, and report lines printed before it.
 Each case dir holds: q.fa, in.paf, args.json ({"args": [...], "rc": N}), stdout, stderr.
@@ -220,6 +244,39 @@ K10_OUT = (">asm30:0-30+ coverage:100.00 score=20 edit_distance=6\n"
            "D\t11\t4(G)\t[13]:\t11\tACCCGGTTTT\tCCCGGGTTT\t[unknown]\tframe shift GF+:GF+\n")
 
 
+# kat13_debug_msa_offsets (derivation in the module docstring)
+SELF_QA = paf("qa", 12, 0, 12, "+", "qa", 12, 0, 12, 12, 12, 60, "NM:i:0", "AS:i:24", "cg:Z:12M", "cs:Z::12")
+K13 = (SELF_QA +
+       paf("qa", 12, 0, 12, "+", "t1", 200, 100, 114, 12, 14, 60, "NM:i:2", "AS:i:10", "cg:Z:4M2D8M", "cs:Z::4-tt:8") +
+       paf("qa", 12, 9, 12, "+", "t2", 100, 50, 53, 3, 3, 60, "NM:i:0", "AS:i:6", "cg:Z:3M", "cs:Z::3") +
+       paf("qa", 12, 0, 12, "-", "t3", 300, 200, 212, 11, 12, 60, "NM:i:1", "AS:i:20", "cg:Z:12M", "cs:Z::3*ct:8") +
+       paf("qa", 12, 0, 12, "+", "t4", 400, 300, 313, 12, 13, 60, "NM:i:1", "AS:i:20", "cg:Z:8M1D4M", "cs:Z::8-g:4"))
+K13_MSA = (">qa\nAACC--GGTT-AACC\n"
+           ">t1:100-114+\nAACCttGGTT-AACC\n"
+           ">t2:50-53+\n------------ACC\n"
+           ">t3:200-212-\nAACC--GGTT-gACC\n"
+           ">t4:300-313+\nAACC--GGTTgAACC\n")
+K13_ERR = ("Skipping alignment of qry seq to itself.\n"
+           ">MSA (5)\n" +
+           " " * 14 + "v" * 15 + "\n"
+           "         qa + AACC--GGTT-AACC\n"
+           "t1:100-114+ + AACCttGGTT-AACC\n"
+           "  t2:50-53+ + " + " " * 12 + "ACC\n"
+           "t3:200-212- - AACC--GGTT-gACC\n"
+           "t4:300-313+ + AACC--GGTTgAACC\n")
+K11_ERR = (">MSA (4)\n" +
+           " " * 14 + "v" * 16 + "\n"
+           "         qa + AACC---GGTTAA-CC\n"
+           "t3:100-114+ + AACCtt-GGTTAA-CC\n"
+           "t4:100-114+ + AACCgggGGTT-A-CC\n"
+           "t5:100-113+ + AACC---GGTTAAcCC\n")
+
+# kat12_*: -v / -c with a self alignment of the query first
+SELF_CDS = paf("cds", 30, 0, 30, "+", "cds", 30, 0, 30, 30, 30, 60, "NM:i:0", "AS:i:60", "cg:Z:30M", "cs:Z::30")
+SKIP_MSG = "Skipping alignment of qry seq to itself.\n"
+CLIP_PCT_ERR = "Error: invalid percent value (100) for -c option  (must be an integer between 1 and 99)!\n"
+
+
 def line(s):
     return s.rstrip("\n")
 
@@ -235,6 +292,19 @@ CASES = {
     "kat9_tctx_walk_reverse": (FA1, K9, ["-r", "q.fa", "in.paf"], 0, K9_OUT, ""),
     "kat10_general": (FA1, K10, ["-r", "q.fa", "in.paf"], 0, K10_OUT, ""),
     "kat6_msa_w": (FA6, K6, ["-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", ""),
+    "kat11_debug_msa": (FA6, K6, ["-D", "-o", "rep.txt", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "", K11_ERR),
+    "kat13_debug_msa_offsets": (FA6, K13, ["-o", "rep.txt", "-D", "-w", "msa.mfa", "-r", "q.fa", "in.paf"], 0, "",
+                                K13_ERR),
+    "kat14_debug_no_w": (FA3, K3, ["-D", "-r", "q.fa", "in.paf"], 0, K3_OUT, SKIP_MSG + K3_ERR),
+    "kat12_verbose_c": (FA1, SELF_CDS + K1, ["-v", "-c", "5", "-r", "q.fa", "in.paf"], 0, K1_OUT,
+                        "Max clipping set to 5 bases\n" + SKIP_MSG),
+    "kat12_verbose_cpct": (FA1, SELF_CDS + K1, ["-v", "-c5%", "-r", "q.fa", "in.paf"], 0, K1_OUT,
+                           "Percentual max clipping set to 5%\n" + SKIP_MSG),
+    "kat12_quiet_unused_opts": (FA1, SELF_CDS + K1, ["-c", "7", "-s", "sum.txt", "-p", "x", "-m", "y", "-d", "z",
+                                                     "-r", "q.fa", "in.paf"], 0, K1_OUT, ""),
+    "err_clip_zero": (FA1, K1, ["-c", "0", "-r", "q.fa", "in.paf"], 1, "",
+                      "Error: invalid -c <clipmax> (0) option provided (must be a positive integer)!\n"),
+    "err_clip_pct": (FA1, K1, ["-v", "-c", "100%", "-r", "q.fa", "in.paf"], 1, "", CLIP_PCT_ERR),
     "kat5_noncoding": (FA1, K1, ["-N", "-r", "q.fa", "in.paf"], 0,
                        K4_OUT.replace(">cds:0-30--asm1", ">asm1"), ""),
     # pafreport.cpp:551-553 base check; records before the failing one are already reported
@@ -304,9 +374,14 @@ def main():
         if name == "kat1_outfile":
             spec["outfile"] = "out.txt"
             spec["outfile_expected"] = K1_OUT
-        if name == "kat6_msa_w":
+        if name in ("kat6_msa_w", "kat11_debug_msa"):
             spec["outfile"] = "msa.mfa"
             spec["outfile_expected"] = K6_MSA
+        if name == "kat13_debug_msa_offsets":
+            spec["outfile"] = "msa.mfa"
+            spec["outfile_expected"] = K13_MSA
+        if name == "kat12_quiet_unused_opts":
+            spec["absent"] = ["sum.txt", "x", "y", "z"]
         with open(os.path.join(d, "args.json"), "w") as f:
             json.dump(spec, f, indent=1)
         with open(os.path.join(d, "stdout"), "w") as f:

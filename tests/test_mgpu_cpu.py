@@ -194,3 +194,48 @@ def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window):
     got = sorted(x for v in res.values() for x in v[2])
     lines = open(paf, "rb").read().replace(b"\r\n", b"\n").split(b"\n")[:-1]
     assert got == [k for k, ln in enumerate(lines) if not ln.startswith(b"#")]
+
+
+def _finish_rank(rank, world, port, out_path, gt_path, errf, fail_rank, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
+    os.dup2(fd, 2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = mgpu.OffsetWriter(5, out_path, world, rank, "cpu")
+        # fail_rank could not read its batch (e.g. an unreadable -r FASTA); every other rank got no
+        # lines at all (lines go to the owner of their target genome)
+        err = "pw_batch_from_buffer: Error: invalid FASTA file q.fa !\n" if rank == fail_rank else None
+        code = mgpu.finish_run(w, err, {}, {"genome-table": gt_path}, world, rank, "cpu")
+        q.put((rank, code, w.failed))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank", [(2, 0), (2, 1), (3, 2), (2, None)])
+def test_input_error_on_one_rank_ends_every_rank(tmp_path, world, fail_rank):
+    """an input error that only some ranks hit must end the run on every rank (exit 1,
+    the message once, from rank 0) — the lineless ranks may not wait in the genome-table gather or
+    the final barrier for ranks that already returned."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    gt = tmp_path / "gt.tsv"
+    ps = [ctx.Process(target=_finish_rank, args=(r, world, port, str(tmp_path / "o.txt"), str(gt),
+                                                 str(tmp_path / f"e{r}"), fail_rank, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {r: (c, f) for r, c, f in (q.get(timeout=90) for _ in range(world))}
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = 0 if fail_rank is None else 1
+    assert {c for c, _ in res.values()} == {want}
+    assert {f for _, f in res.values()} == {fail_rank is not None}
+    noise = (b"/opt/amdgpu/", b"[W", b"[Gloo]", b"[I")
+    err0 = b"".join(ln for ln in open(tmp_path / "e0", "rb").read().splitlines(keepends=True)
+                    if not ln.startswith(noise))
+    assert err0 == (b"Error: invalid FASTA file q.fa !\n" if fail_rank is not None else b"")
+    assert gt.exists() == (fail_rank is None)

@@ -26,6 +26,8 @@ def run_case(binary, case, tmp_path):
     assert err == exp_err
     if "outfile" in spec:
         assert open(dst / spec["outfile"]).read() == spec["outfile_expected"]
+    for name in spec.get("absent", []):  # option values the reference never opens (-s, -p, -m, -d)
+        assert not (dst / name).exists(), name
 
 
 @pytest.mark.parametrize("case", CASES)
