@@ -89,8 +89,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:  # PW_DIST_BACKEND=gloo: rehearsal with several ranks on one GPU (RCCL refuses that)
-        dist.init_process_group(backend=os.environ.get("PW_DIST_BACKEND",
-                                                       "nccl" if torch.cuda.is_available() else "gloo"))
+        # (c10d / gloo announce their connections on fd 1: keep stdout to the one JSON line)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(backend=os.environ.get("PW_DIST_BACKEND",
+                                                           "nccl" if torch.cuda.is_available() else "gloo"))
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     local = local % max(torch.cuda.device_count(), 1)
     dev_name = f"cuda:{local}"
     torch.cuda.set_device(local)

@@ -89,6 +89,12 @@ def make(name):
     elif name.startswith("sy"):  # slot_rows with N workgroups per row (product: 2048 / rows, <= 64)
         s = sub(s, "const unsigned sy = a->n_rows >= 2048 ? 1u : (2048u / a->n_rows < 64u ? 2048u / a->n_rows : 64u);",
                 f"const unsigned sy = {int(name[2:])}u;")
+    elif name == "idealsrc":  # window reads at the gap-free offsets (the rotation's conflict-free pattern)
+        s = sub(s, "            const int src = base0 + 4 * q - (q == 0 ? 0 : __popc(rb & ((1u << (4 * q)) - 1u))) - (q >= qwrap ? wrapc : 0);",
+                "            const int src = 32 * lane + 4 * ((q + rot) & 7) + (base0 & 0);")
+    elif name == "nogather":  # no window reads at all (the group bytes are a constant)
+        s = sub(s, """            const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);""",
+                """            const uint32_t s4 = 0x41434754u + (uint32_t)(src & 0) + (uint32_t)(p == nullptr);""")
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout
