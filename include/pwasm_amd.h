@@ -123,6 +123,11 @@ typedef struct pw_report_args {
                                <= PW_BLOCK_OPS lets the pass skip that pre-pass. */
   uint32_t n_short;         /* records of at most 64 ops, or 0 = unknown: when they are most of the
                                batch, index decoding takes two records per wavefront */
+  uint32_t hot_pbits;       /* 0, or P in 1..31 when every query is shorter than 2^P bases and every
+                               query index (desc[].ref & PW_REF_QMASK) < 2^(32 - P): the pass then
+                               keeps 16 instead of 32 bytes per event between its kernels (an event
+                               that violates it ends its record with PW_REC_LAYOUT) */
+  uint32_t pad;
 } pw_report_args;
 #define PW_BLOCK_OPS 2048
 
@@ -130,6 +135,11 @@ typedef struct pw_report_args {
  * the page area plus an arena of text_bound bytes (sum of pw_cs_totals.text_bound). */
 uint64_t pw_report_page_count(uint64_t n_ev_slots);
 uint64_t pw_report_text_bytes(uint64_t n_ev_slots, uint64_t text_bound);
+
+/* pw_report_args.hot_pbits for queries of at most max_qlen bases and n_queries query indices:
+ * the smallest P with max_qlen < 2^P, when the query index fits the other 32 - P bits, else 0
+ * (32-byte event records). */
+uint32_t pw_report_hot_pbits(uint64_t max_qlen, uint64_t n_queries);
 
 /* Device workspace pw_report_events needs for a batch of n_alns records with n_events_max event
  * slots (pw_cs_totals.n_events_max summed over the batch; pw_batch_view.n_events_max). */

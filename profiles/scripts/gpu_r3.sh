@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: the GPU test suite, then the cfg2 and cfg4 bench lines.
-# Usage: bash tools/gpu_r3.sh <tag> [extra pytest args...]
+# Usage: bash profiles/scripts/gpu_r3.sh <tag> [extra pytest args...]
 set -uo pipefail
 TAG=${1:-r3}
 shift || true

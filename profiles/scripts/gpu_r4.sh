@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: the GPU test suite, the default bench line (cfg2 + the cfg5 sub-object), then the
 # large configs at HEAD (tools/gpu_big.sh: full cfg3, cfg4 >= 1,024 records, kernel traces).
-# Usage: bash tools/gpu_r4.sh <tag> [cfg4 scale] [skip-tests]
+# Usage: bash profiles/scripts/gpu_r4.sh <tag> [cfg4 scale] [skip-tests]
 set -uo pipefail
 TAG=${1:-r4}
 S4=${2:-0.11}

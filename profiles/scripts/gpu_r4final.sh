@@ -2,7 +2,7 @@
 # On the GPU box, end of round 4: the GPU test suite, the default bench line (cfg2 + cfg5), the cfg2
 # profile (kernel trace + PMC passes, profiles/run_prof.sh), then the large configs
 # (tools/gpu_big.sh: full cfg3, cfg4 at the given scale, kernel traces).
-# Usage: bash tools/gpu_r4final.sh <tag> [cfg4 scale] [skip-tests]
+# Usage: bash profiles/scripts/gpu_r4final.sh <tag> [cfg4 scale] [skip-tests]
 set -uo pipefail
 TAG=${1:-r4f}
 S4=${2:-0.11}

@@ -22,15 +22,23 @@ import sys
 N_CU = 256
 
 
+def kname(n):
+    """pw::render_kernel from "void pw::render_kernel<true>(pw_report_args, pw::Work)" (templates)."""
+    n = n.split("(")[0]
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("<")[0]
+
+
 def main(src, out, bench_args=""):
     stats = list(csv.DictReader(open(f"{src}/trace/run_kernel_stats.csv")))
     pmc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0]
+            k = kname(r["Kernel_Name"])
             pmc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     per = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in pmc.items()}
-    kern = [{"name": s["Name"].split("(")[0], "calls": int(s["Calls"]), "avg_us": float(s["AverageNs"]) / 1000,
+    kern = [{"name": kname(s["Name"]), "calls": int(s["Calls"]), "avg_us": float(s["AverageNs"]) / 1000,
              "pct": float(s["Percentage"])} for s in stats]
     pw = [k for k in kern if k["name"].startswith("pw::")]
     fetch = sum(per[k].get("FETCH_SIZE", 0) for k in per) * 1024

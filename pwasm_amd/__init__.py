@@ -69,7 +69,7 @@ class ReportArgs(ctypes.Structure):
                 ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
                 ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p), ("max_rec_ops", ctypes.c_uint32),
-                ("n_short", ctypes.c_uint32)]
+                ("n_short", ctypes.c_uint32), ("hot_pbits", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class CsTotals(ctypes.Structure):
@@ -152,6 +152,7 @@ _SIGS = {
     "pw_report_page_count": (ctypes.c_uint64, [ctypes.c_uint64]),
     "pw_report_text_bytes": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     "pw_report_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+    "pw_report_hot_pbits": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint64]),
     "pw_batch_write_items": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_char_p]),
     "pw_batch_free": (None, [ctypes.c_void_p]),
@@ -461,6 +462,10 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     a.pages = dev["pages"].data_ptr()
     a.max_rec_ops = batch.max_rec_ops()
     a.n_short = 0 if _env_flag("PW_NO_PAIRS") else batch.n_short()
+    # 16-byte event records when the query positions / indices fit (PW_HOT32=1: 32-byte ones)
+    ql = batch.array("qlen")
+    a.hot_pbits = 0 if _env_flag("PW_HOT32") else int(lib().pw_report_hot_pbits(int(ql.max()) if ql.size else 0,
+                                                                               int(v.n_queries)))
     return a
 
 

@@ -286,6 +286,11 @@ struct QueryDb {
   std::unordered_map<std::string_view, int> index;  // first record of each id (built after load)
   std::vector<uint8_t> acgt;  // per query: all bases in {A,C,G,T}
   bool all_acgt(int qi) const { return acgt[qi] != 0; }
+  uint64_t max_len() const {
+    int32_t m = 0;
+    for (int32_t l : len) m = l > m ? l : m;
+    return (uint64_t)m;
+  }
   static bool is_acgt_byte(uint8_t c) { return c == 'A' || c == 'C' || c == 'G' || c == 'T'; }
   // Each sequence starts 16-byte aligned and is followed by >= 64 zero bytes: the kernels'
   // 16-byte-aligned LDS windows then read NUL past the end of a query, as the reference reads
@@ -1396,6 +1401,9 @@ struct Device {
       a.n_short += d.n_ops <= 64 ? 1u : 0u;
     }
     if (getenv("PW_NO_PAIRS") && atoi(getenv("PW_NO_PAIRS")) != 0) a.n_short = 0;  // (tests: one record per wave)
+    // 16-byte event records when the query positions / indices fit (PW_HOT32=1 keeps 32-byte ones)
+    a.hot_pbits = (getenv("PW_HOT32") && atoi(getenv("PW_HOT32")) != 0) ? 0u : pw_report_hot_pbits(q.max_len(), q.len.size());
+    a.pad = 0;
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
       return false;

@@ -86,11 +86,15 @@ constexpr int kIndexOcc = 5;    // index_kernel: waves per SIMD the register bud
 constexpr int kPairOcc = 4;     // index_pair_kernel: (two records per wave hold more live state: 128 VGPRs)
 constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)
 
-// Render record of one event (index_kernel -> render_kernel), 32 bytes.
+// Render record of one event (index_kernel -> render_kernel, tctx_kernel, fixup_kernel), decoded.
 //   fn: type (31-30) | reverse (29) | fast tctx (28) | first line of its record (27) |
 //       last line (26) | ll (25-23) | rl (22-20) | A/C/G/T only (19) | evtbases length (18-0,
 //       saturated)
 //   l0, l1: the event's first 8 literal bytes (SUB: target,query pairs; INS: inserted bases)
+// In memory it is 32 bytes {fn, qp, tloc, ls | qb, L, l0, l1}, or — when the batch's query
+// positions and indices fit (pw_report_args.hot_pbits = P != 0) — 16 bytes {fn, qi << P | qp, tloc,
+// ls}: the query's start and length then come from qoff / qlen, the literal bytes from lits (loads
+// the readers issue a stage before they need them).  fn is word 0 of either.
 struct Hot {
   uint32_t qb;    // forward query start in qseq, in 16-byte units (qoff is 16-byte aligned)
   int32_t L;      // query length
@@ -1425,7 +1429,9 @@ struct Work {
   uint32_t* ctr;
   unsigned long long* arena_used;
   uint64_t* rec_mod;
-  Hot* hot;
+  uint32_t* hotw;     // event records: slot s at word s << hot_sh (fn = that word)
+  uint32_t hot_sh;    // 3 (32-byte records) or 2 (16-byte records: hot_pbits != 0)
+  uint32_t hot_pbits;
   Cold* cold;
   uint8_t* tx;
   uint8_t* sflag;
@@ -1481,7 +1487,9 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->ctr = reinterpret_cast<uint32_t*>(base);
     w->arena_used = reinterpret_cast<unsigned long long*>(base + 16);
     w->rec_mod = reinterpret_cast<uint64_t*>(base + o_rm);
-    w->hot = reinterpret_cast<Hot*>(base + o_hot);
+    w->hotw = reinterpret_cast<uint32_t*>(base + o_hot);
+    w->hot_sh = 3;
+    w->hot_pbits = 0;
     w->cold = reinterpret_cast<Cold*>(base + o_cold);
     w->tx = base + o_tx;
     w->sflag = base + o_sflag;
@@ -1498,6 +1506,53 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
   }
   return o;
+}
+
+// the fn word of slot s (empty slots, last-line flags)
+__device__ __forceinline__ uint32_t& hot_fn(const Work& W, uint64_t s) { return W.hotw[s << W.hot_sh]; }
+// index_kernel's store of an event's record (qi: its query index)
+__device__ __forceinline__ void store_hot(const Work& W, uint64_t s, const Hot& h, uint32_t qi) {
+  v4u* p = reinterpret_cast<v4u*>(W.hotw + (s << W.hot_sh));
+  if (W.hot_pbits) {
+    p[0] = (v4u){h.fn, qi << W.hot_pbits | (uint32_t)h.qp, (uint32_t)h.tloc, h.ls};
+  } else {
+    p[0] = (v4u){h.fn, (uint32_t)h.qp, (uint32_t)h.tloc, h.ls};
+    p[1] = (v4u){h.qb, (uint32_t)h.L, h.l0, h.l1};
+  }
+}
+// a 16-byte record's query index / query position (0 for empty slots, whose other words are stale)
+__device__ __forceinline__ uint32_t hot16_qi(const Work& W, uint32_t fn, uint32_t w1) {
+  return fn == kNoEv ? 0u : w1 >> W.hot_pbits;
+}
+__device__ __forceinline__ uint32_t hot16_qp(const Work& W, uint32_t w1) { return w1 & ((1u << W.hot_pbits) - 1u); }
+// the first 8 literal bytes from ls, given the three dwords from ls & ~3
+__device__ __forceinline__ void lit8(uint32_t ls, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t& l0, uint32_t& l1) {
+  l0 = __builtin_amdgcn_alignbyte(d1, d0, ls & 3u);
+  l1 = __builtin_amdgcn_alignbyte(d2, d1, ls & 3u);
+}
+// the whole record of slot s with its dependent loads (tctx_kernel, fixup_kernel)
+__device__ __forceinline__ Hot load_hot_full(const pw_report_args& A, const Work& W, uint64_t s) {
+  const v4u a = reinterpret_cast<const v4u*>(W.hotw + (s << W.hot_sh))[0];
+  Hot h;
+  h.fn = a.x;
+  h.tloc = (int32_t)a.z;
+  h.ls = a.x == kNoEv ? 0u : a.w;
+  if (W.hot_pbits) {
+    const uint32_t qi = hot16_qi(W, a.x, a.y);
+    h.qp = (int32_t)hot16_qp(W, a.y);
+    h.qb = (uint32_t)(A.qoff[qi] >> 4);
+    h.L = A.qlen[qi];
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + (h.ls >> 2);
+    lit8(h.ls, l32[0], l32[1], l32[2], h.l0, h.l1);
+  } else {
+    const v4u b = reinterpret_cast<const v4u*>(W.hotw + (s << W.hot_sh))[1];
+    h.qp = (int32_t)a.y;
+    h.qb = b.x;
+    h.L = (int32_t)b.y;
+    h.l0 = b.z;
+    h.l1 = b.w;
+  }
+  return h;
 }
 
 // (every caller runs 256 threads: each thread issues its three loads before any store, so the
@@ -1670,6 +1725,8 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   bool prev_sub = B.prev_sub;
   uint32_t ev = B.ev0, ev_last_seg = 0;  // events created; by the last segment processed
   int err = layout_ok ? PW_REC_OK : PW_REC_LAYOUT, err_a = 0, err_b = 0, err_c = 0;
+  const uint32_t qi = d.ref & PW_REF_QMASK;
+  bool bad_hot = false;
 
   for (uint32_t sb = B.sb0; layout_ok && sb < B.sb1; sb += kSegOps) {
     const uint32_t nseg = (B.sb1 - sb) < (uint32_t)kSegOps ? (B.sb1 - sb) : (uint32_t)kSegOps;
@@ -1792,7 +1849,6 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       if (k == 1 && !two) continue;
       const uint32_t idx = 64 * k + lane;
       const uint32_t typ = wd[k] >> 30;
-      bool slow = false;
       uint64_t s = 0;
       TGeom g;
       uint32_t n = 0;
@@ -1840,9 +1896,17 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
           hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, (d.ref & PW_REF_ACGT) != 0, n);
           hh.l0 = hl0[k];
           hh.l1 = hl1[k];
-          W.hot[s] = hh;
+          if (W.hot_pbits && (((uint32_t)hh.qp >> W.hot_pbits) | (qi >> (32 - W.hot_pbits)))) {  // (hot_pbits contract)
+            hh.fn = kNoEv;
+            bad_hot = true;
+          }
+          store_hot(W, s, hh, qi);
           W.sflag[s] = fast ? (uint8_t)0 : (uint8_t)1;  // (every slot's flag is written: no memset)
-          if (kidx == 0 || lastc || n >= kNBig) {  // only the first / last line and saturated lengths read it
+          // the Cold record: read for the first / last line, saturated lengths and — the walk's
+          // start (record, head op, its query / target position) — by tctx_kernel for target
+          // contexts that are not a plain query copy (another event within 5 bases, an S run, a
+          // long insertion; flagged above); one 16-byte store shared by all of them
+          if (kidx == 0 || lastc || n >= kNBig || !fast) {
             Cold cd;
             cd.ai = ai;
             cd.j = j;
@@ -1850,16 +1914,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
             cd.ts = ts[k];
             W.cold[s] = cd;
           }
-          slow = !fast;
         }
-      }
-      // ---- target contexts that are not a plain query copy (another event within 5 bases,
-      // an S run, a long insertion) are rendered by tctx_kernel: flag the slot and leave the
-      // walk's start (head op, its query / target position, record geometry) in its tx record
-      if (slow) {
-        v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
-        dtx[0] = (v4u){d.op_begin, sb + (uint32_t)(64 * k + lane), n_ops, (uint32_t)qs[k]};
-        dtx[1] = (v4u){(uint32_t)ts[k], (uint32_t)T, (uint32_t)d.offset, 0u};
       }
     }
     ev += nev;
@@ -1870,6 +1925,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     lc += ltot;
     wave_sync();
   }
+  if (__ballot(bad_hot) != 0 && err == PW_REC_OK) err = PW_REC_LAYOUT;
   if (B.blocked) {
     // slots nobody writes: this block's after a mismatch, and (last block) those past the
     // record's last event; creation index e sits in slot evb + e ('+') or evb + nmax - 1 - e ('-')
@@ -1877,14 +1933,14 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     if (f1 > f0) {
       const uint64_t a0 = rev ? evb + nmax - f1 : evb + f0, a1 = rev ? evb + nmax - f0 : evb + f1;
       for (uint64_t s = a0 + lane; s < a1; s += kWave) {
-        W.hot[s].fn = kNoEv;
+        hot_fn(W, s) = kNoEv;
         W.sflag[s] = 0;
       }
     }
     if (B.sb1 == n_ops && B.tot < nmax) {
       const uint64_t a0 = rev ? evb : evb + B.tot, a1 = rev ? evb + nmax - B.tot : evb + nmax;
       for (uint64_t s = a0 + lane; s < a1; s += kWave) {
-        W.hot[s].fn = kNoEv;
+        hot_fn(W, s) = kNoEv;
         W.sflag[s] = 0;
       }
     }
@@ -1910,7 +1966,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   }
   if (!layout_ok && pre.ev_next >= evb && pre.ev_next <= A.n_ev_slots)  // (contract violation: no events)
     for (uint64_t s = evb + lane; s < pre.ev_next; s += kWave) {
-      W.hot[s].fn = kNoEv;
+      hot_fn(W, s) = kNoEv;
       W.sflag[s] = 0;
     }
   const bool ev_over = ev > nmax;
@@ -1921,7 +1977,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   // empty slots: merged '*' runs, or everything after a failure
   const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;  // (none if !layout_ok)
   for (uint64_t s = h0 + lane; s < h1; s += kWave) {
-    W.hot[s].fn = kNoEv;
+    hot_fn(W, s) = kNoEv;
     W.sflag[s] = 0;
   }
   // the last created event was flagged when written unless the last segment had no event head
@@ -1929,7 +1985,7 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
   if (lane == 0 && ev > 0 && err == PW_REC_OK && (ev_last_seg == 0 || ev_over)) {
     const uint64_t s_last = rev ? evb + nmax - ev : evb + ev - 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's store of that record first
-    atomicOr(&W.hot[s_last].fn, rev ? 1u << 27 : 1u << 26);
+    atomicOr(&hot_fn(W, s_last), rev ? 1u << 27 : 1u << 26);
     W.cold[s_last].ai = ai;
   }
   if (lane == 0) {
@@ -1969,7 +2025,7 @@ __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
   if (blockIdx.x == 0)
     for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) {
-      W.hot[s].fn = kNoEv;
+      hot_fn(W, s) = kNoEv;
       W.sflag[s] = 0;
     }
 }
@@ -2155,6 +2211,7 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
   }
   // ---- events (none after a mismatch: the record ends at its first one)
   const bool ok = bad_idx == INT_MAX;
+  bool bad_hot = false;
   const uint32_t n0 = (uint32_t)__popc(hm[0]);
   const uint32_t nev = ok ? n0 + (uint32_t)__popc(hm[1]) : 0u;
   const uint32_t lt = (1u << hl) - 1u;
@@ -2194,9 +2251,14 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
         hh.fn = hot_fn(typ, rev, fast, first, last, fast ? g.ll : 0, fast ? g.rl : 0, (d.ref & PW_REF_ACGT) != 0, n);
         hh.l0 = hl0[k];
         hh.l1 = hl1[k];
-        W.hot[s] = hh;
+        const uint32_t qi = d.ref & PW_REF_QMASK;
+        if (W.hot_pbits && (((uint32_t)hh.qp >> W.hot_pbits) | (qi >> (32 - W.hot_pbits)))) {  // (hot_pbits contract)
+          hh.fn = kNoEv;
+          bad_hot = true;
+        }
+        store_hot(W, s, hh, qi);
         W.sflag[s] = fast ? (uint8_t)0 : (uint8_t)1;
-        if (kidx == 0 || lastc || n >= kNBig) {
+        if (kidx == 0 || lastc || n >= kNBig || !fast) {  // (and tctx_kernel's walk start)
           Cold cd;
           cd.ai = ai;
           cd.j = idx;
@@ -2204,16 +2266,12 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
           cd.ts = ts[k];
           W.cold[s] = cd;
         }
-        if (!fast) {  // tctx_kernel's walk start
-          v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
-          dtx[0] = (v4u){d.op_begin, idx, n_ops, (uint32_t)qs[k]};
-          dtx[1] = (v4u){(uint32_t)ts[k], (uint32_t)T, (uint32_t)d.offset, 0u};
-        }
       }
     }
   }
   // ---- empty slots, results
   int err = !layout_ok ? PW_REC_LAYOUT : (ok ? PW_REC_OK : PW_REC_MISMATCH);
+  if (half_bits(__ballot(bad_hot), lane) != 0u && err == PW_REC_OK) err = PW_REC_LAYOUT;
   uint32_t ev = nev;
   if (ev > nmax) {  // host event bound violated (cannot happen: every head is a counted op)
     err = PW_REC_OVERFLOW;
@@ -2223,13 +2281,13 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
     if (!layout_ok) {
       if (P.ev_next >= evb && P.ev_next <= A.n_ev_slots)
         for (uint64_t s = evb + (uint64_t)hl; s < P.ev_next; s += 32) {
-          W.hot[s].fn = kNoEv;
+          hot_fn(W, s) = kNoEv;
           W.sflag[s] = 0;
         }
     } else {
       const uint64_t h0 = rev ? evb : evb + ev, h1 = rev ? evb + nmax - ev : evb + nmax;
       for (uint64_t s = h0 + (uint64_t)hl; s < h1; s += 32) {
-        W.hot[s].fn = kNoEv;
+        hot_fn(W, s) = kNoEv;
         W.sflag[s] = 0;
       }
     }
@@ -2389,38 +2447,70 @@ __device__ __noinline__ uint32_t rec_of_slot(const pw_aln_desc* desc, uint32_t n
 }
 
 
+// the raw record of chunk c's lane (the second half only for 32-byte records)
+template <bool kH16>
 struct HotRaw {
   v4u a, b;
 };
-__device__ __forceinline__ HotRaw load_hot(const Work& W, uint64_t c, int lane) {
+template <>
+struct HotRaw<true> {
+  v4u a;
+};
+template <bool kH16>
+__device__ __forceinline__ HotRaw<kH16> load_hot(const Work& W, uint64_t c, int lane) {
   const uint64_t cc = c < W.n_chunks ? c : W.n_chunks - 1;  // (W.n_chunks >= 1 when render runs)
-  const v4u* p = reinterpret_cast<const v4u*>(W.hot + cc * kWave + lane);
-  HotRaw r;
+  const v4u* p = reinterpret_cast<const v4u*>(W.hotw) + ((cc * kWave + (uint64_t)lane) << (kH16 ? 0 : 1));
+  HotRaw<kH16> r;
   r.a = p[0];
-  r.b = p[1];
+  if constexpr (!kH16) r.b = p[1];
   return r;
 }
+// a 16-byte record's query: start (16-byte units) and length, loaded a stage ahead of its use
+struct QInfo {
+  uint32_t qb;
+  int32_t L;
+};
+__device__ __forceinline__ QInfo load_qinfo(const pw_report_args& A, const Work& W, const HotRaw<true>& r) {
+  const uint32_t qi = hot16_qi(W, r.a.x, r.a.y);
+  QInfo q;
+  q.qb = (uint32_t)(A.qoff[qi] >> 4);
+  q.L = A.qlen[qi];
+  return q;
+}
+__device__ __forceinline__ void pin(QInfo& q) { asm volatile("" : "+v"(q.qb), "+v"(q.L)); }
 // The record is copied out of the load's registers here, before the next prefetch is issued (an
 // explicit move into other registers, ordered as memory): left to hipcc, the copy sinks to the
 // loop latch, after the next load, whose result then needs other registers and a move of its own
-// at the latch — which waits for that load and exposes the prefetch's whole latency.
-__device__ __forceinline__ Hot decode_hot(const HotRaw& r, bool valid) {
+// at the latch — which waits for that load and exposes the prefetch's whole latency.  (16-byte
+// records: l0 / l1 are filled from the literal words render_pre loads, once they are in.)
+template <bool kH16>
+__device__ __forceinline__ Hot decode_hot(const Work& W, const HotRaw<kH16>& r, const QInfo& q, bool valid) {
   Hot h;
-  uint32_t qb, L, qp, tl, ls, fn, l0, l1;
-  asm volatile(
-      "v_mov_b32 %0, %8\n\tv_mov_b32 %1, %9\n\tv_mov_b32 %2, %10\n\tv_mov_b32 %3, %11\n\t"
-      "v_mov_b32 %4, %12\n\tv_mov_b32 %5, %13\n\tv_mov_b32 %6, %14\n\tv_mov_b32 %7, %15"
-      : "=&v"(qb), "=&v"(L), "=&v"(qp), "=&v"(tl), "=&v"(ls), "=&v"(fn), "=&v"(l0), "=&v"(l1)
-      : "v"(r.a.x), "v"(r.a.y), "v"(r.a.z), "v"(r.a.w), "v"(r.b.x), "v"(r.b.y), "v"(r.b.z), "v"(r.b.w)
-      : "memory");
-  h.qb = qb;
-  h.L = (int32_t)L;
-  h.qp = (int32_t)qp;
+  uint32_t fn, qp, tl, w3;
+  asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
+               : "=&v"(fn), "=&v"(qp), "=&v"(tl), "=&v"(w3)
+               : "v"(r.a.x), "v"(r.a.y), "v"(r.a.z), "v"(r.a.w)
+               : "memory");
   h.tloc = (int32_t)tl;
-  h.ls = ls;
+  h.ls = fn == kNoEv ? 0u : w3;
+  if constexpr (kH16) {
+    h.qp = (int32_t)hot16_qp(W, qp);
+    h.qb = q.qb;
+    h.L = q.L;
+    h.l0 = h.l1 = 0u;
+  } else {
+    uint32_t qb, L, l0, l1;
+    asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
+                 : "=&v"(qb), "=&v"(L), "=&v"(l0), "=&v"(l1)
+                 : "v"(r.b.x), "v"(r.b.y), "v"(r.b.z), "v"(r.b.w)
+                 : "memory");
+    h.qp = (int32_t)qp;
+    h.qb = qb;
+    h.L = (int32_t)L;
+    h.l0 = l0;
+    h.l1 = l1;
+  }
   h.fn = valid ? fn : kNoEv;
-  h.l0 = l0;
-  h.l1 = l1;
   return h;
 }
 
@@ -2436,9 +2526,16 @@ struct RenderPre {
   int qlo;            // forward position of q[0]
   int n;              // evtbases length (resolved when the Hot field saturates)
   bool ns_ok;
+  uint32_t lw[3];     // 16-byte records: the literal words from ls & ~3 (the event's first 8 literal bytes)
 };
+template <bool kH16>
 __device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& W, const Hot& h, uint64_t s, bool skip,
                                            RenderPre& p) {
+  if constexpr (kH16) {
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + (h.ls >> 2);
+#pragma unroll
+    for (int q = 0; q < 3; q++) p.lw[q] = l32[q];
+  }
   const bool ev = h.fn != kNoEv;
   const uint32_t typ = h.fn >> 30;
   const bool rev = (h.fn >> 29) & 1u;
@@ -2489,6 +2586,7 @@ __device__ __forceinline__ void render_pre(const pw_report_args& A, const Work& 
   p.ns_raw = (uint32_t)*nsp;
 }
 // the prefetched registers, first touched here
+template <bool kH16>
 __device__ __forceinline__ void render_pre_ready(RenderPre& p) {
 #pragma unroll
   for (int q = 0; q < kQWin / 16; q++) pin(p.q[q]);
@@ -2496,12 +2594,17 @@ __device__ __forceinline__ void render_pre_ready(RenderPre& p) {
   pin(p.t1);
   pin(p.ai);
   pin(p.ns_raw);
+  if constexpr (kH16) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) pin(p.lw[q]);
+  }
 }
 
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
 // inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
 // chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).  Hot records are loaded
 // two chunks ahead, the rest of a lane's inputs one chunk ahead (render_pre).
+template <bool kH16>
 __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) RenderWave rw[kWaves];
@@ -2517,10 +2620,16 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
 
   uint64_t c = (uint64_t)blockIdx.x * kWaves + wv;
   if (c >= W.n_chunks) return;
-  Hot h = decode_hot(load_hot(W, c, lane), true);
-  HotRaw hn = load_hot(W, c + nw, lane);
+  Hot h;
+  QInfo qn = {0u, 0};
+  {
+    const HotRaw<kH16> h0 = load_hot<kH16>(W, c, lane);
+    if constexpr (kH16) qn = load_qinfo(A, W, h0);
+    h = decode_hot<kH16>(W, h0, qn, true);
+  }
+  HotRaw<kH16> hn = load_hot<kH16>(W, c + nw, lane);
   RenderPre pre;
-  render_pre(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
+  render_pre<kH16>(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
   {  // (six dropped stores: the loop is entered with the same count of memory operations after the
      // render_pre loads as each iteration leaves — hipcc's wait at the loop head takes the smaller)
     const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc((void*)A.text, (short)0, 0, 0x00020000);
@@ -2530,7 +2639,13 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
   for (; c < W.n_chunks; c += nw) {
     const uint64_t s = c * kWave + (uint64_t)lane;
     const bool act = h.fn != kNoEv;
-    render_pre_ready(pre);
+    render_pre_ready<kH16>(pre);
+    if constexpr (kH16) {
+      // the next chunk's query starts / lengths (its records came in with this chunk's inputs),
+      // consumed when it is decoded after this chunk's lines; this chunk's first literal bytes
+      qn = load_qinfo(A, W, hn);
+      lit8(h.ls, pre.lw[0], pre.lw[1], pre.lw[2], h.l0, h.l1);
+    }
 #pragma unroll
     for (int q = 0; q < kQWin / 16; q++) {
       *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
@@ -2624,9 +2739,10 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     const uint32_t fn_cur = h.fn;
     const uint32_t ai_cur = pre.ai;
     // the next chunk's inputs load behind this one's output
-    h = decode_hot(hn, c + nw < W.n_chunks);
-    hn = load_hot(W, c + 2 * nw, lane);
-    render_pre(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);
+    if constexpr (kH16) pin(qn);
+    h = decode_hot<kH16>(W, hn, qn, c + nw < W.n_chunks);
+    hn = load_hot<kH16>(W, c + 2 * nw, lane);
+    render_pre<kH16>(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);
     const uint32_t incl = wave_incl_scan((uint32_t)linelen, lane);
     const uint32_t B = wave_last(incl);
     const uint32_t my_off = incl - (uint32_t)linelen;
@@ -2805,20 +2921,31 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
   auto batch = [&](uint32_t nb) {
     if ((uint32_t)lane < nb) {
       const uint64_t s = w->list[lane];
-      const Hot h = W.hot[s];
-      const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
-      const v4u p0 = tp4[0], p1 = tp4[1];  // op_begin, j, n_ops, qs | ts, T, offset (index_kernel)
+      const Hot h = load_hot_full(A, W, s);
+      const Cold cd = W.cold[s];  // the walk's start: record, head op, query / target position (index_kernel)
       Rec r;
-      r.ops = A.ops + p0.x;
-      r.lits = A.lits;
       r.R = A.qseq + ((uint64_t)h.qb << 4);
       r.L = h.L;
+      r.rev = (h.fn >> 29) & 1u;
+      // forward query bytes of the context: [fc - 5, fc + n + 5) for a '+' record, [fc - n - 5,
+      // fc + 5] for a '-' record (n <= 12 unless abbreviated), fc = the event's forward position —
+      // issued before the record's descriptor is read (they depend on the Hot record only)
+      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;
+      int x0 = fc - (r.rev ? kTcQ / 2 : 8);
+      if (x0 < 0) x0 = 0;
+      const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
+      const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
+      v4u qv[kTcQ / 16];
+#pragma unroll
+      for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
+      const pw_aln_desc d = A.desc[cd.ai];
+      r.ops = A.ops + d.op_begin;
+      r.lits = A.lits;
       r.NS = nullptr;
       r.tab = tp;
-      r.offset = (int)p1.z;
-      r.T = (int)p1.y;
-      r.n_ops = p0.z;
-      r.rev = (h.fn >> 29) & 1u;
+      r.offset = d.offset;
+      r.T = d.t_len;
+      r.n_ops = d.n_ops;
       r.acgt = false;
       // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
       // and forward query bytes around the event are staged in LDS
@@ -2829,7 +2956,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
       r.lw = nullptr;
       r.l_lo = 0;
       r.l_n = 0;
-      const int j = (int)p0.y;
+      const int j = (int)cd.j;
       int o0 = j - kTcOps / 2;
       if (o0 < 0) o0 = 0;
       // (indices clamped to the record's last op, values masked after: a guarded load would be
@@ -2840,16 +2967,6 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
       for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
 #pragma unroll
       for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
-      // forward query bytes of the context: [fc - 5, fc + n + 5) for a '+' record, [fc - n - 5,
-      // fc + 5] for a '-' record (n <= 12 unless abbreviated), fc = the event's forward position
-      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;
-      int x0 = fc - (r.rev ? kTcQ / 2 : 8);
-      if (x0 < 0) x0 = 0;
-      const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
-      const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
-      v4u qv[kTcQ / 16];
-#pragma unroll
-      for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
 #pragma unroll
       for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
 #pragma unroll
@@ -2867,7 +2984,7 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
       ks.buf = me->out + 1;
       ks.junk = me->out + kTx;
       ks.pos = 0;
-      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);
+      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, cd.qs, cd.ts, h.ls);
       me->out[0] = (uint8_t)ks.pos;
       const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
       v4u t0, t1;
@@ -2979,7 +3096,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     uint64_t mm = mk[wv][k];
     for (uint32_t r = jl - ex[wv][k]; r > 0; r--) mm &= mm - 1;
     const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];
-    const Hot h = W.hot[f.s];
+    const Hot h = load_hot_full(A, W, f.s);
     const uint32_t typ = h.fn >> 30;
     const bool rev = (h.fn >> 29) & 1u;
     const bool use_tx = !((h.fn >> 28) & 1u);
@@ -3192,6 +3309,12 @@ extern "C" int pw_genome_table(const pw_aln_result* results, const uint32_t* gen
   return hipGetLastError() == hipSuccess ? PW_OK : PW_E_HIP;
 }
 
+extern "C" uint32_t pw_report_hot_pbits(uint64_t max_qlen, uint64_t n_queries) {
+  uint32_t pb = 1, qb = 0;
+  while (pb < 32 && (1ull << pb) <= max_qlen) pb++;
+  while (qb < 32 && (1ull << qb) < n_queries) qb++;
+  return pb <= 31 && pb + qb <= 32 ? pb : 0u;
+}
 extern "C" uint64_t pw_report_workspace_bytes(uint64_t n_events_max, uint64_t n_alns) {
   return pw::work_layout(nullptr, n_events_max, n_alns, nullptr);
 }
@@ -3225,8 +3348,11 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0) ncu = p.multiProcessorCount;
   }
+  if (args->hot_pbits > 31) return PW_E_ARG;
   pw::Work W;
   pw::work_layout(static_cast<uint8_t*>(args->workspace), args->n_ev_slots, args->n_alns, &W);
+  W.hot_pbits = args->hot_pbits;
+  W.hot_sh = args->hot_pbits ? 2u : 3u;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
@@ -3264,7 +3390,10 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
     if (rg > (uint64_t)ncu * 4u * pw::kRenderOcc) rg = (uint64_t)ncu * 4u * pw::kRenderOcc;
     // (render is the first kernel that reads next_stop)
     if (next_stop_ready && hipStreamWaitEvent(st, (hipEvent_t)next_stop_ready, 0) != hipSuccess) return PW_E_HIP;
-    hipLaunchKernelGGL(pw::render_kernel, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+    if (W.hot_pbits)
+      hipLaunchKernelGGL(pw::render_kernel<true>, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+    else
+      hipLaunchKernelGGL(pw::render_kernel<false>, dim3((uint32_t)rg), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
     // (+ finalize: ncu workgroups for the long lines, then one thread per record)
     hipLaunchKernelGGL(pw::fixup_kernel, dim3((uint32_t)ncu + (uint32_t)((args->n_alns + 255) / 256)), dim3(256), 0,
                        st, *args, W);

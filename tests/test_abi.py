@@ -76,3 +76,19 @@ def test_pack_cs_sub_at_query_end_is_left_to_the_device(built):
 @pytest.mark.parametrize("case", ["cli_no_r", "cli_G_F", "cli_C_N", "cli_bad_opt"])
 def test_cli_argument_errors(built, case, tmp_path):
     run_case(CLI, case, tmp_path)
+
+
+@pytest.mark.parametrize("max_qlen,n_queries,want", [
+    (5000, 1000, 13),        # cfg2: 13 position bits + 10 query bits
+    (3000, 200, 12),         # cfg3 gene panel
+    (5_000_000, 100, 23),    # cfg4 Mb contigs
+    (4096, 1, 13),           # a position may equal the query length (a deletion at the end)
+    (0, 0, 1),
+    (1000, 1 << 25, 0),      # 10 + 25 bits: 32-byte records
+    (1 << 31, 2, 0),
+])
+def test_hot_pbits_rule(built, max_qlen, n_queries, want):
+    """pw_report_hot_pbits: when the 16-byte event record (query index and position in one word)
+    applies, and how many position bits it takes."""
+    import pwasm_amd as pw
+    assert pw.lib().pw_report_hot_pbits(max_qlen, n_queries) == want

@@ -744,3 +744,19 @@ def test_pair_index_short_records(built, tmp_path, seed, extra, monkeypatch):
     same(["-r", fa, bad])
     monkeypatch.setenv("PW_NO_PAIRS", "1")
     same(["-r", fa, paf])
+
+
+@pytest.mark.parametrize("cfg,hot32", [(0, "0"), (0, "1"), (4, "0"), (4, "1")])
+def test_event_record_formats(built, tmp_path, monkeypatch, cfg, hot32):
+    """The report pass keeps 16-byte event records between its kernels when the queries' lengths
+    and count fit (query index and position in one word; start, length and literal bytes loaded
+    by the readers) and 32-byte ones otherwise (PW_HOT32=1 forces them): the same bytes either
+    way, on gene-length queries and on 150-250 kb contigs (18 position bits, auto -F)."""
+    monkeypatch.setenv("PW_HOT32", hot32)
+    if cfg == 0:
+        fa, paf = synth_paf(tmp_path, 0, seed=21)
+        same(["-r", fa, paf])
+    else:
+        fa, paf = synth_paf(tmp_path, 4, extra=["--ncds", 2, "--len-min", 150000, "--len-max", 250000, "--recs", 3,
+                                                "--err", 0.02])
+        same(["-r", fa, paf])

@@ -4,9 +4,9 @@
   noflush  the LDS counter-table flush (cnt_flush) never runs (counters still accumulated)
   nowin    the row window is not stored to LDS (loads kept, reads see a stale window)
   noruns   the gap-run ORs into the bitmap are skipped
-  rp_lds   tools/variants/row_prefix_lds.patch (row_prefix stages the row's runs in LDS)
+  rp_lds   profiles/variants/row_prefix_lds.patch (row_prefix stages the row's runs in LDS)
   k1_3ahead  row_chunk_sums with three groups' loads in flight instead of two
-  k1_32b   tools/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
+  k1_32b   profiles/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
   k1g<N>   row_chunk_sums with a grid of N workgroups (product: 2048)
   sy<N>    slot_rows with N workgroups per row (product: 2048 / rows)
   head     pw_msa.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
@@ -50,7 +50,7 @@ def make(name):
         os.makedirs(TMP, exist_ok=True)
         p = os.path.join(TMP, "rp_lds.hip")
         open(p, "w").write(s)
-        subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_prefix_lds.patch")], check=True)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "profiles/variants/row_prefix_lds.patch")], check=True)
         s = open(p).read()
     elif name == "k1_3ahead":  # row_chunk_sums with three groups' loads in flight (unrolled by three)
         s = sub(s, """  SumPre p0, p1;
@@ -77,11 +77,11 @@ def make(name):
   }
   if (n_mine % 3 >= 1) step(p0);
   if (n_mine % 3 == 2) step(p1);""")
-    elif name == "k1_32b":  # tools/variants/row_chunk_sums_32bases.patch
+    elif name == "k1_32b":  # profiles/variants/row_chunk_sums_32bases.patch
         os.makedirs(TMP, exist_ok=True)
         p = os.path.join(TMP, "k1_32b.hip")
         open(p, "w").write(s)
-        subprocess.run(["patch", "-s", p, os.path.join(REPO, "tools/variants/row_chunk_sums_32bases.patch")], check=True)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "profiles/variants/row_chunk_sums_32bases.patch")], check=True)
         s = open(p).read()
     elif name.startswith("k1g"):  # row_chunk_sums grid of N workgroups (product: 2048)
         n = int(name[3:])

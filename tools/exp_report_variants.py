@@ -23,6 +23,7 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   why      render counts its non-fast lanes by reason into Work.ctr[8..15] (ctr[7]: general waves)
   tw2      tctx_kernel in 2-wave workgroups (8 per CU)
   ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
+  h32      32-byte event records whatever the batch (the pre-round-5 format; same bytes)
   kl108    lines up to 108 bytes built in render (kLine 92 -> 108: the whole 40-byte slack of the
            148-byte stride; copy-out over 28 dwords / 7 groups), so fewer lines go to fixup_kernel
 Usage: python tools/exp_report_variants.py [names...]"""
@@ -65,8 +66,8 @@ PATCHES = {
               ("        const LDS v4u* lp4 = reinterpret_cast<const LDS v4u*>(my_line);",
                "        const LDS v4a4* lp4 = reinterpret_cast<const LDS v4a4*>(my_line);")],
     # tctx_kernel without the op walk (an 11-byte record of whatever the buffer holds: timing only)
-    "tc_nowalk": [("      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);",
-                   "      if (A.n_alns == 0) emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, (int)p0.w, (int)p1.x, h.ls);\n      else ks.pos = 11;")],
+    "tc_nowalk": [("      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, cd.qs, cd.ts, h.ls);",
+                   "      if (A.n_alns == 0) emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, cd.qs, cd.ts, h.ls);\n      else ks.pos = 11;")],
     # render_kernel in 2-wave workgroups, 6 per CU (same 3 waves/SIMD; a workgroup's LDS frees
     # when its slower wave ends, so smaller workgroups pack the CU more tightly)
     "rw2": [("constexpr int kRenderOcc = 3;   // render_kernel: workgroups per CU (LDS-limited)",
@@ -202,6 +203,9 @@ PATCHES["cg4"] = [("pw::carry_kernel, dim3((uint32_t)ncu * 8u)", "pw::carry_kern
 for _g in (256, 1024):
     PATCHES[f"ns{_g}"] = [("  const uint32_t grid = nq < 4096u ? nq : 4096u;", f"  const uint32_t grid = nq < {_g}u ? nq : {_g}u;")]
 PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
+# 32-byte event records whatever the batch (round 5: 16-byte records when the queries fit)
+PATCHES["h32"] = [("  W.hot_pbits = args->hot_pbits;\n  W.hot_sh = args->hot_pbits ? 2u : 3u;",
+                   "  W.hot_pbits = 0;\n  W.hot_sh = 3u;")]
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {

@@ -3,5 +3,6 @@ import csv
 import sys
 
 for r in csv.DictReader(open(sys.argv[1])):
-    if r["Name"].startswith("pw::"):
-        print(f"   {r['Name'].split('(')[0]:28s} {float(r['AverageNs']) / 1000:9.1f} us")
+    name = r["Name"][5:] if r["Name"].startswith("void ") else r["Name"]  # (templates: "void pw::k<..>(...)")
+    if name.startswith("pw::"):
+        print(f"   {name.split('(')[0]:28s} {float(r['AverageNs']) / 1000:9.1f} us")
