@@ -357,6 +357,9 @@ int pw_gapassem_run_ex(const char* layout_path, const char* out_path, uint32_t f
 /* The `pafreport` CLI (pafreport.cpp:175-460) on the HIP path; returns the process exit code
  * the reference would produce (it prints exactly what the reference prints). */
 int pw_pafreport_main(int argc, char** argv);
+/* The same, for an executable's main(): the output files are closed, then the process ends with
+ * that exit code (_exit) without freeing the run's host and device state.  Never returns. */
+int pw_pafreport_main_exit(int argc, char** argv);
 
 /* Host batch (the CLI's pre-pass), exposed so bench.py / tests can stage a batch on the
  * device themselves.  Array pointers stay valid until pw_batch_free. */

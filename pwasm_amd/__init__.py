@@ -144,6 +144,7 @@ _SIGS = {
                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(CsTotals),
                                   ctypes.POINTER(ctypes.c_int32)]),
     "pw_pafreport_main": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]),
+    "pw_pafreport_main_exit": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]),  # (ends the process)
     "pw_batch_from_files": (ctypes.c_void_p, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                               ctypes.c_size_t]),
     "pw_batch_view_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(BatchView)]),

@@ -1,15 +1,7 @@
 // pafreport_main.cpp — the `pafreport` executable: a thin main() over the C-ABI entry point
-// pw_pafreport_main (same flags, report format and exit codes as pafreport.cpp:175-460).
-#include <stdio.h>
-#include <unistd.h>
-
+// pw_pafreport_main_exit (same flags, report format and exit codes as pafreport.cpp:175-460; the
+// process ends as soon as the output files are closed — the batches' memory and the HIP runtime's
+// state are left to the exit).
 #include "pwasm_amd.h"
 
-int main(int argc, char** argv) {
-  const int rc = pw_pafreport_main(argc, argv);  // (its output files are closed when it returns)
-  fflush(stdout);
-  fflush(stderr);
-  // skip the HIP runtime's exit-time teardown (~0.1 s): the device memory and the context go with
-  // the process either way
-  _exit(rc);
-}
+int main(int argc, char** argv) { return pw_pafreport_main_exit(argc, argv); }

@@ -1442,6 +1442,7 @@ struct TextStream {
   const uint8_t* dev = nullptr;
   uint64_t region_end = 0, arena0 = 0;
   std::vector<uint8_t> arena;
+  std::vector<uint8_t> img[2];  // emit_parallel's output images (kept across batches: faulted in once)
   bool ok = false;
   bool init() {
     if (ok) return true;
@@ -1680,22 +1681,47 @@ int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, cons
       fprintf(stderr, "Warning: soft clipping shouldn't be found in this application!\n%s\n",
               b.buf.data() + rh.line_off);
   }
+  // Per window: the pieces are copied by up to nt threads into one contiguous host image of the
+  // window's destination range, and that image goes out as one large pwrite on a writer thread
+  // while the next window is copied (two images alternate).  Writers of one file serialise on its
+  // inode lock, so many small concurrent pwritev calls (a piece is a ~60-byte header or a record's
+  // ~2 KB of lines) ran at ~3.3 GB/s where one large pwrite reaches the file system's ~10 GB/s
+  // (tools/gpu_e2e3.sh, round 5).
   const int64_t nwin = pc.empty() ? 0 : pc.back().win + 1;
   std::atomic<bool> bad{false};
+  std::vector<uint8_t>* img = ts.img;
+  std::thread wr[2];
+  auto write_img = [&](int k, uint64_t d0, uint64_t n) {
+    uint64_t done = 0;
+    while (done < n) {
+      const ssize_t w = pwrite(fd, img[k].data() + done, (size_t)(n - done), base + (off_t)(d0 + done));
+      if (w <= 0) {
+        bad = true;
+        return;
+      }
+      done += (uint64_t)w;
+    }
+  };
   size_t i0 = 0;
-  for (int64_t w = 0; w < nwin; w++) {
+  for (int64_t w = 0; w < nwin && !bad; w++) {
     size_t i1 = i0;
     while (i1 < pc.size() && pc[i1].win == w) i1++;
     const int slot = (int)(w & 1);
     const uint64_t wlo = (uint64_t)w * TextStream::kWin;
     const bool dma = wlo < ts.region_end;
     if (dma) {
-      if (ts.base[slot] != wlo) return -3;  // (windows are consumed in order)
+      if (ts.base[slot] != wlo) {
+        bad = true;
+        break;  // (windows are consumed in order)
+      }
       (void)hipEventSynchronize(ts.ev[slot]);
     }
     const uint8_t* wb = ts.buf[slot];
+    if (wr[slot].joinable()) wr[slot].join();  // image `slot` is free again
     if (i1 > i0) {
       const uint64_t d0 = pc[i0].dst, d1 = pc[i1 - 1].dst + pc[i1 - 1].len;
+      if (img[slot].size() < d1 - d0) img[slot].resize(d1 - d0);
+      uint8_t* ib = img[slot].data();
       const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(nt, 1), (d1 - d0) >> 20));
       auto work = [&](int t) {  // the pieces whose destination starts in this thread's byte range
         const uint64_t a = d0 + (d1 - d0) * (uint64_t)t / (uint64_t)T;
@@ -1703,38 +1729,14 @@ int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, cons
         size_t j = (size_t)(std::lower_bound(pc.begin() + (long)i0, pc.begin() + (long)i1, a,
                                              [](const Piece& p, uint64_t v) { return p.dst < v; }) -
                             pc.begin());
-        iovec iov[256];
-        while (j < i1 && pc[j].dst < z) {
-          int n = 0;
-          const uint64_t at = pc[j].dst;
-          uint64_t len = 0;
-          for (; n < 256 && j < i1 && pc[j].dst < z; n++, j++) {
-            iov[n].iov_base = (void*)(pc[j].host ? pc[j].host : wb + (pc[j].src - wlo));
-            iov[n].iov_len = pc[j].len;
-            len += pc[j].len;
-          }
-          uint64_t done = 0;
-          int q0 = 0;
-          while (done < len) {  // (short writes: resume inside the vector)
-            const ssize_t k = pwritev(fd, iov + q0, n - q0, base + (off_t)(at + done));
-            if (k <= 0) {
-              bad = true;
-              return;
-            }
-            done += (uint64_t)k;
-            uint64_t m = (uint64_t)k;
-            while (q0 < n && m >= iov[q0].iov_len) m -= iov[q0++].iov_len;
-            if (q0 < n) {
-              iov[q0].iov_base = (uint8_t*)iov[q0].iov_base + m;
-              iov[q0].iov_len -= m;
-            }
-          }
-        }
+        for (; j < i1 && pc[j].dst < z; j++)
+          memcpy(ib + (pc[j].dst - d0), pc[j].host ? pc[j].host : wb + (pc[j].src - wlo), pc[j].len);
       };
       std::vector<std::thread> th;
       for (int t = 1; t < T; t++) th.emplace_back(work, t);
       work(0);
       for (auto& x : th) x.join();
+      wr[slot] = std::thread(write_img, slot, d0, d1 - d0);
     }
     if (dma) {  // this window's buffer takes window w + 2
       ts.base[slot] += 2 * TextStream::kWin;
@@ -1742,6 +1744,8 @@ int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, cons
     }
     i0 = i1;
   }
+  for (auto& x : wr)
+    if (x.joinable()) x.join();
   if (bad) return -3;
   if (fseeko(out, base + (off_t)dst, SEEK_SET) != 0) return -3;
   return -1;
@@ -1826,7 +1830,43 @@ uint64_t alg_bytes(const Batch& b, const QueryDb& q, bool skip_codan) {
 }  // namespace
 
 // ================================================================= CLI
-extern "C" int pw_pafreport_main(int argc, char** argv) {
+static double mono_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The CLI's host and device state (one allocation, so that the executable can leave it to the
+// process exit: freeing the batches' host vectors and the device buffers took 0.8 s after a
+// 16 GB cfg3 report — tools/gpu_e2e3.sh, round 5).
+struct CliState {
+  QueryDb qdb;
+  Device dev;
+  Packer pk;
+  std::unique_ptr<ChunkReader> rd;
+  Batch bb[2];
+  TextStream tstream;
+  std::vector<pw_aln_result> res_h;
+  std::vector<pw_page> pages_h;
+};
+
+static int run_cli(int argc, char** argv, bool leave_state);
+
+extern "C" int pw_pafreport_main(int argc, char** argv) { return run_cli(argc, argv, false); }
+
+extern "C" int pw_pafreport_main_exit(int argc, char** argv) {
+  const int rc = run_cli(argc, argv, true);  // (output files closed; the rest goes with the process)
+  fflush(stdout);
+  fflush(stderr);
+  _exit(rc);
+}
+
+static int run_cli(int argc, char** argv, bool leave_state) {
+  // (PW_PROFILE_HOST: the destructors' time at the end — declared first, so destroyed last)
+  struct TearTimer {
+    double t = 0;
+    ~TearTimer() {
+      if (t > 0) fprintf(stderr, "[cli] teardown %.3f s\n", mono_s() - t);
+    }
+  } tear;
   Args args;
   args.parse(argc, argv, "DGFCNvd:p:r:o:m:w:c:s:");
   if (args.err > 0) {
@@ -1910,7 +1950,10 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   const bool prof = getenv("PW_PROFILE_HOST") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t_start = prof ? now() : 0;
-  QueryDb qdb;
+  CliState* state = new CliState;
+  std::unique_ptr<CliState, void (*)(CliState*)> state_owner(
+      state, leave_state ? +[](CliState*) {} : +[](CliState* p) { delete p; });
+  QueryDb& qdb = state->qdb;
   std::string err;
   if (!qdb.load(fa, err)) {
     fputs(err.c_str(), stderr);
@@ -1932,8 +1975,8 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
       return 1;
     }
   }
-  Device dev;
-  Packer pk;
+  Device& dev = state->dev;
+  Packer& pk = state->pk;
   pk.qdb = &qdb;
   pk.nt = host_threads();
   pk.opt.fullgenome = fullgenome;
@@ -1946,11 +1989,12 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
   pk.opt.gpu_pack = !pk.opt.msa && !(getenv("PW_PACK_HOST") && atoi(getenv("PW_PACK_HOST")) != 0);
   // Pipeline: while the GPU runs batch k and its report is written, batch k + 1 is read and
   // packed (by pk.nt threads); nothing past a fatal batch is packed.
-  ChunkReader rd(in.f);
-  Batch bb[2];
-  TextStream tstream;
-  std::vector<pw_aln_result> res_h;
-  std::vector<pw_page> pages_h;
+  state->rd = std::make_unique<ChunkReader>(in.f);
+  ChunkReader& rd = *state->rd;
+  Batch* bb = state->bb;
+  TextStream& tstream = state->tstream;
+  std::vector<pw_aln_result>& res_h = state->res_h;
+  std::vector<pw_page>& pages_h = state->pages_h;
   size_t kChunk = 256u << 20;  // input bytes per batch (PW_CHUNK_BYTES: tests force many batches)
   if (const char* e = getenv("PW_CHUNK_BYTES"))
     if (atoll(e) > 0) kChunk = (size_t)atoll(e);
@@ -2021,6 +2065,15 @@ extern "C" int pw_pafreport_main(int argc, char** argv) {
     const int rc = pw::write_run_msa(fmsa.f, debug ? stderr : nullptr, qdb.ids[(size_t)qi].c_str(), qdb.seq.data() + qdb.off[(size_t)qi],
                                  qdb.len[(size_t)qi], pk.run);
     if (rc != 0) return rc;
+  }
+  if (prof) {
+    const double t = now();
+    if (out.f && out.f != stdout) {
+      fclose(out.f);
+      out.f = nullptr;
+    }
+    fprintf(stderr, "[cli] close output %.3f s\n", now() - t);
+    tear.t = mono_s();
   }
   return 0;
 }
