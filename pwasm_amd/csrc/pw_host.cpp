@@ -2012,10 +2012,19 @@ static int run_cli(int argc, char** argv, bool leave_state) {
     par_emit = fstat(fileno(out.f), &os) == 0 && S_ISREG(os.st_mode);
   }
   int cur = 0;
+  // the device side comes up beside the first batch's pack: the HIP runtime (warm-up thread), then
+  // the queries, their next-stop tables and the pinned text windows
+  bool dev_ok = false;
+  std::thread dev_up([&] {
+    warm.join();
+    dev_ok = dev.init(qdb, skip_codan) && tstream.init();
+    if (!dev_ok && tstream.st == nullptr && dev.stream != nullptr)
+      fprintf(stderr, "pafreport: pinned host buffers could not be allocated\n");
+  });
   bool have = pack_next(bb[0]);
   const double t_pack0 = prof ? now() : 0;
-  warm.join();
-  if (!dev.init(qdb, skip_codan)) return 2;
+  dev_up.join();
+  if (!dev_ok) return 2;
   if (prof)
     fprintf(stderr, "[cli] fasta %.3f s, first batch read + pack %.3f s, device init (after warm-up) %.3f s\n",
             t_fasta - t_start, t_pack0 - t_fasta, now() - t_pack0);
@@ -2029,8 +2038,7 @@ static int run_cli(int argc, char** argv, bool leave_state) {
     }
     const double t_r0 = prof ? now() : 0;
     bool ran = dev.run(B, qdb, skip_codan, nullptr, res_h, pages_h);
-    ran = ran && tstream.init() &&
-          tstream.begin(dev.text.p, pages_h, pw_report_page_count(B.n_events_max));
+    ran = ran && tstream.begin(dev.text.p, pages_h, pw_report_page_count(B.n_events_max));
     const double t_r1 = prof ? now() : 0;
     TextSrc src;
     src.stream = &tstream;

@@ -494,10 +494,10 @@ struct TileLds {
   uint32_t bmap[kCntWaves][64];            // per-wave gap-column bitmaps
   uint32_t sel[16];                        // v_perm selectors: 4-bit gap mask -> byte picks
 };
-// LDS slot of column c: rotated by (32-column block & 3), so the adds of one counter index of
-// the 32 lanes of an LDS access group (lane 4a + b: column 32(4a + b) + 4((q + a) & 7) + j) fall
-// into distinct banks (4((q + a) & 7) + b + j)
-__device__ __forceinline__ int cnt_swz(int c) { return (c & ~31) | ((c + ((c >> 5) & 3)) & 31); }
+// LDS slot of column c: rotated within its 32 columns by its 32-column block index, so the adds
+// of one counter index m of the 32 lanes of an LDS access group (lane l: column 32 l + m) fall
+// into distinct banks ((m + l) & 31)
+__device__ __forceinline__ int cnt_swz(int c) { return (c & ~31) | ((c + (c >> 5)) & 31); }
 // the bin shifts (5 x GAlnColumn::addNuc/addGap bin, as bin_of) of 4 characters in a dword:
 // h = (c >> 1) & 7 picks, per byte, the only characters that can have each bin (A/a 0, C/c 1,
 // T/t 2, G/g 3, '*' 5, '-' 6; 4 and 7 none) and v_perm looks up the code, the expected
@@ -631,10 +631,9 @@ __device__ __forceinline__ void pin(v2u& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void cnt_flush(uint32_t (&acc)[32], LDS uint32_t* tab, int lane) {
-  const int rot = (lane >> 2) & 7;
 #pragma unroll
   for (int m = 0; m < 32; m++) {
-    const int x = cnt_swz(32 * lane + 4 * (((m >> 2) + rot) & 7) + (m & 3));  // (see the column groups in K3)
+    const int x = cnt_swz(32 * lane + m);  // (acc[m] = column 32 lane + m)
 #pragma unroll
     for (int f = 0; f < 6; f++) {
       atomicAdd((uint32_t*)&tab[f * kCntW + x], (acc[m] >> (5 * f)) & 31u);
@@ -819,30 +818,23 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
         // byte offset in the window of the base in this lane's first clear column
         const int so = (int)((uint32_t)(roff + (uint64_t)ib) & 15u) + 32 * lane - excl;
         const LDS uint8_t* wb = reinterpret_cast<const LDS uint8_t*>(win);
-        // step q: this lane's column group g = (q + rot) & 7 (columns 32 lane + 4g ..): the 32 lanes
-        // of an LDS access group then read 32 distinct banks of the window (lane 4a + b at dword
-        // 8(4a + b) + g: bank 8b + g), with acc[4q + j] holding column 32 lane + 4 g + j.  In the
-        // bitmap rotated right by 4 rot, group g is nibble q; its source offset is
-        // so + 4g - popc(bits below 4g) = base0 + 4q - popc(rotated bits below 4q), less 32 - pc
-        // once g has wrapped around (q >= 8 - rot).
-        const int rot = (lane >> 2) & 7;
-        const uint32_t rb = rot ? __builtin_amdgcn_alignbit(bmv, bmv, 4u * (uint32_t)rot) : bmv;
-        const int base0 = so + 4 * rot - __popc(__builtin_amdgcn_ubfe(bmv, 0, 4u * (uint32_t)rot));
-        const int wrapc = 32 - pc, qwrap = 8 - rot;
-        // the 8 groups' codes (fast classifier; a wave with another character redoes them with
-        // the general one), then the 32 counters
+        // step q: this lane's column group q (columns 32 lane + 4q ..), its source offset so + 4q -
+        // popc(bitmap bits below 4q).  (Rounds 3-4 rotated each lane's group order so that the 32
+        // lanes of an LDS access group read 32 distinct banks when the row has no gaps; the
+        // rotation's offset and wrap arithmetic cost more than the conflicts it removed: round 5,
+        // tools/exp_msa_variants.py norot, tile_counts 90.5 -> 87.1 us.)
         uint32_t codes[8];
         auto groups = [&](auto edge_c, auto fast_c) {
           constexpr bool kEdge = decltype(edge_c)::value, kFast = decltype(fast_c)::value;
           uint32_t rom = 0, bad = 0;
           if constexpr (kEdge) {
             const uint32_t om = outside_mask(lane, a - c0, z - c0 + 1);
-            rom = rot ? __builtin_amdgcn_alignbit(om, om, 4u * (uint32_t)rot) : om;
+            rom = om;
           }
 #pragma unroll
           for (int q = 0; q < 8; q++) {
-            const uint32_t nb = (rb >> (4 * q)) & 15u;
-            const int src = base0 + 4 * q - (q == 0 ? 0 : __popc(rb & ((1u << (4 * q)) - 1u))) - (q >= qwrap ? wrapc : 0);
+            const uint32_t nb = (bmv >> (4 * q)) & 15u;
+            const int src = so + 4 * q - (q == 0 ? 0 : __popc(bmv & ((1u << (4 * q)) - 1u)));
             const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
             const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
             const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);

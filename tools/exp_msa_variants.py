@@ -9,6 +9,10 @@
   k1_32b   profiles/variants/row_chunk_sums_32bases.patch (8 lanes x 32 bases per chunk)
   k1g<N>   row_chunk_sums with a grid of N workgroups (product: 2048)
   sy<N>    slot_rows with N workgroups per row (product: 2048 / rows)
+  nogather no window reads at all (the group bytes a constant: the cost of the LDS gather)
+  (round 5, measured then dropped from this list: idealsrc — reads at the gap-free offsets,
+  norot — no per-lane rotation of the column groups (adopted), runs2 — gap-run ORs as two
+  words + a loop past 33 columns (93.7 vs 90.5 us))
   head     pw_msa.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
 Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
 import os
@@ -89,9 +93,6 @@ def make(name):
     elif name.startswith("sy"):  # slot_rows with N workgroups per row (product: 2048 / rows, <= 64)
         s = sub(s, "const unsigned sy = a->n_rows >= 2048 ? 1u : (2048u / a->n_rows < 64u ? 2048u / a->n_rows : 64u);",
                 f"const unsigned sy = {int(name[2:])}u;")
-    elif name == "idealsrc":  # window reads at the gap-free offsets (the rotation's conflict-free pattern)
-        s = sub(s, "            const int src = base0 + 4 * q - (q == 0 ? 0 : __popc(rb & ((1u << (4 * q)) - 1u))) - (q >= qwrap ? wrapc : 0);",
-                "            const int src = 32 * lane + 4 * ((q + rot) & 7) + (base0 & 0);")
     elif name == "nogather":  # no window reads at all (the group bytes are a constant)
         s = sub(s, """            const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);""",
                 """            const uint32_t s4 = 0x41434754u + (uint32_t)(src & 0) + (uint32_t)(p == nullptr);""")
