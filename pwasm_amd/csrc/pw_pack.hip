@@ -215,7 +215,8 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
         const uint64_t have_d = (uint64_t)bytes_digit(lo) | (uint64_t)bytes_digit(hi) << 32;
         const int ln = min(max(len, 1), 8);
         const uint64_t lmask = ln >= 8 ? ~0ull : ((1ull << (8 * ln)) - 1ull);
-        const bool dig_bad = len < 1 || len > 9 || (lmask & 0x8080808080808080ull & ~have_d) || (len == 9 && c9 - '0' > 9u);
+        const bool dig_bad = ((uint32_t)(len - 1) > 8u) | ((lmask & 0x8080808080808080ull & ~have_d) != 0) |
+                             ((len == 9) & (c9 - '0' > 9u));
         const uint64_t al = (d & lmask) << (8 * (8 - ln));  // right-aligned
         const uint32_t v8 = dec4((uint32_t)al) * 10000u + dec4((uint32_t)(al >> 32));
         const uint32_t v = len == 9 ? v8 * 10u + (c9 - '0') : v8;
@@ -237,17 +238,20 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       const int g_below = (int)((key_below - 1u) >> 2), ty_below = key_below ? (int)((key_below - 1u) & 3u) : -1;
       const int j0 = __builtin_ctz(sm | 16u), j1 = __builtin_ctz(sm1 | 16u);  // (4: none)
       uint32_t litm = 0;  // literal characters of this lane (bit j)
+      uint32_t need_letter = 0;  // characters of this lane inside a '+' / '-' op (bit j)
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int i = 4 * lane + j;
-        const bool in = i < lim && !((sm >> j) & 1u);
+        const uint32_t in = (uint32_t)(i < lim) & ~(sm >> j) & 1u;
         // governing start: the lane's second start if before j, else its first, else the one below
         const int g = j1 < j ? 4 * lane + j1 : (j0 < j ? 4 * lane + j0 : g_below);
         const int ty = j1 < j ? kind[1] : (j0 < j ? kind[0] : ty_below);
-        const bool letter = ((m_alp >> (8 * j + 7)) & 1u) != 0;
-        lbad = lbad | (in & ((ty == PW_OP_INS) | (ty == PW_OP_DEL)) & !letter);
-        litm |= (in && (ty == PW_OP_INS || (ty == PW_OP_SUB && i - g - 1 < 2))) ? 1u << j : 0u;
+        const uint32_t indel = (uint32_t)(ty == PW_OP_INS) | (uint32_t)(ty == PW_OP_DEL);
+        const uint32_t lit = (uint32_t)(ty == PW_OP_INS) | ((uint32_t)(ty == PW_OP_SUB) & (uint32_t)(i - g - 1 < 2));
+        need_letter |= (in & indel) << j;
+        litm |= (in & lit) << j;
       }
+      lbad = lbad | ((need_letter & ~msb_bits(m_alp)) != 0);
       // exclusive prefixes over the lanes (ops and characters are in lane order)
       const uint32_t nlit = (uint32_t)__popc(litm);
       const int iq = wave_scan_incl(q_a), it = wave_scan_incl(t_a);

@@ -1,7 +1,8 @@
 """Experiment builds of pw_pack.hip (never shipped), linked with the other product objects into
 tools/abl_build/<name>/lib for tools/pk_sweep.sh (PWASM_LIB):
   cur      the working copy
-  pkg<N>   pack_cs_kernel grid capped at N workgroups per CU (product: 16)
+  head     pw_pack.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
+  pkg<N>   pack_cs_kernel grid capped at N workgroups per CU (product: 64)
 Usage: python tools/exp_pack_variants.py [names...]"""
 import os
 import subprocess
@@ -15,8 +16,11 @@ TMP = os.path.join(REPO, "build_exp")
 
 def make(name):
     s = open(SRC).read()
-    if name.startswith("pkg"):
-        old = "const uint32_t cap = (uint32_t)ncu * 16u;"
+    if name == "head":
+        s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_pack.hip"], capture_output=True, text=True,
+                           check=True).stdout
+    elif name.startswith("pkg"):
+        old = "const uint32_t cap = (uint32_t)ncu * 64u;"
         assert old in s
         s = s.replace(old, f"const uint32_t cap = (uint32_t)ncu * {int(name[3:])}u;")
     elif name != "cur":
