@@ -24,6 +24,8 @@ tools/abl_build/<name>/lib for tools/exp_sweep.sh (PWASM_LIB):
   tw2      tctx_kernel in 2-wave workgroups (8 per CU)
   ls148    148-byte line buffer stride (odd dword count: fewer LDS bank conflicts between lanes)
   h32      32-byte event records whatever the batch (the pre-round-5 format; same bytes)
+  qalias / occ4 / occ4q  render's query windows in the line buffers' tails (LDS for 4 workgroups
+           per CU) / the 4-per-CU register budget / both (timing only)
   kl108    lines up to 108 bytes built in render (kLine 92 -> 108: the whole 40-byte slack of the
            148-byte stride; copy-out over 28 dwords / 7 groups), so fewer lines go to fixup_kernel
 Usage: python tools/exp_report_variants.py [names...]"""
@@ -206,6 +208,29 @@ PATCHES["fx_pb"] = PATCHES["fx_par"] + PATCHES["fx_bigwin"]  # (both)
 # 32-byte event records whatever the batch (round 5: 16-byte records when the queries fit)
 PATCHES["h32"] = [("  W.hot_pbits = args->hot_pbits;\n  W.hot_sh = args->hot_pbits ? 2u : 3u;",
                    "  W.hot_pbits = 0;\n  W.hot_sh = 3u;")]
+
+# render occupancy (round 5, timing only): the query windows placed in the line buffers' tails
+# (bytes 100-147 of each lane's 148-byte buffer: 37.9 KB of LDS per workgroup, room for 4 per CU;
+# a line past 100 bytes overwrites its own window), with / without the 4-per-CU register budget
+# (128 VGPRs: hipcc spills the rest)
+_QALIAS = [("  uint8_t qw[kWave * kQStride];     // per-lane forward-query windows\n", ""),
+           ("  LDS uint8_t* my_qw = w->qw + lane * kQStride;", "  LDS uint8_t* my_qw = w->line + lane * kLStride + 100;")]
+PATCHES["qalias"] = _QALIAS
+PATCHES["occ4"] = [("constexpr int kRenderOcc = 3;", "constexpr int kRenderOcc = 4;")]
+PATCHES["occ4q"] = _QALIAS + PATCHES["occ4"]
+
+# (the same with the window stored as dwords: 8-byte stores at the 4-byte aligned tails replay)
+_QALIAS2 = _QALIAS + [("""      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
+      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};""",
+                      """      {
+        volatile LDS uint32_t* q4 = reinterpret_cast<volatile LDS uint32_t*>(my_qw + 16 * q);
+        q4[0] = pre.q[q].x;
+        q4[1] = pre.q[q].y;
+        q4[2] = pre.q[q].z;
+        q4[3] = pre.q[q].w;
+      }""")]
+PATCHES["qalias2"] = _QALIAS2
+PATCHES["occ4q2"] = _QALIAS2 + PATCHES["occ4"]
 
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
