@@ -186,7 +186,10 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       // the (at most two) ops of this lane, without branches: every quantity is computed for both
       // slots and selected by the op kind (a divergent branch per kind costs every wave all kinds)
       int q_a = 0, t_a = 0;                  // query / target advance of this lane's ops
-      uint32_t cnt = 0;                      // ops emitted | events << 10 | substitutions << 20
+      // ops emitted | events << 8 | substitutions << 16 | literals << 23: a window of 256 characters
+      // has at most 128 ops / events, 85 substitutions and 255 literals, so the fields of one
+      // scan's prefixes never carry into each other
+      uint32_t cnt = 0;
       uint32_t opw[2];
       bool emit[2];
       int qb[2], qn[2];                      // bounds checks: query advance before the op, its length
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
         t_a += (is_col || is_sub || is_ins) ? n_op : 0;
         emit[t] = valid && (!is_col || v > 0);
         opw[t] = PW_OP((uint32_t)(kind[t] & 3), (uint32_t)n_op);
-        cnt += (emit[t] ? 1u : 0u) | (valid && !is_col ? 1u << 10 : 0u) | (is_sub ? 1u << 20 : 0u);
+        cnt += (emit[t] ? 1u : 0u) | (valid && !is_col ? 1u << 8 : 0u) | (is_sub ? 1u << 16 : 0u);
       }
       // per character: its governing op (this lane's last start at or before it, else the last
       // one below the lane) -> literal ('*' pair, '-' bases) or letter required ('+' / '-')
@@ -254,22 +257,24 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       lbad = lbad | ((need_letter & ~msb_bits(m_alp)) != 0);
       // exclusive prefixes over the lanes (ops and characters are in lane order)
       const uint32_t nlit = (uint32_t)__popc(litm);
+      cnt += nlit << 23;
       const int iq = wave_scan_incl(q_a), it = wave_scan_incl(t_a);
-      const uint32_t il = wave_scan_incl(nlit), ic = wave_scan_incl(cnt);
+      const uint32_t ic = wave_scan_incl(cnt), il = ic >> 23;
       // bounds checks (pafreport.cpp:542-626 as restated by pw_pack_cs)
       const int q0 = qpos + iq - q_a;
 #pragma unroll
       for (int t = 0; t < 2; t++) {
         const int qp = off + q0 + qb[t];
         const bool chk = kind[t] == PW_OP_MATCH || kind[t] == PW_OP_SUB || kind[t] == PW_OP_DEL;
-        lbad = lbad | (chk & ((qp < 0) | ((int64_t)qp + qn[t] > ql)));
+        // (qp >= 0 and qn < 2^30: the 32-bit unsigned sum does not wrap)
+        lbad = lbad | (chk & ((qp < 0) | ((uint32_t)qp + (uint32_t)qn[t] > (uint32_t)ql)));
       }
       if (__ballot(lbad) || !starts || (!last_win && last_start == 0)) {
         bad = true;  // (one op filling a window also lands here)
         return false;
       }
       // op words and literal bytes at their places (32-bit offsets from the record's bases)
-      const uint32_t op_i = nops + ((ic - cnt) & 0x3FFu);
+      const uint32_t op_i = nops + ((ic - cnt) & 0xFFu);
       if (emit[0]) ops_r[op_i] = opw[0];
       if (emit[1]) ops_r[op_i + (emit[0] ? 1u : 0u)] = opw[1];
       const uint32_t u4 = up_bytes(c4);
@@ -285,12 +290,12 @@ __global__ __launch_bounds__(256) void pack_cs_kernel(const uint8_t* text, const
       // ':' values up to 999,999,999: sums stay in range for queries below 2^31
       qpos += wave_last(iq);
       tpos += wave_last(it);
-      nlits += wave_last(il);
       const uint32_t ctot = wave_last(ic);
-      nops += ctot & 0x3FFu;
-      nev += (ctot >> 10) & 0x3FFu;
-      const uint32_t nsub = ctot >> 20;
-      bound += (uint64_t)kPkBoundIndel * ((ctot >> 10 & 0x3FFu) - nsub) + (uint64_t)kPkBoundSub * nsub;
+      nlits += ctot >> 23;
+      nops += ctot & 0xFFu;
+      const uint32_t wev = (ctot >> 8) & 0xFFu, nsub = (ctot >> 16) & 0x7Fu;
+      nev += wev;
+      bound += (uint64_t)kPkBoundIndel * (wev - nsub) + (uint64_t)kPkBoundSub * nsub;
       pos += (uint64_t)lim;
       __builtin_amdgcn_wave_barrier();
       return true;
