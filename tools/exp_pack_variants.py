@@ -3,6 +3,7 @@ tools/abl_build/<name>/lib for tools/pk_sweep.sh (PWASM_LIB):
   cur      the working copy
   head     pw_pack.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
   pkg<N>   pack_cs_kernel grid capped at N workgroups per CU (product: 64)
+  w8       the kernel held to 8 waves/SIMD (amdgpu_waves_per_eu: SGPRs spilled to VGPR lanes)
 Usage: python tools/exp_pack_variants.py [names...]"""
 import os
 import subprocess
@@ -23,6 +24,10 @@ def make(name):
         old = "const uint32_t cap = (uint32_t)ncu * 64u;"
         assert old in s
         s = s.replace(old, f"const uint32_t cap = (uint32_t)ncu * {int(name[3:])}u;")
+    elif name == "w8":  # amdgpu_waves_per_eu(8): SGPRs <= 96 (more spilled to VGPR lanes), 8 waves/SIMD
+        old = "__global__ __launch_bounds__(256) void pack_cs_kernel"
+        assert old in s
+        s = s.replace(old, "__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void pack_cs_kernel")
     elif name != "cur":
         raise SystemExit(f"unknown variant {name}")
     os.makedirs(TMP, exist_ok=True)
