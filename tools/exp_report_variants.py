@@ -232,6 +232,9 @@ _QALIAS2 = _QALIAS + [("""      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v
 PATCHES["qalias2"] = _QALIAS2
 PATCHES["occ4q2"] = _QALIAS2 + PATCHES["occ4"]
 
+# index_kernel at 4 waves/SIMD (128 VGPRs; product: 5)
+PATCHES["idx4"] = [("constexpr int kIndexOcc = 5;", "constexpr int kIndexOcc = 4;")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
