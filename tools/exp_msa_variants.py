@@ -13,6 +13,8 @@
   (round 5, measured then dropped from this list: idealsrc — reads at the gap-free offsets,
   norot — no per-lane rotation of the column groups (adopted), runs2 — gap-run ORs as two
   words + a loop past 33 columns (93.7 vs 90.5 us))
+  rowlist8 / rowlist8mid  tile_counts_rowlist16.patch at 8 waves per workgroup (rows that meet the
+           tile listed and shared equally; mid: tiles from the middle outwards)
   head     pw_msa.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
 Usage: python tools/exp_msa_variants.py [names...]  -> tools/abl_build/<name>/lib (tools/exp_msa.py)"""
 import os
@@ -56,6 +58,18 @@ def make(name):
         open(p, "w").write(s)
         subprocess.run(["patch", "-s", p, os.path.join(REPO, "profiles/variants/row_prefix_lds.patch")], check=True)
         s = open(p).read()
+    elif name in ("rowlist8", "rowlist8mid"):  # the row-list patch at 8 waves per workgroup (2 per CU)
+        os.makedirs(TMP, exist_ok=True)
+        p = os.path.join(TMP, f"{name}.hip")
+        open(p, "w").write(s)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "profiles/variants/tile_counts_rowlist16.patch")], check=True)
+        s = open(p).read()
+        s = sub(s, "constexpr int kCntWaves = 16;", "constexpr int kCntWaves = 8;")
+        s = sub(s, "constexpr int kRowList = 8192;", "constexpr int kRowList = 2048;")  # (2 workgroups per CU)
+        s = sub(s, "void tile_counts(const pw_msa_args A", "void tile_counts(const pw_msa_args A")
+        s = s.replace("__global__ __launch_bounds__(64 * kCntWaves, 1) void tile_counts", "__global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts")
+        if name == "rowlist8":
+            s = sub(s, "  const int tile = tile_of_block((int)blockIdx.x, (int)gridDim.x);", "  const int tile = (int)blockIdx.x;")
     elif name == "k1_3ahead":  # row_chunk_sums with three groups' loads in flight (unrolled by three)
         s = sub(s, """  SumPre p0, p1;
   sums_load(A, sums_desc(A, sdesc, g, lane), g, lane, p0);
