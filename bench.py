@@ -2,7 +2,7 @@
 """bench.py — pafreport hot path on MI355X: cs-events classified per second.
 
 A "step" = one pass of the hot path over one batch already resident in HBM: the next-stop
-table build (pw_stop_table_build, on a side stream overlapping the decode kernels) + the
+table build (by the pass's first kernel beside the decode: PW_REPORT_BUILD_NEXT_STOP) + the
 decode/classify/codon/render kernels (pw_report_events_after) over every record of the batch.  At N=1 the batch is BASELINE.json
 configs[1] (cfg2: 100k synthetic minimap2-style records, 1,000 CDS of 1-5 kb, ~1% ONT-style
 errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard (different
@@ -201,22 +201,25 @@ def report_leg(args, config, world, rank, dev_name):
         gtab = (mgpu, rows, gt, torch.zeros(max(pad, 16), dtype=torch.uint8, device=dev_name),
                 torch.empty(world * max(pad, 16), dtype=torch.uint8, device=dev_name))
 
-    # the next-stop table is built on a side stream, overlapping the decode kernels (index, tctx);
-    # the pass waits for it before render (pw_report_events_after), the side stream waits for the
-    # previous pass before rebuilding it
+    # the next-stop table is built by the pass itself (PW_REPORT_BUILD_NEXT_STOP: index_kernel's
+    # first workgroups, beside the decode) — round 5; before, a side stream built it and the pass
+    # waited for its event before render.  PW_NS_SIDE=1 keeps that form (A/B sweeps).
+    side_ns = os.environ.get("PW_NS_SIDE") == "1"
     side = torch.cuda.Stream()
     ns_ready, pass_done = torch.cuda.Event(), torch.cuda.Event()
 
     def step():
         ready = None
-        if not v.skip_codan:
+        a = pw.report_args(batch, dev)
+        if not v.skip_codan and side_ns:
             side.wait_event(pass_done)
             rc = pw.lib().pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
                                               int(v.n_queries), dev["next_stop"].data_ptr(), side.cuda_stream)
             assert rc == 0
             ns_ready.record(side)
             ready = ns_ready.cuda_event
-        a = pw.report_args(batch, dev)
+        elif not v.skip_codan:
+            a.flags |= pw.REPORT_BUILD_NEXT_STOP
         rc = pw.lib().pw_report_events_after(pw.ctypes.byref(a), sp, ready)
         assert rc == 0
         pass_done.record(stream)

@@ -127,8 +127,14 @@ typedef struct pw_report_args {
                                query index (desc[].ref & PW_REF_QMASK) < 2^(32 - P): the pass then
                                keeps 16 instead of 32 bytes per event between its kernels (an event
                                that violates it ends its record with PW_REC_LAYOUT) */
+  uint32_t flags;           /* PW_REPORT_* */
+  uint32_t n_queries;       /* queries of qoff / qlen (read with PW_REPORT_BUILD_NEXT_STOP) */
   uint32_t pad;
 } pw_report_args;
+/* The pass builds next_stop itself (pw_stop_table_build's table for n_queries queries, by workgroups
+ * of its first kernel running beside the decode: no second stream, no event); next_stop is then
+ * written, and must not be read by other work until the pass completes. */
+#define PW_REPORT_BUILD_NEXT_STOP 1u
 #define PW_BLOCK_OPS 2048
 
 /* Pages of a batch with n_ev_slots event slots, and the text capacity that always suffices:

@@ -69,7 +69,8 @@ class ReportArgs(ctypes.Structure):
                 ("text_total", ctypes.c_uint64), ("n_alns", ctypes.c_uint32), ("skip_codan", ctypes.c_uint32),
                 ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
                 ("n_ev_slots", ctypes.c_uint64), ("pages", ctypes.c_void_p), ("max_rec_ops", ctypes.c_uint32),
-                ("n_short", ctypes.c_uint32), ("hot_pbits", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("n_short", ctypes.c_uint32), ("hot_pbits", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("n_queries", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class CsTotals(ctypes.Structure):
@@ -228,6 +229,7 @@ def pack_cs(cs: str, offset: int, qlen: int):
 CS_REC = np.dtype([("q_total", "<i4"), ("t_total", "<i4"), ("n_ops", "<u4"), ("n_lits", "<u4"),
                    ("n_events_max", "<u4"), ("flags", "<u4"), ("text_bound", "<u8")])
 PACK_HOST, PACK_ACGT = 1, 2
+REPORT_BUILD_NEXT_STOP = 1  # pw_report_args.flags
 
 
 def pack_cs_gpu(cs_list, offsets, qlens, device: str = "cuda:0"):
@@ -467,19 +469,25 @@ def report_args(batch: HostBatch, dev: dict) -> ReportArgs:
     ql = batch.array("qlen")
     a.hot_pbits = 0 if _env_flag("PW_HOT32") else int(lib().pw_report_hot_pbits(int(ql.max()) if ql.size else 0,
                                                                                int(v.n_queries)))
+    a.n_queries = int(v.n_queries)
     return a
 
 
 def run_report(batch: HostBatch, dev: dict, stream_ptr: int) -> None:
-    """Launch pw_stop_table_build (unless -F/-N) + pw_report_events on device tensors in `dev`."""
+    """pw_report_events on device tensors in `dev`, the next-stop table built by the pass itself
+    (PW_REPORT_BUILD_NEXT_STOP; unless -F/-N) — or, with PW_NS_SEPARATE=1, by pw_stop_table_build
+    launched before it."""
     L = lib()
     v = batch.view
-    if not v.skip_codan:
-        rc = L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
-                                   int(v.n_queries), dev["next_stop"].data_ptr(), stream_ptr)
-        if rc != 0:
-            raise RuntimeError(f"pw_stop_table_build: {rc}")
     a = report_args(batch, dev)
+    if not v.skip_codan:
+        if _env_flag("PW_NS_SEPARATE"):
+            rc = L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                       int(v.n_queries), dev["next_stop"].data_ptr(), stream_ptr)
+            if rc != 0:
+                raise RuntimeError(f"pw_stop_table_build: {rc}")
+        else:
+            a.flags |= REPORT_BUILD_NEXT_STOP
     rc = L.pw_report_events(ctypes.byref(a), stream_ptr)
     if rc != 0:
         raise RuntimeError(f"pw_report_events: {rc}")

@@ -1444,6 +1444,8 @@ struct Work {
   v4u* bcarry;        // per entry: query / target / literal advance and event heads of the block
   v4u* berr;          // per entry (blocks >= 1): mismatch details {err, q_pos, query char, aligned char}
   uint32_t blk_cap;
+  uint32_t ns_grid;   // index's first workgroups that build next_stop (PW_REPORT_BUILD_NEXT_STOP), 0 = none
+  uint32_t clear_ctr; // index clears the counters (no memset launch: a batch without long records)
   uint64_t n_slots, n_chunks;
   uint64_t arena0;  // first arena byte in text (= n_chunks * PW_PAGE_BYTES)
 };
@@ -1501,6 +1503,8 @@ __host__ __device__ inline uint64_t work_layout(uint8_t* base, uint64_t n_slots,
     w->bcarry = reinterpret_cast<v4u*>(base + o_bcarry);
     w->berr = reinterpret_cast<v4u*>(base + o_berr);
     w->blk_cap = (uint32_t)(bcap < 0xFFFFFFF0ull ? bcap : 0xFFFFFFF0ull);
+    w->ns_grid = 0;
+    w->clear_ctr = 0;
     w->n_slots = n_slots;
     w->n_chunks = n_chunks;
     w->arena0 = n_chunks * (uint64_t)PW_PAGE_BYTES;
@@ -1573,6 +1577,78 @@ __device__ __forceinline__ void stage_small_tables(LDS SmallTables* dst, int tid
       d[offsetof(SmallTables, dig2) + 2 * i + 1] = (uint8_t)('0' + i % 10);
     }
   }
+}
+
+// ------------------------------------------------------------------ next-stop table
+// ns[p] = the first q >= p with q = p (mod 3) where codon Q[q, q+3) is a stop (kNoStop if none).
+// One 256-thread workgroup per query; tiles of 768 positions from the end.  Thread t owns the
+// three positions base + 3 * (255 - t) + f, so lanes in increasing order walk the tile
+// backwards: a DPP prefix-minimum over the lanes is the suffix minimum over positions, per frame
+// (positions 3j + f of a thread share the frame f + base mod 3); the four waves combine through
+// LDS, the tiles through a carry.  Workgroup b of nb takes queries b, b + nb, ... (its own launch,
+// pw_stop_table_build, or the first workgroups of index_kernel with PW_REPORT_BUILD_NEXT_STOP).
+__device__ __forceinline__ void stop_table_wg(const uint8_t* qseq, const uint64_t* qoff, const int32_t* qlen, uint32_t nq,
+                                              int32_t* ns, const LDS SmallTables* tp, uint32_t b, uint32_t nb) {
+  __shared__ int32_t wm[kWaves][3];
+  const int t = threadIdx.x, wv = t / kWave;
+  for (uint32_t qi = b; qi < nq; qi += nb) {
+    const uint8_t* R = qseq + qoff[qi];
+    int32_t* out = ns + qoff[qi];
+    const int L = qlen[qi];
+    int carry[3] = {kNoStop, kNoStop, kNoStop};
+    const int ntile = (L + 767) / 768;
+    for (int tile = ntile - 1; tile >= 0; tile--) {
+      const int pb = tile * 768 + 3 * (255 - t);
+      // five bytes from pb (indices clamped to L: the query is followed by zero bytes)
+      uint8_t bq[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) bq[q] = R[pb + q < L ? pb + q : L];
+      int sm[3];
+#pragma unroll
+      for (int f = 0; f < 3; f++) {
+        const int p = pb + f;
+        const int v = (p + 2 < L && translate(tp, bq[f], bq[f + 1], bq[f + 2]) == '.') ? p : kNoStop;
+        sm[f] = wave_min_incl(v);
+      }
+      if ((t & (kWave - 1)) == kWave - 1) {
+#pragma unroll
+        for (int f = 0; f < 3; f++) wm[wv][f] = sm[f];
+      }
+      __syncthreads();
+      // positions above this wave's: the waves before it in this tile, then the tiles above
+#pragma unroll
+      for (int f = 0; f < 3; f++) {
+        int above = carry[f];
+        for (int w2 = 0; w2 < wv; w2++) above = min(above, wm[w2][f]);
+        const int p = pb + f;
+        if (p < L) out[p] = min(sm[f], above);
+      }
+#pragma unroll
+      for (int f = 0; f < 3; f++)
+        for (int w2 = 0; w2 < kWaves; w2++) carry[f] = min(carry[f], wm[w2][f]);
+      __syncthreads();
+    }
+  }
+}
+__global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, const uint64_t* qoff,
+                                                         const int32_t* qlen, uint32_t nq, int32_t* ns) {
+  __shared__ SmallTables tab;
+  LDS SmallTables* tp = (LDS SmallTables*)&tab;
+  stage_small_tables(tp, threadIdx.x, 256);
+  __syncthreads();
+  stop_table_wg(qseq, qoff, qlen, nq, ns, tp, blockIdx.x, gridDim.x);
+}
+
+// index_kernel / index_pair_kernel's start: next_stop workgroups, the counters.  Returns the
+// workgroup's index among the decode workgroups (-1: it built next_stop and is done).
+__device__ __forceinline__ int index_prologue(const pw_report_args& A, const Work& W, const LDS SmallTables* tp) {
+  if (blockIdx.x < W.ns_grid) {
+    stop_table_wg(A.qseq, A.qoff, A.qlen, A.n_queries, const_cast<int32_t*>(A.next_stop), tp, blockIdx.x, W.ns_grid);
+    return -1;
+  }
+  // (render is the first kernel that uses ctr[0..2] and the arena counter: a memset launch less)
+  if (W.clear_ctr && blockIdx.x == W.ns_grid && threadIdx.x < 8) W.ctr[threadIdx.x] = 0u;
+  return (int)(blockIdx.x - W.ns_grid);
 }
 
 // ------------------------------------------------------------------ index_kernel
@@ -2007,10 +2083,11 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 // wavefronts (a record of 1-5 Mb walked by one wave would be the whole kernel's critical path), and
 // the padding slots of the last chunk (empty)
 __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
-                                                  LDS IndexWave* w, int lane, int wv, uint32_t stride, bool planned) {
+                                                  LDS IndexWave* w, int lane, int wv, uint32_t stride, bool planned,
+                                                  uint32_t bid) {
   if (planned) {
     const uint32_t nbl = W.ctr[3] < W.blk_cap ? W.ctr[3] : W.blk_cap;
-    for (uint32_t i = blockIdx.x * kWaves + wv; i < nbl; i += stride) {
+    for (uint32_t i = bid * kWaves + wv; i < nbl; i += stride) {
       const uint64_t e = W.blist[i];
       const uint32_t bai = (uint32_t)(e >> 32), k = (uint32_t)e;
       if (k == 0) continue;
@@ -2023,7 +2100,7 @@ __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const
     }
   }
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
-  if (blockIdx.x == 0)
+  if (bid == 0)
     for (uint64_t s = pad0 + threadIdx.x; s < pad1; s += kWave * kWaves) {
       hot_fn(W, s) = kNoEv;
       W.sflag[s] = 0;
@@ -2036,13 +2113,16 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, kWave * kWaves);
   __syncthreads();
+  const int bid_ = index_prologue(A, W, tp);
+  if (bid_ < 0) return;
+  const uint32_t bid = (uint32_t)bid_;
   const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   LDS IndexWave* w = (LDS IndexWave*)&iw[wv];
   // records ai, ai + stride, ...: the next record's head loads are issued before this record is
   // processed (its descriptor two records ahead), so their latency overlaps the work
-  const uint32_t stride = gridDim.x * kWaves;
+  const uint32_t stride = (gridDim.x - W.ns_grid) * kWaves;
   const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;  // plan_kernel ran
-  uint32_t ai = blockIdx.x * kWaves + wv;
+  uint32_t ai = bid * kWaves + wv;
   if (ai < A.n_alns) {
     // (indices past the batch are clamped to its last record: the loads stay unconditional)
     const uint32_t nm1 = A.n_alns - 1;
@@ -2073,7 +2153,7 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
       dn = dnn;
     }
   }
-  index_long_blocks(A, W, tp, w, lane, wv, stride, planned);
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned, bid);
 }
 
 // ------------------------------------------------------------------ index_kernel, two short records per wave
@@ -2328,13 +2408,16 @@ __global__ __launch_bounds__(kWave* kWaves, kPairOcc) void index_pair_kernel(pw_
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
   stage_small_tables(tp, threadIdx.x, kWave * kWaves);
   __syncthreads();
+  const int bid_ = index_prologue(A, W, tp);
+  if (bid_ < 0) return;
+  const uint32_t bid = (uint32_t)bid_;
   const int lane = threadIdx.x & (kWave - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int hl = lane & 31;
   LDS IndexWave* w = (LDS IndexWave*)&iw[wv];
-  const uint32_t stride = gridDim.x * kWaves;
+  const uint32_t stride = (gridDim.x - W.ns_grid) * kWaves;
   const bool planned = A.max_rec_ops == 0 || A.max_rec_ops > (uint32_t)kBlkOps;
   const uint32_t nu = (A.n_alns + 1) / 2;  // units of two records
-  uint32_t u = blockIdx.x * kWaves + wv;
+  uint32_t u = bid * kWaves + wv;
   if (u < nu) {
     // the next unit's heads are loaded while this one is processed
     PairHead cur;
@@ -2359,7 +2442,7 @@ __global__ __launch_bounds__(kWave* kWaves, kPairOcc) void index_pair_kernel(pw_
       }
     }
   }
-  index_long_blocks(A, W, tp, w, lane, wv, stride, planned);
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned, bid);
 }
 
 // ------------------------------------------------------------------ long records: plan + carries
@@ -3223,61 +3306,6 @@ __global__ __launch_bounds__(256) void finalize_kernel(pw_report_args A, Work W)
   if (ai < A.n_alns) finalize_record(A, W, ai);
 }
 
-// ------------------------------------------------------------------ next-stop table
-// ns[p] = the first q >= p with q = p (mod 3) where codon Q[q, q+3) is a stop (kNoStop if none).
-// One 256-thread workgroup per query; tiles of 768 positions from the end.  Thread t owns the
-// three positions base + 3 * (255 - t) + f, so lanes in increasing order walk the tile
-// backwards: a DPP prefix-minimum over the lanes is the suffix minimum over positions, per frame
-// (positions 3j + f of a thread share the frame f + base mod 3); the four waves combine through
-// LDS, the tiles through a carry.
-__global__ __launch_bounds__(256) void stop_table_kernel(const uint8_t* qseq, const uint64_t* qoff,
-                                                         const int32_t* qlen, uint32_t nq, int32_t* ns) {
-  __shared__ SmallTables tab;
-  __shared__ int32_t wm[kWaves][3];
-  const int t = threadIdx.x, wv = t / kWave;
-  LDS SmallTables* tp = (LDS SmallTables*)&tab;
-  stage_small_tables(tp, t, 256);
-  __syncthreads();
-  for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
-    const uint8_t* R = qseq + qoff[qi];
-    int32_t* out = ns + qoff[qi];
-    const int L = qlen[qi];
-    int carry[3] = {kNoStop, kNoStop, kNoStop};
-    const int ntile = (L + 767) / 768;
-    for (int tile = ntile - 1; tile >= 0; tile--) {
-      const int pb = tile * 768 + 3 * (255 - t);
-      // five bytes from pb (indices clamped to L: the query is followed by zero bytes)
-      uint8_t b[5];
-#pragma unroll
-      for (int q = 0; q < 5; q++) b[q] = R[pb + q < L ? pb + q : L];
-      int s[3];
-#pragma unroll
-      for (int f = 0; f < 3; f++) {
-        const int p = pb + f;
-        const int v = (p + 2 < L && translate(tp, b[f], b[f + 1], b[f + 2]) == '.') ? p : kNoStop;
-        s[f] = wave_min_incl(v);
-      }
-      if ((t & (kWave - 1)) == kWave - 1) {
-#pragma unroll
-        for (int f = 0; f < 3; f++) wm[wv][f] = s[f];
-      }
-      __syncthreads();
-      // positions above this wave's: the waves before it in this tile, then the tiles above
-#pragma unroll
-      for (int f = 0; f < 3; f++) {
-        int above = carry[f];
-        for (int w2 = 0; w2 < wv; w2++) above = min(above, wm[w2][f]);
-        const int p = pb + f;
-        if (p < L) out[p] = min(s[f], above);
-      }
-#pragma unroll
-      for (int f = 0; f < 3; f++)
-        for (int w2 = 0; w2 < kWaves; w2++) carry[f] = min(carry[f], wm[w2][f]);
-      __syncthreads();
-    }
-  }
-}
-
 // ------------------------------------------------------------------ per-genome tables
 // One row per target sequence: alignments, event lines, aligned target bases (the tables the
 // multi-GPU driver all-gathers).  A thread per record, atomics into the rows.
@@ -3333,7 +3361,13 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
       (!args->text && args->text_total))
     return PW_E_ARG;
   if (!args->skip_codan && !args->next_stop) return PW_E_ARG;
-  if (args->n_alns == 0) return PW_OK;
+  const bool build_ns = (args->flags & PW_REPORT_BUILD_NEXT_STOP) && !args->skip_codan;
+  if (args->n_alns == 0) {  // (the table is still built when asked for)
+    if (build_ns && args->n_queries)
+      return pw_stop_table_build(args->qseq, args->qoff, args->qlen, args->n_queries, const_cast<int32_t*>(args->next_stop),
+                                 stream);
+    return PW_OK;
+  }
   const uint64_t need = pw_report_workspace_bytes(args->n_ev_slots, args->n_alns);
   if (!args->workspace || args->workspace_bytes < need || ((uintptr_t)args->workspace & 255)) return PW_E_ARG;
   // per-lane windows are 16-byte loads, literal words 4-byte loads, pages 16-byte stores
@@ -3357,9 +3391,14 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   const uint32_t nwave = pw::kWaves;
   uint64_t ig = (args->n_alns + nwave - 1) / nwave;
   const bool planned = args->max_rec_ops == 0 || args->max_rec_ops > (uint32_t)pw::kBlkOps;
-  // the counters (a memset launch: without it index_kernel starts at once and the next-stop table
-  // built beside it on a side stream slows it down — index 127 -> 143 us, table 29 -> 66 us)
-  if (hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;
+  // the next-stop table by index's first workgroups (one per query, 4096 at most), and the
+  // counters: a memset launch when plan_kernel runs first (it counts blocks in ctr[3]), else
+  // cleared by index itself (round 5: the memset dispatch and the side stream's event wait before
+  // render were ~11 us of the cfg2 pass)
+  W.ns_grid = build_ns ? (args->n_queries < 4096u ? args->n_queries : 4096u) : 0u;
+  W.clear_ctr = planned ? 0u : 1u;
+  if (build_ns && args->n_queries && !args->qseq) return PW_E_ARG;
+  if (planned && hipMemsetAsync(args->workspace, 0, 64, st) != hipSuccess) return PW_E_HIP;
   // (four rounds at 5 waves/SIMD — round-4 sweep on cfg2, same-box pairs: 10 / 15 / 20 / 30 per
   // CU 127.9-128.8 / 128.3 / 125.9-126.1 / 128.7 us; round 2 found 16 worse than 10 before the
   // segment and prefetch changes); with long records (planned) the blocks of 1.. are spread over a
@@ -3375,10 +3414,11 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   // 4 / 12 1,427 / 1,421, 10 — index_kernel's, 2.5 rounds here — 1,474-1,481, 16 1,458)
   if (args->n_short && (uint64_t)args->n_short * 4 >= (uint64_t)args->n_alns * 3)
     hipLaunchKernelGGL(pw::index_pair_kernel,
-                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 8u)),
+                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 8u) +
+                            W.ns_grid),
                        dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   else
-    hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+    hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig + W.ns_grid), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
     uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
