@@ -235,6 +235,54 @@ PATCHES["occ4q2"] = _QALIAS2 + PATCHES["occ4"]
 # index_kernel at 4 waves/SIMD (128 VGPRs; product: 5)
 PATCHES["idx4"] = [("constexpr int kIndexOcc = 5;", "constexpr int kIndexOcc = 4;")]
 
+# render with the next chunk's inputs issued before this chunk's line is built (one whole
+# iteration of lead instead of the copy-out's): the Hot records three chunks ahead, the query
+# starts two ahead (round 5, timing + register experiment)
+PATCHES["early"] = [
+    ("""  HotRaw<kH16> hn = load_hot<kH16>(W, c + nw, lane);
+  RenderPre pre;
+  render_pre<kH16>(A, W, h, c * kWave + (uint64_t)lane, skip, pre);""",
+     """  HotRaw<kH16> hn = load_hot<kH16>(W, c + nw, lane);
+  if constexpr (kH16) qn = load_qinfo(A, W, hn);
+  HotRaw<kH16> hn2 = load_hot<kH16>(W, c + 2 * nw, lane);
+  RenderPre pre;
+  render_pre<kH16>(A, W, h, c * kWave + (uint64_t)lane, skip, pre);"""),
+    ("""    render_pre_ready<kH16>(pre);
+    if constexpr (kH16) {
+      // the next chunk's query starts / lengths (its records came in with this chunk's inputs),
+      // consumed when it is decoded after this chunk's lines; this chunk's first literal bytes
+      qn = load_qinfo(A, W, hn);
+      lit8(h.ls, pre.lw[0], pre.lw[1], pre.lw[2], h.l0, h.l1);
+    }""",
+     """    render_pre_ready<kH16>(pre);
+    if constexpr (kH16) lit8(h.ls, pre.lw[0], pre.lw[1], pre.lw[2], h.l0, h.l1);"""),
+    ("""    const v4u t0 = pre.t0, t1 = pre.t1;
+    const int ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
+    const int qlo = pre.qlo, n_cur = pre.n;""",
+     """    const v4u t0 = pre.t0, t1 = pre.t1;
+    const int ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
+    const int qlo = pre.qlo, n_cur = pre.n;
+    const uint32_t ai_cur = pre.ai;
+    // the next chunk: decoded and its inputs issued now, in flight during this chunk's line
+    if constexpr (kH16) pin(qn);
+    const Hot hx = decode_hot<kH16>(W, hn, qn, c + nw < W.n_chunks);
+    render_pre<kH16>(A, W, hx, (c + nw) * kWave + (uint64_t)lane, skip, pre);
+    if constexpr (kH16) qn = load_qinfo(A, W, hn2);
+    hn = hn2;
+    hn2 = load_hot<kH16>(W, c + 3 * nw, lane);"""),
+    ("""    const uint32_t fn_cur = h.fn;
+    const uint32_t ai_cur = pre.ai;
+    // the next chunk's inputs load behind this one's output
+    if constexpr (kH16) pin(qn);
+    h = decode_hot<kH16>(W, hn, qn, c + nw < W.n_chunks);
+    hn = load_hot<kH16>(W, c + 2 * nw, lane);
+    render_pre<kH16>(A, W, h, (c + nw) * kWave + (uint64_t)lane, skip, pre);""",
+     """    const uint32_t fn_cur = h.fn;
+    h = hx;"""),
+]
+
+PATCHES["early2"] = PATCHES["early"] + [("constexpr int kRenderOcc = 3;", "constexpr int kRenderOcc = 2;")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
