@@ -232,6 +232,48 @@ def test_report_events_after_side_stream(built, tmp_path):
         assert open(outp, "rb").read() == want
 
 
+def test_report_builds_next_stop_in_pass(built, tmp_path):
+    """PW_REPORT_BUILD_NEXT_STOP: the pass's first kernel builds the next-stop table itself (its
+    first workgroups) and clears the pass counters — the table equals pw_stop_table_build's, the
+    report equals the oracle's, twice on the same buffers (a stale table and stale counters from
+    the previous pass are overwritten), with 16- and 32-byte event records; and a batch of no
+    records still gets its table."""
+    import torch
+    fa, paf = synth_paf(tmp_path, 2, seed=13, scale=0.05)
+    b = pw.HostBatch(fa, paf, pw.FLAG_G | pw.FLAG_C)
+    v = b.view
+    dev = pw.stage_batch(b, "cuda:0")
+    L = pw.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    _, want, _ = run([ORACLE, "-G", "-C", "-r", fa, paf])
+    dev["next_stop"].fill_(-7)  # (the padding between queries is never written)
+    assert L.pw_stop_table_build(dev["qseq"].data_ptr(), dev["qoff"].data_ptr(), dev["qlen"].data_ptr(),
+                                 int(v.n_queries), dev["next_stop"].data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    ref_ns = dev["next_stop"].clone()
+    for it, hot32 in enumerate((False, False, True)):
+        dev["next_stop"].fill_(-7)
+        dev["work"][:64].fill_(0xFF)  # stale counters: the pass must clear them
+        a = pw.report_args(b, dev)
+        assert a.max_rec_ops <= 2048  # (no plan pass: index clears the counters)
+        if hot32:
+            a.hot_pbits = 0
+        a.flags = pw.REPORT_BUILD_NEXT_STOP
+        assert L.pw_report_events(pw.ctypes.byref(a), s) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dev["next_stop"], ref_ns), it
+        outp = str(tmp_path / f"inpass{it}.txt")
+        assert b.write_report_from(dev, outp) == 0
+        assert open(outp, "rb").read() == want, it
+    dev["next_stop"].fill_(-7)
+    a = pw.report_args(b, dev)
+    a.n_alns = 0
+    a.flags = pw.REPORT_BUILD_NEXT_STOP
+    assert L.pw_report_events(pw.ctypes.byref(a), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dev["next_stop"], ref_ns)
+
+
 # ---------------------------------------------------------------- GapAssem consensus
 def ga_same(layout, tmp_path, extra=(), writers=True):
     """gapassem_consensus (GapAssem C++ API on the GPU) against the oracle: exit code, stderr, the
