@@ -3,7 +3,8 @@ tools/abl_build/<name>/lib for tools/pk_sweep.sh (PWASM_LIB):
   cur      the working copy
   head     pw_pack.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
   pkg<N>   pack_cs_kernel grid capped at N workgroups per CU (product: 64)
-  k<N>     N records per task (product: 8)
+  stream / s5 / s6 / s7  the stream packer (profiles/variants/pack_stream_tasks.patch), held to 5-7 waves/SIMD
+  k<N>     N records per task (stream patch builds; 8)
   w8       the kernel held to 8 waves/SIMD (amdgpu_waves_per_eu: SGPRs spilled to VGPR lanes)
 Usage: python tools/exp_pack_variants.py [names...]"""
 import os
@@ -29,6 +30,16 @@ def make(name):
         old = "__global__ __launch_bounds__(256) void pack_cs_kernel"
         assert old in s
         s = s.replace(old, "__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void pack_cs_kernel")
+    elif name in ("stream", "s5", "s6", "s7"):  # profiles/variants/pack_stream_tasks.patch (+ waves/SIMD held)
+        os.makedirs(TMP, exist_ok=True)
+        p = os.path.join(TMP, f"pack_{name}_base.hip")
+        open(p, "w").write(s)
+        subprocess.run(["patch", "-s", p, os.path.join(REPO, "profiles/variants/pack_stream_tasks.patch")], check=True)
+        s = open(p).read()
+        if name != "stream":
+            old = "__global__ __launch_bounds__(256) void pack_cs_kernel"
+            assert old in s
+            s = s.replace(old, f"__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu({name[1]}, {name[1]}))) void pack_cs_kernel")
     elif name.startswith("k") and name[1:].isdigit():  # records per task (product: 8)
         old = "constexpr uint32_t kTaskRecs = 8;"
         assert old in s
