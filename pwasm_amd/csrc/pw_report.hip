@@ -73,6 +73,11 @@ constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
 static_assert(kLine + kLSlack <= 148, "line buffer stride");
 constexpr uint32_t kDropOff = 0xFFFFFF00u;  // a buffer-store offset past any range: the store is dropped
+// the report text is written non-temporal (cache policy nt): no kernel reads it again, and left to
+// the default policy its 303 MB per cfg2 pass linger dirty in the caches the next kernels (and the
+// next pass's index / tctx) read through — round 5, same call: render 213 -> 197 us, index 126 ->
+// 117, tctx 75 -> 71, pass 0.439 -> 0.408 ms (sc1, write-through that drops the line: no change)
+constexpr int kTextPolicy = 2;
 constexpr int kLStride = 148;  // line buffer stride (37 dwords, odd: lanes at the same line position hit 32 banks)
 // (render's copy-out builds an in-place page, <= PW_PAGE_BYTES, over the wave's line buffers)
 static_assert(kWave * kLStride >= PW_PAGE_BYTES, "the LDS page image must fit the wave's line buffers");
@@ -2948,12 +2953,12 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
 #pragma unroll
         for (int q = 0; q < 8; q++) {  // (PW_PAGE_BYTES / 1024 rows; rows past B are dropped)
           const uint32_t o = 1024u * (uint32_t)q + 16u * (uint32_t)lane;
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const LDS v4u*>(img + o), rs, o < B ? o : kDropOff, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const LDS v4u*>(img + o), rs, o < B ? o : kDropOff, 0, kTextPolicy);
         }
       } else {  // an arena page: every lane stores its own groups
 #pragma unroll
         for (int j = 6; j >= 0; j--)
-          __builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, kTextPolicy);
       }
     }
     wave_sync();

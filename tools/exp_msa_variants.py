@@ -110,6 +110,12 @@ def make(name):
     elif name == "nogather":  # no window reads at all (the group bytes are a constant)
         s = sub(s, """            const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);""",
                 """            const uint32_t s4 = 0x41434754u + (uint32_t)(src & 0) + (uint32_t)(p == nullptr);""")
+    elif name == "ofs_nt":  # row_chunk_sums' ofs loads non-temporal (once-read stream)
+        s = sub(s, "  p.q0 = src[0];\n  p.q1 = src[1];", "  p.q0 = __builtin_nontemporal_load(src);\n  p.q1 = __builtin_nontemporal_load(src + 1);")
+    elif name == "seq_nt":  # tile_counts' base-window loads non-temporal
+        for k in ("o + 16u * (uint32_t)lane, 0, 0);", "o + 1024u + 16u * (uint32_t)lane, 0, 0);",
+                  "o + 2048u + 16u * (uint32_t)(lane & 7), 0, 0);"):
+            s = sub(s, k, k.replace(", 0, 0);", ", 0, 2);"))
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout

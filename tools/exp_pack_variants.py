@@ -40,6 +40,12 @@ def make(name):
             old = "__global__ __launch_bounds__(256) void pack_cs_kernel"
             assert old in s
             s = s.replace(old, f"__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu({name[1]}, {name[1]}))) void pack_cs_kernel")
+    elif name == "pk_nt":  # cs text loads non-temporal
+        for k in ("  d0 = *reinterpret_cast<const uint32_t*>(text + (a0 < last ? a0 : last));",
+                  "  d1 = *reinterpret_cast<const uint32_t*>(text + (a0 + 4 < last ? a0 + 4 : last));"):
+            assert k in s
+            s = s.replace(k, k.replace("*reinterpret_cast<const uint32_t*>(", "__builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(").replace(";", ");", 1) if False else
+                          k.replace("= *reinterpret_cast<const uint32_t*>(text + ", "= __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(text + ").replace("));", ")));"))
     elif name.startswith("k") and name[1:].isdigit():  # records per task (product: 8)
         old = "constexpr uint32_t kTaskRecs = 8;"
         assert old in s

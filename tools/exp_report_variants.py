@@ -283,6 +283,26 @@ PATCHES["early"] = [
 
 PATCHES["early2"] = PATCHES["early"] + [("constexpr int kRenderOcc = 3;", "constexpr int kRenderOcc = 2;")]
 
+# render's text stores with a cache policy (round 5): nt (aux 2) or sc1 (aux 16: write-through,
+# the line leaves the XCD's L2 — the text is never read again on the GPU)
+for _nm, _aux in (("txt_nt", 2), ("txt_sc1", 16)):
+    PATCHES[_nm] = [
+        ("__builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const LDS v4u*>(img + o), rs, o < B ? o : kDropOff, 0, 0);",
+         f"__builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const LDS v4u*>(img + o), rs, o < B ? o : kDropOff, 0, {_aux});"),
+        ("__builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, 0);",
+         f"__builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, {_aux});")]
+
+# non-temporal stores of index's 16-byte event records / tctx's tx records (round 5)
+PATCHES["hot_nt"] = [("    p[0] = (v4u){h.fn, qi << W.hot_pbits | (uint32_t)h.qp, (uint32_t)h.tloc, h.ls};",
+                      "    __builtin_nontemporal_store((v4u){h.fn, qi << W.hot_pbits | (uint32_t)h.qp, (uint32_t)h.tloc, h.ls}, p);")]
+PATCHES["tx_nt"] = [("      dtx[0] = t0;\n      dtx[1] = t1;", "      __builtin_nontemporal_store(t0, dtx);\n      __builtin_nontemporal_store(t1, dtx + 1);")]
+
+# index's op-word loads non-temporal (a once-read stream for index)
+PATCHES["ops_nt"] = [
+    ("  p.w0 = *((uint32_t)lane < d.n_ops ? ops + lane : dummy);\n  p.w1 = *((uint32_t)(lane + 64) < d.n_ops ? ops + lane + 64 : dummy);",
+     "  p.w0 = __builtin_nontemporal_load((uint32_t)lane < d.n_ops ? ops + lane : dummy);\n  p.w1 = __builtin_nontemporal_load((uint32_t)(lane + 64) < d.n_ops ? ops + lane + 64 : dummy);"),
+    ("        uint32_t w = ops[idx < nseg ? sb + idx : sb];", "        uint32_t w = __builtin_nontemporal_load(ops + (idx < nseg ? sb + idx : sb));")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
