@@ -879,12 +879,14 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
     }
   }
   __syncthreads();
-  // the tile's counters: [col][6] rows in memory, coalesced
+  // the tile's counters: [col][6] rows in memory, coalesced — non-temporal stores, as the
+  // consensus below: no later kernel of the step reads them (round 5: tile_counts -1 us,
+  // row_chunk_sums of the next step -1 us)
   const int cw = c1 - c0;
   int32_t* dst = A.counts + (int64_t)c0 * 6;
   for (int i = tid; i < cw * 6; i += 64 * kCntWaves) {
     const int c = i / 6, f = i - 6 * c;
-    dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];
+    __builtin_nontemporal_store((int32_t)tab[f * kCntW + cnt_swz(c)], dst + i);
   }
   if (call) {  // pw_msa_columns (all rows in this launch): the call step from the same table
     const int zlo = A.minmax[0], zhi = A.minmax[1];
@@ -895,8 +897,9 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
 #pragma unroll
       for (int f = 0; f < 6; f++) v[f] = (int)tab[f * kCntW + cnt_swz(c)];
       const uint8_t best = best_char(v);
-      A.consensus[c0 + c] = best;
-      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) cons_star[c0 + c - zlo] = best == '-' ? (uint8_t)'*' : best;
+      __builtin_nontemporal_store(best, A.consensus + c0 + c);
+      if (cons_star && c0 + c >= zlo && c0 + c <= zhi)
+        __builtin_nontemporal_store(best == '-' ? (uint8_t)'*' : best, cons_star + c0 + c - zlo);
       if (best == 0 && c0 + c >= zlo && c0 + c <= zhi) atomicMin(&A.minmax[3], c0 + c);
     }
   }

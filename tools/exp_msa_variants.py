@@ -116,6 +116,10 @@ def make(name):
         for k in ("o + 16u * (uint32_t)lane, 0, 0);", "o + 1024u + 16u * (uint32_t)lane, 0, 0);",
                   "o + 2048u + 16u * (uint32_t)(lane & 7), 0, 0);"):
             s = sub(s, k, k.replace(", 0, 0);", ", 0, 2);"))
+    elif name == "cnt_nt":  # tile_counts' counter table / consensus stores non-temporal
+        s = sub(s, "    dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];", "    __builtin_nontemporal_store((int32_t)tab[f * kCntW + cnt_swz(c)], dst + i);")
+        s = sub(s, "      A.consensus[c0 + c] = best;\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) cons_star[c0 + c - zlo] = best == '-' ? (uint8_t)'*' : best;",
+                "      __builtin_nontemporal_store(best, A.consensus + c0 + c);\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) __builtin_nontemporal_store(best == '-' ? (uint8_t)'*' : best, cons_star + c0 + c - zlo);")
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout
