@@ -303,6 +303,11 @@ PATCHES["ops_nt"] = [
      "  p.w0 = __builtin_nontemporal_load((uint32_t)lane < d.n_ops ? ops + lane : dummy);\n  p.w1 = __builtin_nontemporal_load((uint32_t)(lane + 64) < d.n_ops ? ops + lane + 64 : dummy);"),
     ("        uint32_t w = ops[idx < nseg ? sb + idx : sb];", "        uint32_t w = __builtin_nontemporal_load(ops + (idx < nseg ? sb + idx : sb));")]
 
+# render's Hot record loads / tx loads non-temporal (round 5)
+PATCHES["hotld_nt"] = [("  r.a = p[0];\n  if constexpr (!kH16) r.b = p[1];",
+                        "  r.a = __builtin_nontemporal_load(p);\n  if constexpr (!kH16) r.b = __builtin_nontemporal_load(p + 1);")]
+PATCHES["txld_nt"] = [("    p.t0 = tp4[0];\n    p.t1 = tp4[1];", "    p.t0 = __builtin_nontemporal_load(tp4);\n    p.t1 = __builtin_nontemporal_load(tp4 + 1);")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
