@@ -1053,8 +1053,14 @@ __device__ __forceinline__ int emit_event(S& k, const R& r, const EvIn& in, bool
 // per codon index) and appended to the lane's line buffer as whole dwords — the partial dword at
 // the line end is read back and merged with v_perm, so a 16-byte field costs one read, five perms
 // and three stores instead of sixteen byte stores.  Same bytes as emit_event (pafreport.cpp:886-953).
+// The fast path's line buffers and query windows are lane-interleaved: dword k of a lane's buffer
+// is at k * kTS dwords + lane (kTS = 64: a wave's buffers as rows of 256 bytes).  Every lane's
+// dword access then hits bank lane mod 32 whatever its line position or window offset — with
+// per-lane contiguous buffers those positions are data-dependent and a wave's dword accesses met
+// 2-4-way bank conflicts (render: 37 % of its LDS cycles).
+constexpr int kTS = kWave;
 struct DLine {
-  LDS uint8_t* buf;  // the lane's line buffer (4-byte aligned, kLine + kLSlack bytes)
+  LDS uint8_t* buf;  // the lane's dword column of the wave's interleaved line buffers (kLine + kLSlack bytes)
   int pos;
 };
 // (a line that grows past kLine is rewritten by fixup_kernel: its appends are folded onto the slack)
@@ -1065,7 +1071,7 @@ __device__ __forceinline__ void app(DLine& L, const uint32_t (&f)[D], int n) {
   const int p = L.pos;
   const int a = min(p & ~3, kAppMax);
   const uint32_t sh = (uint32_t)p & 3u;
-  LDS uint32_t* d = reinterpret_cast<LDS uint32_t*>(L.buf + a);
+  LDS uint32_t* d = reinterpret_cast<LDS uint32_t*>(L.buf) + (a >> 2) * kTS;
   const uint32_t cur = d[0];  // bytes [a, p) of the line
   // result byte j of dword i = stream byte 4i + j - sh: selector 4 - sh + j over {f[i], f[i - 1]};
   // dword 0 keeps its first sh bytes from cur
@@ -1078,7 +1084,7 @@ __device__ __forceinline__ void app(DLine& L, const uint32_t (&f)[D], int n) {
   for (int i = 1; i < D; i++) g[i] = __builtin_amdgcn_perm(f[i], f[i - 1], sel);
   g[D] = __builtin_amdgcn_perm(0u, f[D - 1], sel);
 #pragma unroll
-  for (int i = 0; i <= D; i++) d[i] = g[i];
+  for (int i = 0; i <= D; i++) d[i * kTS] = g[i];
   L.pos = p + n;
 }
 // OR the bytes of w into img at byte offset k (k + the bytes w uses <= 4N)
@@ -1096,14 +1102,15 @@ __device__ __forceinline__ uint32_t keep32(uint32_t v, int n) {  // bytes [0, n)
 __device__ __forceinline__ uint64_t keep64(uint64_t v, int n) {  // bytes [0, n) of v (n clamped to [0, 8])
   return n >= 8 ? v : (n <= 0 ? 0ull : (v & ((1ull << (8 * n)) - 1ull)));
 }
-// N dwords of an LDS window from byte offset off (off >= 0; reads one dword past them)
+// N dwords of a lane-interleaved LDS window (qw: the lane's column) from byte offset off (off >=
+// -8; reads one dword past them)
 template <int N>
 __device__ __forceinline__ void lds_img(const LDS uint8_t* qw, int off, uint32_t (&o)[N]) {
-  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw + (off & ~3));
+  const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(qw) + (off >> 2) * kTS;
   const uint32_t sh = (uint32_t)off & 3u;
   uint32_t d[N + 1];
 #pragma unroll
-  for (int i = 0; i <= N; i++) d[i] = p[i];
+  for (int i = 0; i <= N; i++) d[i] = p[i * kTS];
 #pragma unroll
   for (int i = 0; i < N; i++) o[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
 }
@@ -2734,15 +2741,45 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       qn = load_qinfo(A, W, hn);
       lit8(h.ls, pre.lw[0], pre.lw[1], pre.lw[2], h.l0, h.l1);
     }
-#pragma unroll
-    for (int q = 0; q < kQWin / 16; q++) {
-      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
-      *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};
-    }
     const v4u t0 = pre.t0, t1 = pre.t1;
     const int ns_pre = pre.ns_ok ? (int)pre.ns_raw : kNsNone;
     const int qlo = pre.qlo, n_cur = pre.n;
     const Hot& hc = h;
+    // the fast instantiation when every active lane's reads are in its registers / window: A/C/G/T,
+    // rloc >= 4 (r_trloc = 3 * (rloc / 3 - 1) >= 0 with rloc - r_trloc in 3..5, and the RCTX
+    // window rloc - 4 unclipped; the window starts at max(rloc - 8, 0) rounded down to 16, so it
+    // covers every query byte in [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8
+    // bases, deletions of <= 12 (the largest read, the tail image at r_trloc + deletion, ends by
+    // rloc + 25).  (An insertion's modseq tail image starts at r_trloc - n, up to 8 bytes before
+    // the lane's window: those bytes are LDS of the wave's line buffers, read and masked off.)
+    // (and numbers below 10^8: emit_fast's decimal conversion)
+    const int rlc = event_rloc(hc.L, (hc.fn >> 29) & 1u, hc.fn >> 30, hc.qp, n_cur);
+    bool fast;
+    {
+      const uint32_t typ = hc.fn >> 30;
+      const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
+      fast = !act || ((hc.fn & kFnAcgt) && rlc >= 4 && hc.L >= 9 && hc.L < 100000000 && hc.tloc < 99999999 &&
+                      (typ == PW_OP_SUB ? (n_cur <= 4 && rt + 9 <= hc.L) : n_cur <= (typ == PW_OP_INS ? 8 : 12)));
+    }
+    // (uniform) the wave's line buffers and windows lane-interleaved (emit_fast) or per lane
+    // (emit_event's byte sinks)
+    const bool ilv = __ballot(!fast) == 0;
+    if (ilv) {
+      LDS uint32_t* q4 = reinterpret_cast<LDS uint32_t*>(w->qw) + lane;
+#pragma unroll
+      for (int q = 0; q < kQWin / 16; q++) {
+        q4[(4 * q) * kTS] = pre.q[q].x;
+        q4[(4 * q + 1) * kTS] = pre.q[q].y;
+        q4[(4 * q + 2) * kTS] = pre.q[q].z;
+        q4[(4 * q + 3) * kTS] = pre.q[q].w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kQWin / 16; q++) {
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q) = (v2u){pre.q[q].x, pre.q[q].y};
+        *reinterpret_cast<LDS v2u*>(my_qw + 16 * q + 8) = (v2u){pre.q[q].z, pre.q[q].w};
+      }
+    }
     int linelen = 0;
     if (act) {
       const uint32_t typ = hc.fn >> 30;
@@ -2789,24 +2826,12 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       k.line = my_line;
       k.pos = 0;
       int rel = 0;
-      // the fast instantiation when every active lane's reads are in its registers / window: A/C/G/T,
-      // rloc >= 4 (r_trloc = 3 * (rloc / 3 - 1) >= 0 with rloc - r_trloc in 3..5, and the RCTX
-      // window rloc - 4 unclipped; the window starts at max(rloc - 8, 0) rounded down to 16, so it
-      // covers every query byte in [rloc - 8, rloc + 25]), S runs of <= 4, insertions of <= 8
-      // bases, deletions of <= 12 (the largest read, the tail image at r_trloc + deletion, ends by
-      // rloc + 25).  (An insertion's modseq tail image starts at r_trloc - n, up to 8 bytes before
-      // the lane's window: those bytes are LDS of the wave's line buffers, read and masked off.)
-      const int rlc = event_rloc(r.L, rev, typ, hc.qp, n);
-      const int rt = rlc >= 3 ? 3 * (rlc / 3 - 1) : 0;
-      // (and numbers below 10^8: emit_fast's decimal conversion)
-      const bool fast = r.acgt && rlc >= 4 && r.L >= 9 && r.L < 100000000 && hc.tloc < 99999999 &&
-                        (typ == PW_OP_SUB ? (n <= 4 && rt + 9 <= r.L) : n <= (typ == PW_OP_INS ? 8 : 12));
       int merr;
-      if (__ballot(!fast) == 0) {
+      if (ilv) {
         DLine dl;
-        dl.buf = my_line;
+        dl.buf = w->line + 4 * lane;
         dl.pos = 0;
-        merr = emit_fast(dl, my_qw, qlo, tp, in, rev, r.L, hc.l0, hc.l1, r.NS, skip, rel);
+        merr = emit_fast(dl, w->qw + 4 * lane, qlo, tp, in, rev, r.L, hc.l0, hc.l1, r.NS, skip, rel);
         linelen = dl.pos;
       } else {
         merr = emit_event(k, r, in, skip, rel);
@@ -2908,17 +2933,12 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       const uint32_t sh = my_off & 3u, a0 = my_off & ~3u;
       // this line's bytes in the dword at floor4(my_off + linelen): [linelen - t, linelen), t of them
       const uint32_t t = (my_off + (uint32_t)linelen) & 3u;
-      uint32_t tail;
-      {
-        const int tb = min(linelen - (int)t, kLine);
-        const LDS uint32_t* tp4 = reinterpret_cast<const LDS uint32_t*>(my_line + (tb & ~3));
-        tail = __builtin_amdgcn_alignbyte(tp4[1], tp4[0], (uint32_t)tb & 3u) & (uint32_t)((1ull << (8 * t)) - 1ull);
-      }
-      const uint64_t below = ne & ((1ull << lane) - 1ull);
-      const int prev = below ? 63 - __builtin_clzll(below) : lane;
-      const uint32_t ptail = (uint32_t)__shfl((int)tail, prev, kWave) & (uint32_t)((1ull << (8 * sh)) - 1ull);
       uint32_t Lw[28];
-      {
+      if (ilv) {  // (uniform) lane-interleaved line buffers
+        const LDS uint32_t* l4 = reinterpret_cast<const LDS uint32_t*>(w->line) + lane;
+#pragma unroll
+        for (int k = 0; k < 28; k++) Lw[k] = l4[k * kTS];
+      } else {
         const LDS v4a4* lp4 = reinterpret_cast<const LDS v4a4*>(my_line);  // (4-byte aligned: 148-byte stride)
 #pragma unroll
         for (int q = 0; q < 7; q++) {
@@ -2926,6 +2946,25 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
           Lw[4 * q] = v.x, Lw[4 * q + 1] = v.y, Lw[4 * q + 2] = v.z, Lw[4 * q + 3] = v.w;
         }
       }
+      uint32_t tail;
+      {
+        // (an empty line's tail is never used: tb < 0 reads dword 0)
+        const int tb = min(linelen - (int)t, kLine);
+        uint32_t d0, d1;
+        if (ilv) {
+          const LDS uint32_t* tp4 = reinterpret_cast<const LDS uint32_t*>(w->line) + lane + (max(tb, 0) >> 2) * kTS;
+          d0 = tp4[0];
+          d1 = tp4[kTS];
+        } else {
+          const LDS uint32_t* tp4 = reinterpret_cast<const LDS uint32_t*>(my_line + (tb & ~3));
+          d0 = tp4[0];
+          d1 = tp4[1];
+        }
+        tail = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)tb & 3u) & (uint32_t)((1ull << (8 * t)) - 1ull);
+      }
+      const uint64_t below = ne & ((1ull << lane) - 1ull);
+      const int prev = below ? 63 - __builtin_clzll(below) : lane;
+      const uint32_t ptail = (uint32_t)__shfl((int)tail, prev, kWave) & (uint32_t)((1ull << (8 * sh)) - 1ull);
       const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);
       const int kmax = linelen > 0 ? ((int)sh + ln - 1) >> 2 : -1;  // last dword (from a0) holding a line byte
       const int jmax = kmax >> 2;

@@ -120,6 +120,9 @@ def make(name):
         s = sub(s, "    dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];", "    __builtin_nontemporal_store((int32_t)tab[f * kCntW + cnt_swz(c)], dst + i);")
         s = sub(s, "      A.consensus[c0 + c] = best;\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) cons_star[c0 + c - zlo] = best == '-' ? (uint8_t)'*' : best;",
                 "      __builtin_nontemporal_store(best, A.consensus + c0 + c);\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) __builtin_nontemporal_store(best == '-' ? (uint8_t)'*' : best, cons_star + c0 + c - zlo);")
+    elif name == "k1_sumonly":  # timing only: row_chunk_sums loads and sums, no run entries / stores of runs
+        s = sub(s, "  const int cs = sums_group(A, p, lane, (LDS uint16_t*)lr32);",
+                "  int cs = 0;\n    { uint32_t t = p.q0.x + p.q0.y + p.q0.z + p.q0.w + p.q1.x + p.q1.y + p.q1.z + p.q1.w; cs = (int)row16_scan_incl(t); }")
     elif name == "head":
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_msa.hip"], check=True,
                            capture_output=True, text=True).stdout
