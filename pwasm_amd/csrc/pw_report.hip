@@ -72,6 +72,12 @@ constexpr int kLine = 108;      // render_kernel: report lines up to this long a
 constexpr int kLSlack = 40;     // ... + slack: a field block writes at most 35 bytes past its start (the
                                 // bases + tloc block of a 12-base S run), so none needs a bounds check
 static_assert(kLine + kLSlack <= 148, "line buffer stride");
+// Lines longer than kLine: a fast wave's line grows past its line buffer into its own query-window
+// column (up to kAppMax bytes, below) and render stores the wave's first such line itself; the
+// wave's other long lines of up to kLong bytes (kLongCap per wave) are emitted again after the
+// wave's last chunk (render's epilogue), the rest by fixup_kernel
+constexpr int kLong = 252;
+constexpr int kLongCap = 4;
 constexpr uint32_t kDropOff = 0xFFFFFF00u;  // a buffer-store offset past any range: the store is dropped
 // the report text is written non-temporal (cache policy nt): no kernel reads it again, and left to
 // the default policy its 303 MB per cfg2 pass linger dirty in the caches the next kernels (and the
@@ -439,15 +445,16 @@ struct LdsSink {
 struct ClampSink {
   LDS uint8_t* line;
   int pos;
+  int lim;  // kLine (the lane's line buffer) or kLong - kLSlack (render's epilogue)
   template <class F>
   __device__ __forceinline__ void block(int, F&& f) {
-    const int p0 = pos < kLine ? pos : kLine;
+    const int p0 = pos < lim ? pos : lim;
     RawSink u{line + (p0 - pos), pos};
     f(u);
     pos = u.pos;
   }
   __device__ __forceinline__ void put(uint8_t c) {
-    st8(line + (pos < kLine ? pos : kLine), c);
+    st8(line + (pos < lim ? pos : lim), c);
     pos++;
   }
 };
@@ -1063,8 +1070,13 @@ struct DLine {
   LDS uint8_t* buf;  // the lane's dword column of the wave's interleaved line buffers (kLine + kLSlack bytes)
   int pos;
 };
-// (a line that grows past kLine is rewritten by fixup_kernel: its appends are folded onto the slack)
-constexpr int kAppMax = kLine & ~3;
+// The wave's interleaved buffers and windows are kIlvRows rows, the query windows last: a line
+// grows past its buffer into its own window column, which emit_fast has read for the last time by
+// then (a line reaches ~101 bytes at most before the codon consequence, whose window reads come
+// first).  Past kAppMax an append is folded back (that line goes elsewhere): every append writes
+// at most 7 dwords.
+constexpr int kIlvRows = (kLStride + kQStride) / 4;
+constexpr int kAppMax = (kIlvRows - 7) * 4;
 // append bytes [0, n) of f (4D bytes; bytes past n may be anything) at the line end
 template <int D>
 __device__ __forceinline__ void app(DLine& L, const uint32_t (&f)[D], int n) {
@@ -2527,7 +2539,12 @@ __global__ __launch_bounds__(kWave* kWaves) void carry_kernel(pw_report_args A, 
 struct RenderWave {
   uint8_t line[kWave * kLStride];   // per-lane line buffers
   uint8_t qw[kWave * kQStride];     // per-lane forward-query windows
+  Fixup lst[kLongCap];              // long lines for the epilogue
 };
+// kRenderOcc = 3 workgroups per CU: LDS is allocated in blocks larger than 1 KB (measured: a
+// 53,864-byte workgroup ran render at 2 per CU, +50 % time; 53,096 at 3), so the bound is kept at
+// 26 blocks of 2 KB
+static_assert(sizeof(SmallTables) + kWaves * sizeof(RenderWave) <= 26 * 2048, "render LDS: 3 workgroups per CU");
 
 // the record owning event slot s: the last one whose first slot is <= s (error path only)
 // (arguments by value: a reference to the kernel arguments would put a copy of them in scratch)
@@ -2695,6 +2712,109 @@ __device__ __forceinline__ void render_pre_ready(RenderPre& p) {
   }
 }
 
+// One line, whole, from its slot's records (a long line: fixup_kernel, render's epilogue): the
+// windows render stages (query bytes around the event, the tx record) plus kFxLit literal bytes go
+// to the LDS buffers qwb (kQWin bytes) and lwb (kFxLit), the line to the sink
+constexpr int kFxLit = 32;
+template <class S>
+__device__ __forceinline__ void long_line(const pw_report_args& A, const Work& W, const LDS SmallTables* tp, uint64_t s,
+                                          LDS uint8_t* qwb, LDS uint8_t* lwb, S& g, bool skip) {
+  const Hot h = load_hot_full(A, W, s);
+  const uint32_t typ = h.fn >> 30;
+  const bool rev = (h.fn >> 29) & 1u;
+  const bool use_tx = !((h.fn >> 28) & 1u);
+  int ne = (int)(h.fn & kNBig);
+  Rec r;
+  r.lits = A.lits;
+  r.R = A.qseq + ((uint64_t)h.qb << 4);
+  r.L = h.L;
+  r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;
+  r.tab = tp;
+  r.opw = nullptr;
+  r.op_lo = 0;
+  r.op_n = 0;
+  r.lit0 = h.l0;
+  r.lit1 = h.l1;
+  r.ls0 = h.ls;
+  r.ln = 8;
+  r.rev = rev;
+  r.acgt = (h.fn & kFnAcgt) != 0;
+  r.offset = 0;
+  r.T = 0;
+  r.ops = nullptr;
+  r.n_ops = 0;
+  if ((uint32_t)ne == kNBig) {  // saturated length: from the op stream
+    const Cold cd = W.cold[s];
+    const pw_aln_desc d = A.desc[cd.ai];
+    r.ops = A.ops + d.op_begin;
+    r.n_ops = d.n_ops;
+    ne = event_len(r, cd.j, r.ops[cd.j]);
+  }
+  // windows: tx record, 48 query bytes from 8 before the event, 32 literal bytes from ls
+  v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
+  if (use_tx) {
+    const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * s);
+    t0 = tp4[0];
+    t1 = tp4[1];
+  }
+  const int rl = event_rloc(r.L, rev, typ, h.qp, ne);
+  int x0 = rl - 8;
+  if (x0 < 0) x0 = 0;
+  const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
+  const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
+#pragma unroll
+  for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(qwb + 16 * q) = a0[q];
+  r.qw = qwb;
+  r.qlo = x0a;
+  r.qn = kQWin;
+  const uint32_t l0 = h.ls & ~3u;
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
+#pragma unroll
+  for (int q = 0; q < kFxLit / 4; q++) reinterpret_cast<LDS uint32_t*>(lwb)[q] = l32[q];
+  r.lw = lwb;
+  r.l_lo = l0;
+  r.l_n = kFxLit;
+  EvIn in;
+  in.typ = typ;
+  in.n = ne;
+  in.qp = h.qp;
+  in.tloc = h.tloc;
+  in.ls = h.ls;
+  in.tmode = use_tx ? 1 : 0;
+  in.ll = (int)((h.fn >> 23) & 7u);
+  in.rl = (int)((h.fn >> 20) & 7u);
+  in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
+  in.ns_pre = kNsNone;
+  int rel;
+  emit_event(g, r, in, skip, rel);
+}
+
+// render's epilogue: the wave's listed long lines, one per lane (buffers over the wave's line /
+// window area: the line at 256 lane, its literal window at 1024 + 32 lane, its query window at
+// qwb), then stored byte by byte over the wave once the wave's page stores have completed
+__device__ __forceinline__ void render_long_lines(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
+                                               LDS RenderWave* w, LDS uint8_t* my_qw, int n_long, int lane, bool skip) {
+  int len = 0;
+  if (lane < n_long) {
+    const uint32_t ls = w->lst[lane].s;
+    LineSink ks;
+    ks.line = w->line + 256 * lane;
+    ks.pos = 0;
+    ks.lim = kLong - kLSlack;
+    long_line(A, W, tp, ls, my_qw, w->line + 1024 + kFxLit * lane, ks, skip);
+    len = ks.pos;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int j = 0; j < n_long; j++) {
+    const uint64_t dst = w->lst[j].dst;
+    const int n = __builtin_amdgcn_readlane(len, j);
+    const uint32_t v = reinterpret_cast<const LDS uint32_t*>(w->line + 256 * j)[lane];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * lane + i < n) __builtin_nontemporal_store((uint8_t)(v >> (8 * i)), A.text + dst + 4 * lane + i);
+  }
+}
+
 // Chunks are assigned statically (wave g takes chunks g, g + NW, ...): no work queue, no
 // inter-wave communication.  Each chunk's lines form one text page (PW_PAGE_BYTES at
 // chunk * PW_PAGE_BYTES, or an arena allocation when they do not fit).  Hot records are loaded
@@ -2723,6 +2843,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
     h = decode_hot<kH16>(W, h0, qn, true);
   }
   HotRaw<kH16> hn = load_hot<kH16>(W, c + nw, lane);
+  int n_long = 0;  // entries in the wave's long-line list (uniform)
   RenderPre pre;
   render_pre<kH16>(A, W, h, c * kWave + (uint64_t)lane, skip, pre);
   {  // (six dropped stores: the loop is entered with the same count of memory operations after the
@@ -2781,6 +2902,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       }
     }
     int linelen = 0;
+    bool held = false;  // a long line of a fast wave that the copy-out stores (one lane at most)
     if (act) {
       const uint32_t typ = hc.fn >> 30;
       const bool rev = (hc.fn >> 29) & 1u;
@@ -2825,6 +2947,7 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
       LineSink k;
       k.line = my_line;
       k.pos = 0;
+      k.lim = kLine;
       int rel = 0;
       int merr;
       if (ilv) {
@@ -2833,6 +2956,8 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         dl.pos = 0;
         merr = emit_fast(dl, w->qw + 4 * lane, qlo, tp, in, rev, r.L, hc.l0, hc.l1, r.NS, skip, rel);
         linelen = dl.pos;
+        const uint64_t lng = __ballot(linelen > kLine);
+        if (lng && lane == (int)__builtin_ctzll(lng) && linelen <= kAppMax) held = true;
       } else {
         merr = emit_event(k, r, in, skip, rel);
         linelen = k.pos;
@@ -2874,10 +2999,27 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         if (lane == 0) atomicOr(&W.ctr[2], 1u);
       }
     }
-    // long lines -> fixup_kernel: the chunk's lane mask (every chunk writes it) and the lines'
-    // destinations — plain stores: a returning atomic here cost a round trip per chunk with a
-    // long line
-    const bool need_fix = ok && linelen > kLine;
+    // long lines not held -> the wave's list (kLongCap, lines up to kLong bytes) or fixup_kernel:
+    // the chunk's lane mask (every chunk writes it) and the lines' destinations — plain stores: a
+    // returning atomic here cost a round trip per chunk with a long line
+    const uint64_t lone = __ballot(held);
+    const bool later = ok && linelen > kLine && !held;
+    bool need_fix = later && linelen > kLong - kLSlack;
+    {
+      const uint64_t lm2 = __ballot(later && linelen <= kLong - kLSlack);
+      if (lm2) {  // (uniform)
+        const int k = n_long + __popcll(lm2 & ((1ull << lane) - 1ull));
+        if ((lm2 >> lane) & 1ull) {
+          if (k < kLongCap) {
+            w->lst[k].s = (uint32_t)s;
+            w->lst[k].dst = P + my_off;
+          } else {
+            need_fix = true;
+          }
+        }
+        n_long = min(n_long + __popcll(lm2), kLongCap);
+      }
+    }
     const uint64_t lm = __ballot(need_fix);
     if (lane == 0) {
       pw_page pg;
@@ -2979,6 +3121,15 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         if (j == 0) v[0] |= ptail;
         return (v4u){v[0], v[1], v[2], v[3]};
       };
+      // the held line's column, contiguous, to the window rows past it (from row kLStride / 4,
+      // column jl + 1: clear of the column's own dwords there), before the page image overwrites
+      // the line rows
+      LDS uint32_t* const hl = reinterpret_cast<LDS uint32_t*>(w->line) + (kLStride / 4) * kTS + 1;
+      if (lone != 0) {  // (uniform)
+        const int jl = (int)__builtin_ctzll(lone);
+        const uint32_t v = reinterpret_cast<const LDS uint32_t*>(w->line)[(lane < kIlvRows ? lane : 0) * kTS + jl];
+        if (lane < kIlvRows) hl[jl + lane] = v;
+      }
       if (B + (uint32_t)kPageSlack <= (uint32_t)PW_PAGE_BYTES) {  // (uniform) the page in place:
         // every lane writes its groups into the wave's line buffer at its page offset (the page
         // image; the lines are in Lw already), then the image goes out as contiguous 1 KB stores —
@@ -2999,8 +3150,29 @@ __global__ __launch_bounds__(kWave* kWaves, kRenderOcc) void render_kernel(pw_re
         for (int j = 6; j >= 0; j--)
           __builtin_amdgcn_raw_buffer_store_b128(group(j), rs, j <= jmax ? a0 + 16u * (uint32_t)j : kDropOff, 0, kTextPolicy);
       }
+      if (lone != 0 && wr) {  // (uniform) the held line, byte by byte over the wave, once the stores
+        // above (its first kLine bytes; the next line's first dword, which ORs in this line's tail
+        // from the clamped buffer) have completed
+        const int jl = (int)__builtin_ctzll(lone);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)my_off, jl);
+        const int ln2 = __builtin_amdgcn_readlane(linelen, jl);
+        const uint32_t v = lane < kIlvRows ? hl[jl + lane] : 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int o = 4 * lane + i;
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> (8 * i)), rs, o < ln2 ? lo + (uint32_t)o : kDropOff, 0, kTextPolicy);
+        }
+      }
     }
     wave_sync();
+  }
+  // epilogue: the listed long lines (out of line: a second emit_event instance inlined here
+  // doubled the kernel's code)
+  if (n_long > 0) {  // (the lane-derived addresses recomputed: kept live across the loop, one was spilled)
+    int l2 = lane;
+    asm volatile("" : "+v"(l2));
+    render_long_lines(A, W, tp, w, w->qw + l2 * kQStride, n_long, l2, skip);
   }
 }
 
@@ -3174,7 +3346,6 @@ __device__ __forceinline__ void finalize_record(const pw_report_args& A, const W
 // Lines longer than the LDS line buffer, one per thread, rewritten in place (their bytes were
 // reserved).  The thread stages the same windows as render_kernel (query bytes around the event,
 // the tx record) plus 32 literal bytes in LDS, so only the line itself goes to global memory.
-constexpr int kFxLit = 32;
 struct FixLane {
   uint8_t qw[kQWin];
   uint8_t lw[kFxLit];
@@ -3223,77 +3394,10 @@ __global__ __launch_bounds__(256) void fixup_kernel(pw_report_args A, Work W) {
     uint64_t mm = mk[wv][k];
     for (uint32_t r = jl - ex[wv][k]; r > 0; r--) mm &= mm - 1;
     const Fixup f = W.fix[(c0 + (uint64_t)k) * kWave + (uint64_t)__builtin_ctzll(mm)];
-    const Hot h = load_hot_full(A, W, f.s);
-    const uint32_t typ = h.fn >> 30;
-    const bool rev = (h.fn >> 29) & 1u;
-    const bool use_tx = !((h.fn >> 28) & 1u);
-    int ne = (int)(h.fn & kNBig);
-    Rec r;
-    r.lits = A.lits;
-    r.R = A.qseq + ((uint64_t)h.qb << 4);
-    r.L = h.L;
-    r.NS = A.next_stop ? A.next_stop + ((uint64_t)h.qb << 4) : nullptr;
-    r.tab = tp;
-    r.opw = nullptr;
-    r.op_lo = 0;
-    r.op_n = 0;
-    r.lit0 = h.l0;
-    r.lit1 = h.l1;
-    r.ls0 = h.ls;
-    r.ln = 8;
-    r.rev = rev;
-    r.acgt = (h.fn & kFnAcgt) != 0;
-    r.offset = 0;
-    r.T = 0;
-    r.ops = nullptr;
-    r.n_ops = 0;
-    if ((uint32_t)ne == kNBig) {  // saturated length: from the op stream
-      const Cold cd = W.cold[f.s];
-      const pw_aln_desc d = A.desc[cd.ai];
-      r.ops = A.ops + d.op_begin;
-      r.n_ops = d.n_ops;
-      ne = event_len(r, cd.j, r.ops[cd.j]);
-    }
-    // windows: tx record, 48 query bytes from 8 before the event, 32 literal bytes from ls
-    v4u t0 = {0u, 0u, 0u, 0u}, t1 = t0;
-    if (use_tx) {
-      const v4u* tp4 = reinterpret_cast<const v4u*>(W.tx + (uint64_t)kTx * f.s);
-      t0 = tp4[0];
-      t1 = tp4[1];
-    }
-    const int rl = event_rloc(r.L, rev, typ, h.qp, ne);
-    int x0 = rl - 8;
-    if (x0 < 0) x0 = 0;
-    const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
-    const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
-#pragma unroll
-    for (int q = 0; q < kQWin / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = a0[q];
-    r.qw = me->qw;
-    r.qlo = x0a;
-    r.qn = kQWin;
-    const uint32_t l0 = h.ls & ~3u;
-    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + l0 / 4;
-#pragma unroll
-    for (int q = 0; q < kFxLit / 4; q++) reinterpret_cast<LDS uint32_t*>(me->lw)[q] = l32[q];
-    r.lw = me->lw;
-    r.l_lo = l0;
-    r.l_n = kFxLit;
-    EvIn in;
-    in.typ = typ;
-    in.n = ne;
-    in.qp = h.qp;
-    in.tloc = h.tloc;
-    in.ls = h.ls;
-    in.tmode = use_tx ? 1 : 0;
-    in.ll = (int)((h.fn >> 23) & 7u);
-    in.rl = (int)((h.fn >> 20) & 7u);
-    in.tx[0] = t0.x, in.tx[1] = t0.y, in.tx[2] = t0.z, in.tx[3] = t0.w, in.tx[4] = t1.x, in.tx[5] = t1.y;
-    in.ns_pre = kNsNone;
     GlobalSink g;
     g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);
     g.pos = 0;
-    int rel;
-    emit_event(g, r, in, skip, rel);
+    long_line(A, W, tp, f.s, me->qw, me->lw, g, skip);
   }
     wave_sync();
   }

@@ -118,6 +118,26 @@ def test_long_lines_many_chunks(built, tmp_path):
     assert sum(92 <= len(l) < 108 for l in lines) > 500  # (681)
 
 
+@pytest.mark.parametrize("opts,lo,hi", [
+    # S runs of 5+ bases (a general-path wave's long lines: render's per-wave list and epilogue,
+    # several per chunk)
+    (["--err", 0.05, "--subrun", 0.5, "--psub", 1.0, "--pdel", 0, "--pins", 0], 20, 0),
+    # every line a long S run past 212 bytes (more long lines per chunk than render holds or lists,
+    # and lines past the epilogue's buffer: fixup_kernel)
+    (["--err", 0.1, "--subrun", 1.0, "--psub", 1.0, "--pdel", 0, "--pins", 0], 100, 100),
+])
+def test_long_lines_render_paths(built, tmp_path, opts, lo, hi):
+    """Lines past render's line buffer (kLine = 108): a fast wave's first one is held in the
+    interleaved rows and stored by the copy-out, a wave's others of up to 212 bytes go to its list
+    (kLongCap = 4) and are emitted again after its last chunk, the rest to fixup_kernel — same
+    bytes as the oracle on each route."""
+    fa, paf = synth_paf(tmp_path, 0, seed=5, scale=2, extra=opts)
+    out = same(["-r", fa, paf])
+    lines = [l for l in out.split(b"\n") if l[:2] in (b"S\t", b"I\t", b"D\t")]
+    assert sum(len(l) >= 108 for l in lines) >= lo
+    assert sum(len(l) >= 212 for l in lines) >= hi
+
+
 def test_reverse_only_and_forward_only(built, tmp_path):
     for rev in (0.0, 1.0):
         fa, paf = synth_paf(tmp_path, 0, seed=31, extra=["--rev", rev])

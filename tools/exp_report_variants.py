@@ -308,6 +308,29 @@ PATCHES["hotld_nt"] = [("  r.a = p[0];\n  if constexpr (!kH16) r.b = p[1];",
                         "  r.a = __builtin_nontemporal_load(p);\n  if constexpr (!kH16) r.b = __builtin_nontemporal_load(p + 1);")]
 PATCHES["txld_nt"] = [("    p.t0 = tp4[0];\n    p.t1 = tp4[1];", "    p.t0 = __builtin_nontemporal_load(tp4);\n    p.t1 = __builtin_nontemporal_load(tp4 + 1);")]
 
+# fixup_kernel's long lines emitted into one shared LDS scratch line instead of global memory (no
+# global byte stores: wrong output, timing only)
+PATCHES["fx_ldssink"] = [("""    GlobalSink g;
+    g.p = (PW_GLOBAL uint8_t*)(A.text + f.dst);
+    g.pos = 0;
+    int rel;
+    emit_event(g, r, in, skip, rel);""", """    LdsSink<128> g;
+    g.buf = (LDS uint8_t*)&lsk[0];
+    g.junk = g.buf + 128;
+    g.pos = 0;
+    int rel;
+    emit_event(g, r, in, skip, rel);
+    if (g.pos == 12345) A.text[f.dst] = 0;"""),
+    ("  __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts",
+     "  __shared__ uint32_t ex[kWaves][kWave];  // exclusive prefix of their popcounts\n  __shared__ uint8_t lsk[136];")]
+
+# render's long-line epilogue (round 5): left out (listed lines never written: timing only), or
+# compiled in but never run
+PATCHES["le_none"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (n_long > 0 && A.n_alns == 0xFFFFFFFFu) {  // (the lane-derived"),
+                      ("__device__ __forceinline__ void render_long_lines(", "__device__ __forceinline__ void render_long_lines_x(const int);\n__device__ __forceinline__ void render_long_lines(")]
+PATCHES["le_cold"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (n_long > 0 && A.n_alns == 0xFFFFFFFFu) {  // (the lane-derived")]
+PATCHES["le_skip"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (false) {  // (the lane-derived")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
