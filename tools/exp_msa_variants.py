@@ -120,6 +120,24 @@ def make(name):
         s = sub(s, "    dst[i] = (int32_t)tab[f * kCntW + cnt_swz(c)];", "    __builtin_nontemporal_store((int32_t)tab[f * kCntW + cnt_swz(c)], dst + i);")
         s = sub(s, "      A.consensus[c0 + c] = best;\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) cons_star[c0 + c - zlo] = best == '-' ? (uint8_t)'*' : best;",
                 "      __builtin_nontemporal_store(best, A.consensus + c0 + c);\n      if (cons_star && c0 + c >= zlo && c0 + c <= zhi) __builtin_nontemporal_store(best == '-' ? (uint8_t)'*' : best, cons_star + c0 + c - zlo);")
+    elif name == "winpad":  # tile_counts' base window padded one dword per eight (no 8-way read conflicts)
+        s = sub(s, "  uint32_t win[kCntWaves][kWin / 4];", "  uint32_t win[kCntWaves][kWin / 4 + kWin / 32 + 8];")
+        s = sub(s, "__device__ __forceinline__ uint32_t bin_codes5(", "typedef unsigned int v4a4 __attribute__((ext_vector_type(4), aligned(4)));\n__device__ __forceinline__ uint32_t bin_codes5(")
+        s = sub(s, """        LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+        w4[lane] = cc.w0;
+        w4[64 + lane] = cc.w1;
+        if (lane < 8) w4[128 + lane] = cc.w2;""", """        *reinterpret_cast<LDS v4a4*>(win + 4 * lane + (lane >> 1)) = cc.w0;
+        *reinterpret_cast<LDS v4a4*>(win + 288 + 4 * lane + (lane >> 1)) = cc.w1;
+        if (lane < 8) *reinterpret_cast<LDS v4a4*>(win + 576 + 4 * lane + (lane >> 1)) = cc.w2;""")
+        s = sub(s, """          LDS v4u* w4 = reinterpret_cast<LDS v4u*>(win);
+          w4[lane] = w0;
+          w4[64 + lane] = w1;
+          if (lane < 8) w4[128 + lane] = w2;""", """          *reinterpret_cast<LDS v4a4*>(win + 4 * lane + (lane >> 1)) = w0;
+          *reinterpret_cast<LDS v4a4*>(win + 288 + 4 * lane + (lane >> 1)) = w1;
+          if (lane < 8) *reinterpret_cast<LDS v4a4*>(win + 576 + 4 * lane + (lane >> 1)) = w2;""")
+        s = sub(s, """            const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
+            const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);""", """            const int dd = src >> 2, de = dd + 1;
+            const uint32_t s4 = __builtin_amdgcn_alignbyte(win[de + (de >> 3)], win[dd + (dd >> 3)], (uint32_t)src & 3u);""")
     elif name == "k1_sumonly":  # timing only: row_chunk_sums loads and sums, no run entries / stores of runs
         s = sub(s, "  const int cs = sums_group(A, p, lane, (LDS uint16_t*)lr32);",
                 "  int cs = 0;\n    { uint32_t t = p.q0.x + p.q0.y + p.q0.z + p.q0.w + p.q1.x + p.q1.y + p.q1.z + p.q1.w; cs = (int)row16_scan_incl(t); }")
