@@ -3194,8 +3194,147 @@ struct TctxLane {
 };
 struct TctxWave {
   TctxLane ln[kWave];
-  uint32_t list[5 * kWave];  // the wave's queue of flagged slots (< 64 carried + a 256-slot group)
+  uint32_t list[5 * kWave];  // the wave's queue of flagged slots (carried + a 256-slot group: the
+                             // carried entries are taken first when they would not fit)
 };
+// One flagged event's inputs, loaded in three dependent levels (tc_load1..3: the caller issues
+// each level for all its events before the next)
+struct TcIn {
+  uint64_t s;
+  v4u a;             // the event record's first 16 bytes
+  v4u b;             // its second 16 bytes (32-byte records)
+  Cold cd;           // the walk's start: record, head op, query / target position (index_kernel)
+  uint32_t qi_off_lo, qi_off_hi;
+  int32_t L;
+  uint32_t lw0, lw1, lw2;  // literal dwords from ls & ~3 (16-byte records)
+  uint32_t op_begin, n_ops;
+  int32_t offset, t_len;
+  v4u qv[kTcQ / 16];
+  uint32_t ow[kTcOps];
+  int x0a, o0;
+};
+__device__ __forceinline__ void tc_load1(const Work& W, uint64_t s, TcIn& x) {
+  x.s = s;
+  const v4u* p = reinterpret_cast<const v4u*>(W.hotw + (s << W.hot_sh));
+  x.a = p[0];
+  x.b = W.hot_pbits ? (v4u){0u, 0u, 0u, 0u} : p[1];
+  x.cd = W.cold[s];
+}
+__device__ __forceinline__ void tc_load2(const pw_report_args& A, const Work& W, TcIn& x) {
+  const pw_aln_desc d = A.desc[x.cd.ai];
+  x.op_begin = d.op_begin;
+  x.n_ops = d.n_ops;
+  x.offset = d.offset;
+  x.t_len = d.t_len;
+  if (W.hot_pbits) {
+    const uint32_t qi = hot16_qi(W, x.a.x, x.a.y);
+    const uint64_t qo = A.qoff[qi];
+    x.qi_off_lo = (uint32_t)(qo >> 4);
+    x.qi_off_hi = 0;
+    x.L = A.qlen[qi];
+    const uint32_t ls = x.a.x == kNoEv ? 0u : x.a.w;
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + (ls >> 2);
+    x.lw0 = l32[0];
+    x.lw1 = l32[1];
+    x.lw2 = l32[2];
+  } else {
+    x.qi_off_lo = x.b.x;
+    x.qi_off_hi = 0;
+    x.L = (int32_t)x.b.y;
+    x.lw0 = x.lw1 = x.lw2 = 0u;
+  }
+}
+__device__ __forceinline__ int tc_qp(const Work& W, const TcIn& x) {
+  return W.hot_pbits ? (int32_t)hot16_qp(W, x.a.y) : (int32_t)x.a.y;
+}
+__device__ __forceinline__ void tc_load3(const pw_report_args& A, TcIn& x, const Work& W) {
+  // forward query bytes of the context: [fc - 5, fc + n + 5) for a '+' record, [fc - n - 5,
+  // fc + 5] for a '-' record (n <= 12 unless abbreviated), fc = the event's forward position
+  const bool rev = (x.a.x >> 29) & 1u;
+  const int qp = tc_qp(W, x);
+  const int fc = rev ? x.L - 1 - qp : qp;
+  int x0 = fc - (rev ? kTcQ / 2 : 8);
+  if (x0 < 0) x0 = 0;
+  x.x0a = x0 & ~15;  // (the query is 16-byte aligned)
+  const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(A.qseq + ((uint64_t)x.qi_off_lo << 4)) + x.x0a);
+#pragma unroll
+  for (int q = 0; q < kTcQ / 16; q++) x.qv[q] = a0[q];
+  // op words [j - 6, j + 6) (indices clamped to the record's last op, values masked after: a
+  // guarded load would be a branch and a vmcnt(0) per word)
+  const int j = (int)x.cd.j;
+  x.o0 = j - kTcOps / 2 < 0 ? 0 : j - kTcOps / 2;
+  const uint32_t* ops = A.ops + x.op_begin;
+  const uint32_t olast = x.n_ops ? x.n_ops - 1 : 0u;
+#pragma unroll
+  for (int q = 0; q < kTcOps; q++) x.ow[q] = ops[(uint32_t)(x.o0 + q) < olast ? (uint32_t)(x.o0 + q) : olast];
+}
+// the event's target context, walked over the staged windows, stored as its 32-byte tx record
+__device__ __forceinline__ void tc_event(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
+                                         LDS TctxLane* me, const TcIn& x) {
+  Rec r;
+  r.R = A.qseq + ((uint64_t)x.qi_off_lo << 4);
+  r.L = x.L;
+  const uint32_t fn = x.a.x;
+  r.rev = (fn >> 29) & 1u;
+  r.ops = A.ops + x.op_begin;
+  r.lits = A.lits;
+  r.NS = nullptr;
+  r.tab = tp;
+  r.offset = x.offset;
+  r.T = x.t_len;
+  r.n_ops = x.n_ops;
+  r.acgt = false;
+  // the event's first 8 literal bytes are in registers; op words and forward query bytes
+  // around the event are staged in LDS
+  const uint32_t ls = fn == kNoEv ? 0u : x.a.w;
+  uint32_t l0, l1;
+  if (W.hot_pbits) {
+    lit8(ls, x.lw0, x.lw1, x.lw2, l0, l1);
+  } else {
+    l0 = x.b.z;
+    l1 = x.b.w;
+  }
+  r.lit0 = l0;
+  r.lit1 = l1;
+  r.ls0 = ls;
+  r.ln = 8;
+  r.lw = nullptr;
+  r.l_lo = 0;
+  r.l_n = 0;
+  const int j = (int)x.cd.j;
+#pragma unroll
+  for (int q = 0; q < kTcOps; q++) me->opw[q] = (uint32_t)(x.o0 + q) < r.n_ops ? x.ow[q] : 0u;
+#pragma unroll
+  for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = x.qv[q];
+  r.opw = me->opw;
+  r.op_lo = x.o0;
+  r.op_n = (uint32_t)kTcOps;
+  r.qw = me->qw;
+  r.qlo = x.x0a;
+  r.qn = kTcQ;
+  const uint32_t wd = opword(r, (uint32_t)j);
+  int ne = (int)(fn & kNBig);
+  if ((uint32_t)ne == kNBig) ne = event_len(r, (uint32_t)j, wd);
+  LdsSink<kTx - 1> ks;
+  ks.buf = me->out + 1;
+  ks.junk = me->out + kTx;
+  ks.pos = 0;
+  emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, x.cd.qs, x.cd.ts, ls);
+  me->out[0] = (uint8_t)ks.pos;
+  const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
+  v4u t0, t1;
+  t0.x = t32[0];
+  t0.y = t32[1];
+  t0.z = t32[2];
+  t0.w = t32[3];
+  t1.x = t32[4];
+  t1.y = t32[5];
+  t1.z = t32[6];
+  t1.w = t32[7];
+  v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * x.s);
+  dtx[0] = t0;
+  dtx[1] = t1;
+}
 __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) TctxWave tw[kWaves];
@@ -3217,87 +3356,26 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
   // (every lane has an event except in the wave's last batch): the walk runs once per 64 events,
   // not once per group (~40 flagged slots per 256 at cfg2)
   uint32_t nl = 0;  // entries in the list (wave-uniform)
+  // A batch takes up to 128 entries: lane l the events of entries l and 64 + l.  Both events'
+  // records load together, level by level (Hot / Cold, then the query table / descriptor /
+  // literal words); the second event's wait in registers while the first one is walked, so a
+  // wave's second 64 events cost one level of loads (their windows) and a walk, not a whole chain.
   auto batch = [&](uint32_t nb) {
-    if ((uint32_t)lane < nb) {
-      const uint64_t s = w->list[lane];
-      const Hot h = load_hot_full(A, W, s);
-      const Cold cd = W.cold[s];  // the walk's start: record, head op, query / target position (index_kernel)
-      Rec r;
-      r.R = A.qseq + ((uint64_t)h.qb << 4);
-      r.L = h.L;
-      r.rev = (h.fn >> 29) & 1u;
-      // forward query bytes of the context: [fc - 5, fc + n + 5) for a '+' record, [fc - n - 5,
-      // fc + 5] for a '-' record (n <= 12 unless abbreviated), fc = the event's forward position —
-      // issued before the record's descriptor is read (they depend on the Hot record only)
-      const int fc = r.rev ? r.L - 1 - h.qp : h.qp;
-      int x0 = fc - (r.rev ? kTcQ / 2 : 8);
-      if (x0 < 0) x0 = 0;
-      const int x0a = x0 & ~15;  // (r.R is 16-byte aligned)
-      const GV4* a0 = reinterpret_cast<const GV4*>((GU8)(r.R) + x0a);
-      v4u qv[kTcQ / 16];
-#pragma unroll
-      for (int q = 0; q < kTcQ / 16; q++) qv[q] = a0[q];
-      const pw_aln_desc d = A.desc[cd.ai];
-      r.ops = A.ops + d.op_begin;
-      r.lits = A.lits;
-      r.NS = nullptr;
-      r.tab = tp;
-      r.offset = d.offset;
-      r.T = d.t_len;
-      r.n_ops = d.n_ops;
-      r.acgt = false;
-      // the event's first 8 literal bytes are in its render record; op words [j - 6, j + 6)
-      // and forward query bytes around the event are staged in LDS
-      r.lit0 = h.l0;
-      r.lit1 = h.l1;
-      r.ls0 = h.ls;
-      r.ln = 8;
-      r.lw = nullptr;
-      r.l_lo = 0;
-      r.l_n = 0;
-      const int j = (int)cd.j;
-      int o0 = j - kTcOps / 2;
-      if (o0 < 0) o0 = 0;
-      // (indices clamped to the record's last op, values masked after: a guarded load would be
-      // a branch and a vmcnt(0) per word)
-      uint32_t ow[kTcOps];
-      const uint32_t olast = r.n_ops ? r.n_ops - 1 : 0u;
-#pragma unroll
-      for (int q = 0; q < kTcOps; q++) ow[q] = r.ops[(uint32_t)(o0 + q) < olast ? (uint32_t)(o0 + q) : olast];
-#pragma unroll
-      for (int q = 0; q < kTcOps; q++) ow[q] = (uint32_t)(o0 + q) < r.n_ops ? ow[q] : 0u;
-#pragma unroll
-      for (int q = 0; q < kTcOps; q++) me->opw[q] = ow[q];
-#pragma unroll
-      for (int q = 0; q < kTcQ / 16; q++) *reinterpret_cast<LDS v4u*>(me->qw + 16 * q) = qv[q];
-      r.opw = me->opw;
-      r.op_lo = o0;
-      r.op_n = (uint32_t)kTcOps;
-      r.qw = me->qw;
-      r.qlo = x0a;
-      r.qn = kTcQ;
-      const uint32_t wd = opword(r, (uint32_t)j);
-      int ne = (int)(h.fn & kNBig);
-      if ((uint32_t)ne == kNBig) ne = event_len(r, (uint32_t)j, wd);
-      LdsSink<kTx - 1> ks;
-      ks.buf = me->out + 1;
-      ks.junk = me->out + kTx;
-      ks.pos = 0;
-      emit_tctx_walk(ks, r, wd >> 30, ne, (uint32_t)j, wd, cd.qs, cd.ts, h.ls);
-      me->out[0] = (uint8_t)ks.pos;
-      const LDS uint32_t* t32 = reinterpret_cast<const LDS uint32_t*>(me->out);
-      v4u t0, t1;
-      t0.x = t32[0];
-      t0.y = t32[1];
-      t0.z = t32[2];
-      t0.w = t32[3];
-      t1.x = t32[4];
-      t1.y = t32[5];
-      t1.z = t32[6];
-      t1.w = t32[7];
-      v4u* dtx = reinterpret_cast<v4u*>(W.tx + (uint64_t)kTx * s);
-      dtx[0] = t0;
-      dtx[1] = t1;
+    const bool has1 = (uint32_t)lane < nb, has2 = (uint32_t)lane + kWave < nb;
+    // (unconditional loads: a lane without an entry reads entry 0's records)
+    const uint64_t s1 = w->list[has1 ? lane : 0], s2 = w->list[has2 ? kWave + lane : 0];
+    TcIn x1, x2;
+    tc_load1(W, s1, x1);
+    tc_load1(W, s2, x2);
+    tc_load2(A, W, x1);
+    tc_load2(A, W, x2);
+    tc_load3(A, x1, W);
+    if (has1) tc_event(A, W, tp, me, x1);
+    // (the second event's windows load after the first walk: held across it, they pushed the
+    // kernel past 128 VGPRs)
+    if (nb > (uint32_t)kWave) {  // (uniform)
+      tc_load3(A, x2, W);
+      if (has2) tc_event(A, W, tp, me, x2);
     }
   };
   for (; gi < n_groups; gi += gstride) {
@@ -3311,22 +3389,27 @@ __global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, W
     const uint32_t incl = wave_incl_scan(cnt, lane);
     const uint32_t total = wave_last(incl);
     if (total == 0) continue;
+    if (nl + total > 5u * kWave) {  // (uniform; only groups of > 192 flagged slots)
+      batch(nl);
+      nl = 0;
+      wave_sync();
+    }
     uint32_t o = nl + incl - cnt;
 #pragma unroll
     for (int q = 0; q < 4; q++)
       if ((f4 >> (8 * q)) & 1u) w->list[o++] = (uint32_t)(gi * 256 + (uint64_t)(4 * lane + q));
     nl += total;
     wave_sync();
-    while (nl >= (uint32_t)kWave) {
-      batch((uint32_t)kWave);
+    while (nl >= (uint32_t)(2 * kWave)) {
+      batch((uint32_t)(2 * kWave));
       // the entries after the batch move to the front (<= 4 per lane)
-      const uint32_t rest = nl - (uint32_t)kWave;
+      const uint32_t rest = nl - (uint32_t)(2 * kWave);
       uint32_t mv[4];
       wave_sync();
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t i = (uint32_t)(lane + kWave * k);
-        mv[k] = i < rest ? w->list[kWave + i] : 0u;
+        mv[k] = i < rest ? w->list[2 * kWave + i] : 0u;
       }
       wave_sync();
 #pragma unroll

@@ -107,9 +107,9 @@ def test_arena_pages(built, tmp_path):
 
 def test_long_lines_many_chunks(built, tmp_path):
     """~300 chunks of lines with long indels and S runs: dozens of lines longer than render's LDS
-    line buffer (kLine = 108 bytes with the newline), rewritten in place by fixup_kernel, and
-    hundreds of 93-108 byte lines, built by render in the line buffer's slack (kLine was 92 until
-    round 4)."""
+    line buffer (kLine = 108 bytes with the newline: held or re-emitted by render, or rewritten in
+    place by fixup_kernel), and hundreds of 93-108 byte lines, built by render in the line buffer's
+    slack (kLine was 92 until round 4)."""
     fa, paf = synth_paf(tmp_path, 0, seed=21, scale=10, extra=["--longindel", 0.5, "--subrun", 0.6, "--err", 0.05])
     out = same(["-r", fa, paf])
     lines = [l for l in out.split(b"\n") if l[:2] in (b"S\t", b"I\t", b"D\t")]
@@ -136,6 +136,15 @@ def test_long_lines_render_paths(built, tmp_path, opts, lo, hi):
     lines = [l for l in out.split(b"\n") if l[:2] in (b"S\t", b"I\t", b"D\t")]
     assert sum(len(l) >= 108 for l in lines) >= lo
     assert sum(len(l) >= 212 for l in lines) >= hi
+
+
+@pytest.mark.parametrize("err", [0.25, 0.45])
+def test_dense_target_contexts(built, tmp_path, err):
+    """Events every few bases: most target contexts need the op walk (tctx_kernel's batches of
+    128, and groups of slots with more flagged events than its list holds beside the carried ones)."""
+    fa, paf = synth_paf(tmp_path, 0, seed=11, scale=2, extra=["--err", err])
+    out = same(["-r", fa, paf])
+    assert out.count(b"\n") > 1000
 
 
 def test_reverse_only_and_forward_only(built, tmp_path):
