@@ -512,6 +512,30 @@ __device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, 
     int pe = c.ts + tl;
     if (pe > p1 || pe <= p) pe = p1;  // (pe <= p: past the last op; cannot happen on valid input)
     const uint32_t t = c.w >> 30;
+    if (t == PW_OP_MATCH) {
+      // a match run inside the query and the window: its query bytes as 8-byte images (one LDS
+      // round trip per 8 bytes instead of one per byte: a byte read could not pass the previous
+      // byte's store to the sink, which may alias it)
+      const int xa = r.offset + c.qs + (p - c.ts), cnt = pe - p;
+      const int fs = r.rev ? r.L - xa - cnt : xa;  // first forward position of the run's bytes
+      const int o = fs - r.qlo;
+      if (xa >= 0 && xa + cnt <= r.L && o >= 0 && o + cnt <= r.qn) {
+        for (int q = 0; q < cnt; q += 8) {
+          const uint64_t v = lds8(r.qw, o + q);
+#pragma unroll
+          for (int b = 0; b < 8; b++) {
+            if (q + b >= cnt) break;
+            const uint8_t f = (uint8_t)(v >> (8 * b));
+            // forward byte fs + q + b: aligned position xa + q + b ('+'), or L - 1 - (fs + q + b)
+            // = xa + cnt - 1 - (q + b) ('-', complemented)
+            const int pp = r.rev ? p + cnt - 1 - (q + b) : p + q + b;
+            k.put_at(r.rev ? base + (p1 - 1 - pp) : base + (pp - p0), r.rev ? comp2(f) : f);
+          }
+        }
+        p = pe;
+        continue;
+      }
+    }
     for (; p < pe; p++) {
       const int off = p - c.ts;
       uint8_t ch;
