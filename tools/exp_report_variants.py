@@ -331,6 +331,12 @@ PATCHES["le_none"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (n_lon
 PATCHES["le_cold"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (n_long > 0 && A.n_alns == 0xFFFFFFFFu) {  // (the lane-derived")]
 PATCHES["le_skip"] = [("  if (n_long > 0) {  // (the lane-derived", "  if (false) {  // (the lane-derived")]
 
+# timing only (wrong bytes): the walk's byte reads outside the staged windows / literal registers
+# answered without their global load
+PATCHES["nolitg"] = [("  return lit_global(r.lits, i);\n}", "  return r.lits == nullptr ? lit_global(r.lits, i) : (uint8_t)'A';\n}")]
+PATCHES["norcg"] = [("  if (o < (unsigned)r.qn) return r.qw[o];\n  return rc_global(r.R, r.L, x);",
+                     "  if (o < (unsigned)r.qn) return r.qw[o];\n  return r.R == nullptr ? rc_global(r.R, r.L, x) : (uint8_t)'A';")]
+
 # scheduler flags per variant (default: the Makefile's max-memory-clause)
 FLAGS = {
     "sch_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
