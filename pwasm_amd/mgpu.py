@@ -15,8 +15,10 @@ Replaces the reference's sequential record loop (pafreport.cpp:303-436) over a n
                 is packed on host threads while the GPU runs batch k (pw_batch_from_buffer, the
                 dedupe state moving from batch to batch; pw_stop_table_build + pw_report_events).
   output        no rank-0 merge, written window by window of global input lines (OffsetWriter,
-                PW_WINDOW_LINES) as the batches finish, so a rank holds only the batches of the
-                current window: the first fatal input line of the window over all ranks ends the run
+                PW_WINDOW_LINES) as the batches finish.  A rank holds the batches with lines in
+                the current window or a later one (a batch stays pending until its last line's
+                window is written), and waits in each window's collectives for the slowest rank.
+                The first fatal input line of the window over all ranks ends the run
                 (all-reduce MIN); every rank's per-line stdout byte counts of the window are summed
                 over the ranks (all-reduce of one int64 per line of the window) and exclusive-scanned
                 into file offsets after the previous windows, and each rank pwrites its own items
