@@ -1377,7 +1377,10 @@ struct Device {
       HIPCHK(hipMemcpyAsync(ops.p, b.ops.data(), b.ops.size() * 4, hipMemcpyHostToDevice, stream));
     if (!b.lits.empty())
       HIPCHK(hipMemcpyAsync(lits.p, b.lits.data(), b.lits.size(), hipMemcpyHostToDevice, stream));
+    // every field is assigned below; PW_ARGS_POISON=1 (tests) fills the struct with 0xFF first so
+    // that a field left unset shows up as a wrong report instead of as whatever the stack held
     pw_report_args a;
+    memset(&a, (getenv("PW_ARGS_POISON") && atoi(getenv("PW_ARGS_POISON")) != 0) ? 0xFF : 0, sizeof a);
     a.desc = desc.p;
     a.ops = ops.p;
     a.lits = lits.p;
@@ -1403,6 +1406,8 @@ struct Device {
     if (getenv("PW_NO_PAIRS") && atoi(getenv("PW_NO_PAIRS")) != 0) a.n_short = 0;  // (tests: one record per wave)
     // 16-byte event records when the query positions / indices fit (PW_HOT32=1 keeps 32-byte ones)
     a.hot_pbits = (getenv("PW_HOT32") && atoi(getenv("PW_HOT32")) != 0) ? 0u : pw_report_hot_pbits(q.max_len(), q.len.size());
+    a.flags = 0;  // the CLI builds the next-stop table once per query set (Device::init)
+    a.n_queries = (uint32_t)q.len.size();
     a.pad = 0;
     if (pw_report_events(&a, stream) != PW_OK) {
       fprintf(stderr, "pafreport: kernel launch failed\n");
@@ -1444,13 +1449,18 @@ struct TextStream {
   std::vector<uint8_t> arena;
   std::vector<uint8_t> img[2];  // emit_parallel's output images (kept across batches: faulted in once)
   bool ok = false;
-  bool init() {
+  bool init() {  // (reports its own failure)
     if (ok) return true;
     for (int k = 0; k < 2; k++)
       if (hipHostMalloc((void**)&buf[k], kWin, hipHostMallocDefault) != hipSuccess ||
-          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess)
+          hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) {
+        fprintf(stderr, "pafreport: pinned host buffers could not be allocated\n");
         return false;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return false;
+      }
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      fprintf(stderr, "pafreport: HIP stream creation failed\n");
+      return false;
+    }
     ok = true;
     return true;
   }
@@ -1702,6 +1712,13 @@ int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, cons
       done += (uint64_t)w;
     }
   };
+  // A window's pieces are cut into groups of at most kImg destination bytes, so an image never
+  // holds more than that (host pieces after the last page-region piece all join the last window:
+  // a batch of mostly arena text would otherwise make one image of its whole output); a single
+  // piece larger than kImg is written straight from its source.
+  uint64_t kImg = 2 * TextStream::kWin;
+  if (const char* e = getenv("PW_EMIT_IMG_BYTES")) kImg = std::max<uint64_t>(1, strtoull(e, nullptr, 10));  // (tests)
+  int ik = 0;  // the image the next group is copied into (the two alternate)
   size_t i0 = 0;
   for (int64_t w = 0; w < nwin && !bad; w++) {
     size_t i1 = i0;
@@ -1717,26 +1734,43 @@ int emit_parallel(const Batch& b, TextStream& ts, const pw_aln_result* res, cons
       (void)hipEventSynchronize(ts.ev[slot]);
     }
     const uint8_t* wb = ts.buf[slot];
-    if (wr[slot].joinable()) wr[slot].join();  // image `slot` is free again
-    if (i1 > i0) {
-      const uint64_t d0 = pc[i0].dst, d1 = pc[i1 - 1].dst + pc[i1 - 1].len;
-      if (img[slot].size() < d1 - d0) img[slot].resize(d1 - d0);
-      uint8_t* ib = img[slot].data();
+    for (size_t g0 = i0; g0 < i1 && !bad;) {
+      if (pc[g0].len > kImg) {  // one large piece: written from its source, before wb is refilled
+        const uint8_t* src = pc[g0].host ? pc[g0].host : wb + (pc[g0].src - wlo);
+        for (uint64_t done = 0; done < pc[g0].len;) {
+          const ssize_t n = pwrite(fd, src + done, (size_t)(pc[g0].len - done), base + (off_t)(pc[g0].dst + done));
+          if (n <= 0) {
+            bad = true;
+            break;
+          }
+          done += (uint64_t)n;
+        }
+        g0++;
+        continue;
+      }
+      size_t g1 = g0 + 1;
+      while (g1 < i1 && pc[g1].len <= kImg && pc[g1].dst + pc[g1].len - pc[g0].dst <= kImg) g1++;
+      if (wr[ik].joinable()) wr[ik].join();  // image `ik` is free again
+      const uint64_t d0 = pc[g0].dst, d1 = pc[g1 - 1].dst + pc[g1 - 1].len;
+      if (img[ik].size() < d1 - d0) img[ik].resize(d1 - d0);
+      uint8_t* ib = img[ik].data();
       const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(nt, 1), (d1 - d0) >> 20));
       auto work = [&](int t) {  // the pieces whose destination starts in this thread's byte range
         const uint64_t a = d0 + (d1 - d0) * (uint64_t)t / (uint64_t)T;
         const uint64_t z = d0 + (d1 - d0) * (uint64_t)(t + 1) / (uint64_t)T;
-        size_t j = (size_t)(std::lower_bound(pc.begin() + (long)i0, pc.begin() + (long)i1, a,
+        size_t j = (size_t)(std::lower_bound(pc.begin() + (long)g0, pc.begin() + (long)g1, a,
                                              [](const Piece& p, uint64_t v) { return p.dst < v; }) -
                             pc.begin());
-        for (; j < i1 && pc[j].dst < z; j++)
+        for (; j < g1 && pc[j].dst < z; j++)
           memcpy(ib + (pc[j].dst - d0), pc[j].host ? pc[j].host : wb + (pc[j].src - wlo), pc[j].len);
       };
       std::vector<std::thread> th;
       for (int t = 1; t < T; t++) th.emplace_back(work, t);
       work(0);
       for (auto& x : th) x.join();
-      wr[slot] = std::thread(write_img, slot, d0, d1 - d0);
+      wr[ik] = std::thread(write_img, ik, d0, d1 - d0);
+      ik ^= 1;
+      g0 = g1;
     }
     if (dma) {  // this window's buffer takes window w + 2
       ts.base[slot] += 2 * TextStream::kWin;
@@ -2017,9 +2051,7 @@ static int run_cli(int argc, char** argv, bool leave_state) {
   bool dev_ok = false;
   std::thread dev_up([&] {
     warm.join();
-    dev_ok = dev.init(qdb, skip_codan) && tstream.init();
-    if (!dev_ok && tstream.st == nullptr && dev.stream != nullptr)
-      fprintf(stderr, "pafreport: pinned host buffers could not be allocated\n");
+    dev_ok = dev.init(qdb, skip_codan) && tstream.init();  // (each prints its own failure)
   });
   bool have = pack_next(bb[0]);
   const double t_pack0 = prof ? now() : 0;

@@ -3616,6 +3616,8 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
       (!args->text && args->text_total))
     return PW_E_ARG;
   if (!args->skip_codan && !args->next_stop) return PW_E_ARG;
+  // (unknown flag bits or a nonzero pad: a caller that left fields unset, e.g. a stack struct)
+  if ((args->flags & ~(uint32_t)PW_REPORT_BUILD_NEXT_STOP) || args->pad || args->skip_codan > 1) return PW_E_ARG;
   const bool build_ns = (args->flags & PW_REPORT_BUILD_NEXT_STOP) && !args->skip_codan;
   if (args->n_alns == 0) {  // (the table is still built when asked for)
     if (build_ns && args->n_queries)

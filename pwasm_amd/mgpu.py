@@ -216,6 +216,7 @@ class OffsetWriter:
         self.nwin = -(-self.n_total // self.W)
         self.j, self.base, self.code, self.done, self.err = 0, 0, 0, False, None
         self.failed = False  # an input error of some rank, all-reduced: the same on every rank
+        self.fatal = False  # the run ended at a fatal line (all-reduced window stop: the same on every rank)
         self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item], ...] in line order
         self.tmp_out = None
         if out_path is None:  # stdout: assembled in a file, streamed out by rank 0 window by window
@@ -326,6 +327,7 @@ class OffsetWriter:
         if stop != self.BIG:  # the exit code is the fatal item's (its owner's status)
             self.code = int(self._reduce([owner], dist.ReduceOp.MAX if self.world > 1 else None)[0])
             self.done = True
+            self.fatal = True
 
     def close(self):
         """Finish every window; -> the exit code of the single-process run."""
@@ -466,7 +468,9 @@ def finish_run(writer, err, gtabs, extra, world, rank, device):
     import torch.distributed as dist
     writer.err = err
     code = writer.close()
-    if writer.failed:
+    # A run that ends at a fatal line writes no genome table: each rank stops at whatever batch it
+    # had reached when that line's window completed, so the rows would depend on timing.
+    if writer.failed or writer.fatal:
         return code
     if "genome-table" in extra:
         names = list(gtabs.keys())

@@ -58,6 +58,16 @@ def test_edge_mix_host_packer(built, tmp_path, seed, monkeypatch):
     same(["-r", fa, paf])
 
 
+@pytest.mark.parametrize("flags", [["-G", "-C"], ["-F", "-N"]])
+def test_cli_report_args_poisoned(built, tmp_path, monkeypatch, flags):
+    """PW_ARGS_POISON=1 fills the CLI's pw_report_args with 0xFF before its fields are assigned
+    (flags / n_queries were left as stack garbage): a field left unset then shows up as
+    PW_E_ARG or a wrong report, never as whatever the stack held."""
+    monkeypatch.setenv("PW_ARGS_POISON", "1")
+    fa, paf = synth_paf(tmp_path, 0, seed=12)
+    same([*flags, "-r", fa, paf])
+
+
 @pytest.mark.parametrize("flags", [[], ["-C"], ["-N"], ["-G"], ["-F"], ["-G", "-C"], ["-F", "-C"]])
 def test_modes(built, tmp_path, flags):
     fa, paf = synth_paf(tmp_path, 0, seed=11)

@@ -304,15 +304,24 @@ def test_cli_many_batches(built, tmp_path, chunk, kind, monkeypatch):
 
 
 @pytest.mark.parametrize("chunk,kind", [(None, None), (3000, None), (20000, "dups"), (5000, "mismatch"),
-                                        (None, "cfg2"), (None, "long"), (60000, "long")])
+                                        (None, "cfg2"), (None, "long"), (60000, "long"), (None, "arena"),
+                                        (None, "cfg2img")])
 def test_cli_output_file(built, tmp_path, chunk, kind, monkeypatch):
     """-o to a regular file (a stale longer file is truncated), one batch or many, clean batches and
     batches with messages / a fatal record: same bytes, stderr and exit code as the oracle."""
     from test_gpu_parity import _inject
     from test_shard import _with_duplicates_and_comments
-    if kind == "cfg2":  # (~90 MB of report: three pinned text windows, written by threads at offsets)
+    if kind in ("cfg2", "cfg2img"):  # (~90 MB of report: three pinned text windows, written by threads)
         fa, paf = synth_paf(tmp_path, 2, seed=31, scale=0.3)
         flags = ["-G", "-C"]
+        if kind == "cfg2img":  # windows cut into 1 MB image groups
+            monkeypatch.setenv("PW_EMIT_IMG_BYTES", str(1 << 20))
+    elif kind == "arena":  # every line kilobytes: most text in arena pages; images capped at 64 KB so
+        # windows are cut into groups and pieces past the cap are written from their sources
+        fa, paf = synth_paf(tmp_path, 0, seed=21, extra=["--subrun", 1.0, "--psub", 1.0, "--pdel", 0, "--pins", 0,
+                                                         "--err", 0.2, "--rev", 0.5])
+        flags = []
+        monkeypatch.setenv("PW_EMIT_IMG_BYTES", "65536")
     elif kind == "long":  # long lines (fixup_kernel) and pages that overflow into the arena
         fa, paf = synth_paf(tmp_path, 0, seed=21, extra=["--longindel", 0.5, "--subrun", 0.6, "--err", 0.05])
         flags = []

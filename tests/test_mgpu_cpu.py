@@ -145,7 +145,9 @@ def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None):
             for k, o in enumerate(outs):
                 w.add(o)
                 w.advance(int(o[4][0][-1]) + 1 if len(o[4][0]) else 0)
-            code = w.close()
+            # (finish_run closes the writer; a run ended by a fatal line writes no genome table)
+            gtab = {f"t{rank}".encode(): np.array([1, 2, 3], np.uint64)}
+            code = mgpu.finish_run(w, None, gtab, {"genome-table": out_path + ".gt"}, world, rank, "cpu")
         q.put((rank, code, n_total, [int(x) for x in line_no]))
         dist.barrier()
     finally:
@@ -190,6 +192,8 @@ def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window):
                    if not ln.startswith(noise))
     assert out.read_bytes() == (tmp_path / "want.out").read_bytes()
     assert err == (tmp_path / "want.err").read_bytes()
+    if window is not None:  # no timing-dependent genome table after a fatal line
+        assert os.path.exists(str(out) + ".gt") == (not fatal)
     # every non-comment line went to exactly one rank, with its global line number
     got = sorted(x for v in res.values() for x in v[2])
     lines = open(paf, "rb").read().replace(b"\r\n", b"\n").split(b"\n")[:-1]
