@@ -8,9 +8,10 @@ configs[1] (cfg2: 100k synthetic minimap2-style records, 1,000 CDS of 1-5 kb, ~1
 errors, run with -G -C).  With N>1 every rank processes its own cfg2-sized shard (different
 seed = different target genomes; weak scaling, no data-path collective; the per-genome tables
 are all-gathered over RCCL every step); the timed region is bracketed by barrier + synchronize,
-the max over ranks is reported.  Beside it at N>1 (sub-object "cfg3"): BASELINE configs[2], the
-one 10M-record set sharded by target genome over the N ranks (strong scaling), and the node's
-end-to-end run of it (pwasm_amd.mgpu).
+the max over ranks is reported.  Beside it at every N, N = 1 included (sub-object "cfg3", and its
+strong-scaling figures as the top-level "scaling_cfg3"): BASELINE configs[2], the one 10M-record
+set sharded by target genome over the N ranks, and the node's end-to-end run of it
+(pwasm_amd.mgpu) — speedup(N) = scaling_cfg3.value(N) / scaling_cfg3.value(1).
 
 `python3 bench.py --gpus N` with no WORLD_SIZE in the environment launches the N ranks itself
 (one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
@@ -59,11 +60,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle diff + end-to-end CLI run")
     ap.add_argument("--remove-gaps", action="store_true", help="cfg5: MSAColumns::removeConsGaps=true")
-    ap.add_argument("--no-e2e", action="store_true", help="N > 1: skip the end-to-end pwasm_amd.mgpu leg")
+    ap.add_argument("--no-e2e", action="store_true", help="cfg3: skip the end-to-end pwasm_amd.mgpu leg")
     ap.add_argument("--no-gapassem", action="store_true", help="N = 1, cfg2: skip the cfg5 (GapAssem) sub-object")
     ap.add_argument("--e2e-parity", action="store_true", help="N > 1: CRC the end-to-end report against the oracle")
-    ap.add_argument("--no-cfg3", action="store_true", help="N > 1: skip the cfg3 (10M records sharded) sub-object")
-    ap.add_argument("--cfg3-scale", type=float, default=1.0, help="N > 1: scale of the cfg3 sub-object's record set")
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 (10M records sharded) sub-object")
+    ap.add_argument("--cfg3-scale", type=float, default=1.0, help="scale of the cfg3 sub-object's record set")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC-derived HBM bytes per pass (profiles/run_prof.sh summary of the same command)")
     args = ap.parse_args()
@@ -112,20 +113,23 @@ def main():
         return
 
     out = report_leg(args, args.config, world, rank, dev_name)
-    if world > 1 and args.config == 2 and not args.no_cfg3:
-        # BASELINE configs[2] beside the weak-scaled line: the one 10M-record set sharded by target
-        # genome over the N ranks (strong scaling) + the node's end-to-end run of it
+    subs = sub_objects(world, args)
+    if "cfg3" in subs:
+        # BASELINE configs[2] beside the cfg2 line, at EVERY N (N = 1 included, so the driver's 1 -> 8
+        # run has the denominator of the north star's scaling target): the one 10M-record set sharded
+        # by target genome over the N ranks (strong scaling) + the node's end-to-end run of it
         torch.cuda.empty_cache()
-        c3 = argparse.Namespace(**{**vars(args), "scale": args.cfg3_scale, "traffic_json": None})
+        c3 = argparse.Namespace(**{**vars(args), "scale": args.cfg3_scale, "traffic_json": None, "no_parity": True,
+                                   "no_cpu_baseline": True})
         sub = report_leg(c3, 3, world, rank, dev_name)
         if rank == 0:
-            out["cfg3"] = {k: sub[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config",
-                                               "roofline", "e2e")}
+            out["cfg3"] = {k: sub[k] for k in CFG3_KEYS}
+            out["scaling_cfg3"] = scaling_cfg3(sub, world)
     if rank == 0:
         out["config"]["ranks"] = world
         out["config"]["backend"] = dist.get_backend() if dist.is_initialized() else "none"
         out["config"]["launcher"] = os.environ.get("PW_BENCH_LAUNCHER", "torchrun" if world > 1 else "single process")
-        if world == 1 and args.config == 2 and not args.no_gapassem:
+        if "gapassem" in subs:
             # BASELINE configs[4] beside it, timed in its own region after the cfg2 one (cfg2's
             # device buffers released first): the GapAssem step, its roofline, parity, CPU baseline
             torch.cuda.empty_cache()
@@ -137,6 +141,34 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+CFG3_KEYS = ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config", "roofline", "e2e")
+
+
+def sub_objects(world, args):
+    """The sub-objects the bench line carries beside its own leg (pure; tests/test_bench_launch.py):
+    "cfg3" (BASELINE configs[2], the 10M-record set sharded over the N ranks) at every N when the
+    line is cfg2, "gapassem" (configs[4]) at N = 1."""
+    subs = []
+    if args.config == 2 and not args.no_cfg3:
+        subs.append("cfg3")
+    if world == 1 and args.config == 2 and not args.no_gapassem:
+        subs.append("gapassem")
+    return subs
+
+
+def scaling_cfg3(sub, world):
+    """Where a scaling reader looks: the strong-scaling figures of the one cfg3 set at this N.  The
+    speedup at N is read from two bench lines of the same command, speedup(N) = value(N) / value(1)
+    (kernel pass over the node, events/s) and e2e_wall_s(1) / e2e_wall_s(N) (PAF text to report
+    file through pwasm_amd.mgpu); north_star's target is >= 6 at N = 8."""
+    e2e = sub.get("e2e") or {}
+    return {"value": sub["value"], "unit": sub["unit"], "n_gpus": world, "scaling": "strong",
+            "records": sub["config"].get("records_total"), "events": sub["config"].get("events_total"),
+            "kernel_ms_per_pass": sub["roofline"]["kernel_ms"], "ms_per_step": sub["ms_per_step"],
+            "e2e_wall_s": e2e.get("wall_s"), "e2e_events_per_s": e2e.get("events_per_s"),
+            "speedup_formula": "value(N) / value(1); e2e: e2e_wall_s(1) / e2e_wall_s(N); same cfg3 set, same scale"}
 
 
 def report_leg(args, config, world, rank, dev_name):
@@ -276,20 +308,24 @@ def report_leg(args, config, world, rank, dev_name):
         tot_events = int(e[0].item())
         tot_records = int(e[1].item())
     e2e_node = None
-    if sharded and world > 1 and not args.no_e2e:
+    if sharded and not args.no_e2e:
         # end to end over the node: pwasm_amd.mgpu (every rank reads 1/N of the PAF, exchanges lines
-        # by target genome, packs / runs / writes its own records at their offsets of one report)
+        # by target genome, packs / runs / writes its own records at their offsets of one report);
+        # at N = 1 the same driver with one rank, so the N-rank walls divide by it
         from pwasm_amd import mgpu
         dev = None
         torch.cuda.empty_cache()
         out_path = os.path.join(shared, "report_e2e.txt")
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         t0 = time.perf_counter()
         code = mgpu.main(["-G", "-C", "-r", fa, paf, "-o", out_path])
-        dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+        wall = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            wall = float(t.item())
         if rank == 0:
             e2e_node = {"wall_s": round(wall, 3), "events_per_s": tot_events / wall, "rc": code,
                         "cmd": f"torchrun x{world} -m pwasm_amd.mgpu -G -C -r q.fa a.paf -o report.txt "
@@ -300,7 +336,8 @@ def report_leg(args, config, world, rank, dev_name):
                     got = crc_stream(f)
                 e2e_node["parity"] = "ok" if code == 0 and got == want[:3] else "FAIL"
             log(f"[e2e] {world} ranks: {wall:.2f} s, rc {code}")
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
 
     if rank == 0:
         report = {}
@@ -380,9 +417,12 @@ def report_leg(args, config, world, rank, dev_name):
                                     f"cfg{config}: {v.n_alns} PAF records/GPU over {v.n_queries} CDS "
                                     f"({'-G -C' if flags else 'auto'}), {n_events} events/GPU"),
                        "records_per_gpu": int(v.n_alns), "events_per_gpu": n_events, "scale": args.scale,
+                       "records_total": tot_records, "events_total": tot_events,
                        "parallelism": (f"shard-by-target x{world} + RCCL all-gather of per-genome tables"
                                        if sharded and world > 1 else
-                                       ("independent per-rank batches" if world > 1 else "single GPU"))},
+                                       ("independent per-rank batches (weak scaling: the same cfg2 work per "
+                                        "GPU at every N; the strong-scaling figure is scaling_cfg3)"
+                                        if world > 1 else "single GPU"))},
             "parity": parity,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

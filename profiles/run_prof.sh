@@ -8,7 +8,7 @@ TAG=${1:-r1}; shift || true
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-parity --no-gapassem $*"
+B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-parity --no-gapassem --no-cfg3 $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $B > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || { echo "trace failed"; exit 1; }
 i=0
 for G in "FETCH_SIZE" "WRITE_SIZE" \

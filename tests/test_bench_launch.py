@@ -56,3 +56,36 @@ def test_bench_refuses_mismatch():
     env = {**os.environ, "WORLD_SIZE": "2"}
     p = subprocess.run([sys.executable, bench.__file__, "--gpus", "4"], env=env, capture_output=True, timeout=60)
     assert p.returncode == 2 and b"WORLD_SIZE=2" in p.stderr
+
+
+def _args(**kw):
+    import argparse
+    base = {"config": 2, "no_cfg3": False, "no_gapassem": False}
+    base.update(kw)
+    return argparse.Namespace(**base)
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_cfg3_sub_object_at_every_n(world):
+    """the N = 1 line carries the cfg3 sub-object too (the denominator of the 1 -> 8
+    strong-scaling curve on BASELINE configs[2]); gapassem only at N = 1."""
+    subs = bench.sub_objects(world, _args())
+    assert "cfg3" in subs
+    assert ("gapassem" in subs) == (world == 1)
+    assert bench.sub_objects(world, _args(no_cfg3=True)) == (["gapassem"] if world == 1 else [])
+    assert bench.sub_objects(world, _args(config=3)) == []
+
+
+def test_scaling_cfg3_keys_same_at_every_n():
+    """scaling_cfg3 has the same keys at N = 1 and N > 1 (speedup(N) = value(N) / value(1))."""
+    def sub(v, n, e2e):
+        return {"value": v, "unit": "events/s", "ms_per_step": 1.0, "e2e": e2e,
+                "config": {"records_total": 10_000_000, "events_total": 208_439_620},
+                "roofline": {"kernel_ms": 18.5 / n}}
+    one = bench.scaling_cfg3(sub(1.1e10, 1, {"wall_s": 6.0, "events_per_s": 3.4e7}), 1)
+    eight = bench.scaling_cfg3(sub(8.0e10, 8, {"wall_s": 1.2, "events_per_s": 1.7e8}), 8)
+    assert one.keys() == eight.keys()
+    assert one["n_gpus"] == 1 and eight["n_gpus"] == 8 and one["scaling"] == "strong"
+    assert eight["value"] / one["value"] > 7 and one["e2e_wall_s"] / eight["e2e_wall_s"] == 5.0
+    assert bench.CFG3_KEYS == ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config", "roofline",
+                               "e2e")
