@@ -777,18 +777,33 @@ def hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp):
 
 def cli_phases(flags_cli, fa, paf, outp):
     """A second CLI run with PW_PROFILE_HOST=1: its own phase timestamps (FASTA load, first batch read
-    + pack, device init, per batch GPU run + result copies and emit, total), parsed from stderr."""
+    + pack, device init, per batch GPU run + result copies and emit, total), parsed from stderr, plus
+    the two ends its own clock cannot see: `process_start` (spawn -> main's first instruction: exec,
+    the dynamic loader and the HIP runtime library's static initialisers) and `exit` (the last
+    instruction -> the parent has reaped it: the kernel's teardown of the process and its GPU
+    state), from wall-clock epochs the CLI prints; `wall_s` is this run's own wall clock."""
     import re
     env = {**os.environ, "PW_PROFILE_HOST": "1"}
+    t_spawn = time.time()
     p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", outp],
                        stderr=subprocess.PIPE, env=env)
+    t_reaped = time.time()
     ph = {}
     for ln in p.stderr.decode(errors="replace").splitlines():
         if not ln.startswith("[cli]"):
             continue
+        m = re.match(r"\[cli\] (main_entry|exit)_epoch ([0-9.]+)", ln)
+        if m:
+            ph["process_start" if m.group(1) == "main_entry" else "exit"] = round(
+                float(m.group(2)) - t_spawn if m.group(1) == "main_entry" else t_reaped - float(m.group(2)), 4)
+            continue
         for name, val in re.findall(r"([a-z][a-z +()\-]*?) ([0-9.]+) s", ln[5:]):
             key = re.sub(r"[^a-z0-9]+", "_", name.strip()).strip("_")
             ph[key] = round(ph.get(key, 0.0) + float(val), 4)
+    if ph:
+        ph["wall_s"] = round(t_reaped - t_spawn, 4)
+        ph["accounted_s"] = round(sum(ph.get(k, 0.0) for k in ("process_start", "total", "close_output", "teardown",
+                                                                  "exit")), 4)
     try:
         os.remove(outp)
     except OSError:

@@ -1886,8 +1886,17 @@ static int run_cli(int argc, char** argv, bool leave_state);
 
 extern "C" int pw_pafreport_main(int argc, char** argv) { return run_cli(argc, argv, false); }
 
+// (PW_PROFILE_HOST: wall-clock epochs at main's entry and just before the process exits, so the
+// caller can attribute its own wall time: process start = entry - spawn, exit = reaped - exit)
+static double epoch_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
 extern "C" int pw_pafreport_main_exit(int argc, char** argv) {
+  const bool prof = getenv("PW_PROFILE_HOST") != nullptr;
+  if (prof) fprintf(stderr, "[cli] main_entry_epoch %.6f\n", epoch_s());
   const int rc = run_cli(argc, argv, true);  // (output files closed; the rest goes with the process)
+  if (prof) fprintf(stderr, "[cli] exit_epoch %.6f\n", epoch_s());
   fflush(stdout);
   fflush(stderr);
   _exit(rc);

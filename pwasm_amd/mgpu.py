@@ -400,13 +400,16 @@ def main(argv=None) -> int:
              (pw.FLAG_C if "C" in opts else 0) | (pw.FLAG_N if "N" in opts else 0))
     dv = device if backend != "gloo" else "cpu"
 
+    prof = _Phases(rank)
     # ---- 1. read 1/N of the PAF, exchange lines by target genome
     text, line_no, n_total = exchange(nonopt[0], world, rank, device, backend)
+    prof.mark("exchange")
 
     # ---- 2. this rank's lines in pipelined batches: batch k + 1 is packed (host threads, no GIL)
     # while the GPU runs batch k and its outputs come back (as the CLI pipelines its chunks)
     target = int(os.environ.get("PW_CHUNK_BYTES", str(256 << 20)))
     cuts = batch_cuts(text, line_no, target)
+    prof.mark("cuts")
     err = None
     made = {}
 
@@ -427,6 +430,7 @@ def main(argv=None) -> int:
         th.start()
     for k in range(len(cuts)):
         th.join()
+        prof.mark("pack wait")
         b = made.pop(k)
         if isinstance(b, RuntimeError):
             err = str(b)
@@ -435,10 +439,15 @@ def main(argv=None) -> int:
             th = threading.Thread(target=make, args=(k + 1, b))
             th.start()
         dev = pw.stage_batch(b, device)
+        prof.mark("stage")
         pw.run_report(b, dev, stream.cuda_stream)
         rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
         launch_genome_table(dev, rows, gt, stream.cuda_stream)
+        if prof.on:
+            stream.synchronize()
+            prof.mark("gpu pass")
         text_h, res_h, pages_h = pw.fetch_outputs(dev)  # (synchronises the stream)
+        prof.mark("fetch")
         r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
         for nm, row in zip(names, r):  # per-genome rows of all batches, summed by target
             acc = gtabs.setdefault(nm, np.zeros(3, np.uint64))
@@ -446,16 +455,41 @@ def main(argv=None) -> int:
         items = b.items(text_h, res_h, pages_h)
         writer.add((b, text_h, res_h, pages_h, items))
         del dev, b
+        prof.mark("items")
         if (items[1] >= 0).any():  # a fatal item: nothing after it is reached
             break
         # ---- 3. the windows this rank's lines so far complete: offsets, pwrites, stderr
         writer.advance(int(line_no[cuts[k + 1][2]]) if k + 1 < len(cuts) else n_total)
+        prof.mark("write windows")
         if writer.done:  # the run ended at a window every rank has processed: nothing later is written
             break
     if th is not None and th.is_alive():
         th.join()
     made.clear()
-    return finish_run(writer, err, gtabs, extra, world, rank, device)
+    code = finish_run(writer, err, gtabs, extra, world, rank, device)
+    prof.mark("finish")
+    prof.report()
+    return code
+
+
+class _Phases:
+    """PW_PROFILE_HOST=1: wall time per phase of main() (summed over batches), one stderr line per rank."""
+
+    def __init__(self, rank):
+        import time
+        self.on = bool(os.environ.get("PW_PROFILE_HOST"))
+        self.rank, self.t, self.acc, self.clock = rank, time.perf_counter(), {}, time.perf_counter
+
+    def mark(self, name):
+        if self.on:
+            t = self.clock()
+            self.acc[name] = self.acc.get(name, 0.0) + t - self.t
+            self.t = t
+
+    def report(self):
+        if self.on:
+            print(f"[mgpu rank {self.rank}] " + ", ".join(f"{k} {v:.3f} s" for k, v in self.acc.items()),
+                  file=sys.stderr, flush=True)
 
 
 def finish_run(writer, err, gtabs, extra, world, rank, device):
