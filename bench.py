@@ -790,6 +790,10 @@ def cli_phases(flags_cli, fa, paf, outp):
     t_reaped = time.time()
     ph = {}
     for ln in p.stderr.decode(errors="replace").splitlines():
+        if ln.startswith("[cli-dev]"):  # (the device side's steps, overlapped with the phases: not summed)
+            ph["device_steps_at"] = {re.sub(r"[^a-z0-9]+", "_", k.strip()).strip("_"): float(v)
+                                     for k, v in re.findall(r"([a-z][a-z +()\-]*?) at ([0-9.]+) s", ln[9:])}
+            continue
         if not ln.startswith("[cli]"):
             continue
         m = re.match(r"\[cli\] (main_entry|exit)_epoch ([0-9.]+)", ln)

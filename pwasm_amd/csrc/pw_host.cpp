@@ -2058,17 +2058,26 @@ static int run_cli(int argc, char** argv, bool leave_state) {
   // the device side comes up beside the first batch's pack: the HIP runtime (warm-up thread), then
   // the queries, their next-stop tables and the pinned text windows
   bool dev_ok = false;
+  double t_warm = 0, t_dinit = 0, t_tsinit = 0;  // (PW_PROFILE_HOST: when each step of dev_up ended)
   std::thread dev_up([&] {
     warm.join();
-    dev_ok = dev.init(qdb, skip_codan) && tstream.init();  // (each prints its own failure)
+    if (prof) t_warm = now();
+    dev_ok = dev.init(qdb, skip_codan);  // (each prints its own failure)
+    if (prof) t_dinit = now();
+    dev_ok = dev_ok && tstream.init();
+    if (prof) t_tsinit = now();
   });
   bool have = pack_next(bb[0]);
   const double t_pack0 = prof ? now() : 0;
   dev_up.join();
   if (!dev_ok) return 2;
-  if (prof)
+  if (prof) {
     fprintf(stderr, "[cli] fasta %.3f s, first batch read + pack %.3f s, device init (after warm-up) %.3f s\n",
             t_fasta - t_start, t_pack0 - t_fasta, now() - t_pack0);
+    // (the device side's own steps from t_start, overlapped with the above: not summed into the total)
+    fprintf(stderr, "[cli-dev] hip runtime up at %.3f s, queries + stop tables at %.3f s, pinned windows at %.3f s\n",
+            t_warm - t_start, t_dinit - t_start, t_tsinit - t_start);
+  }
   while (have) {
     Batch& B = bb[cur];
     const bool more = !B.fatal;
@@ -2599,60 +2608,85 @@ extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, u
 // Output items of a finished batch (the log items up to and including the first one that ends the
 // run, as pw_batch_write_items): their global line, status (-1 = continue, else the exit code) and
 // the bytes each writes to stdout / stderr.
+extern "C" uint64_t pw_batch_item_count(const pw_batch* bt) { return bt ? bt->b.log.size() : 0; }
+
 namespace {
-struct CountCookie {
-  uint64_t n = 0;
-};
-ssize_t count_write(void* c, const char*, size_t n) {
-  static_cast<CountCookie*>(c)->n += n;
-  return (ssize_t)n;
+constexpr char kSoftclipMsg[] = "Warning: soft clipping shouldn't be found in this application!\n";
+// A record item that prints its header, all its lines and nothing on stderr but soft-clip warnings
+// (every item of a clean batch): its bytes are known without formatting it.  Anything else
+// (messages, errors, partial records) goes through emit_item.
+bool item_plain(const Batch& b, const LogItem& it, const pw_aln_result* res) {
+  if (it.kind != 1) return false;
+  const RecHost& rh = b.recs[it.idx];
+  const pw_aln_result& r = res[it.idx];
+  return rh.pre_msg < 0 && r.err == PW_REC_OK && rh.cs_msg < 0 && rh.post_msg < 0 && rh.w_msg < 0 &&
+         !(rh.qlen < 9 && r.n_events > 0);
 }
-struct PwriteCookie {
-  int fd;
-  uint64_t off;
-  bool bad = false;
-};
-ssize_t pwrite_write(void* c, const char* buf, size_t n) {
-  PwriteCookie* k = static_cast<PwriteCookie*>(c);
-  size_t done = 0;
-  while (done < n) {
-    const ssize_t w = pwrite(k->fd, buf + done, n - done, (off_t)(k->off + done));
-    if (w <= 0) {
-      k->bad = true;
-      return done ? (ssize_t)done : -1;
-    }
-    done += (size_t)w;
+// the event-line bytes write_lines prints for all of a record's lines (page spans in chunk order)
+template <class F>
+void for_spans(const pw_aln_result& r, const pw_page* pages, F&& f) {
+  if (r.n_events == 0) return;
+  for (uint32_t c = r.page_first;; c++) {
+    const uint64_t lo = c == r.page_first ? r.text_off : pages[c].off;
+    const uint64_t hi = c == r.page_last ? r.text_end : pages[c].off + pages[c].len;
+    if (hi > lo) f(lo, hi - lo);
+    if (c == r.page_last) break;
   }
-  k->off += n;
-  return (ssize_t)n;
+}
+void plain_sizes(const Batch& b, const LogItem& it, const pw_aln_result* res, const pw_page* pages, uint64_t& out,
+                 uint64_t& err) {
+  const RecHost& rh = b.recs[it.idx];
+  out = rh.hdr_len;
+  for_spans(res[it.idx], pages, [&](uint64_t, uint64_t n) { out += n; });
+  err = rh.n_softclip ? (uint64_t)rh.n_softclip * (sizeof(kSoftclipMsg) - 1 + strlen(b.buf.data() + rh.line_off) + 1) : 0;
+}
+// any item through emit_item into counting / memory streams (the rare items that are not plain)
+int item_slow(const Batch& b, const LogItem& it, const uint8_t* text_host, const pw_aln_result* res, const pw_page* pages,
+              std::string* out, std::string* err, uint64_t* out_n, uint64_t* err_n) {
+  TextSrc src;
+  src.host = text_host;
+  char *ob = nullptr, *eb = nullptr;
+  size_t on = 0, en = 0;
+  FILE* o = open_memstream(&ob, &on);
+  FILE* e = open_memstream(&eb, &en);
+  if (!o || !e) {
+    if (o) fclose(o);
+    if (e) fclose(e);
+    free(ob);
+    free(eb);
+    return INT_MIN;
+  }
+  const int st = emit_item(b, it, src, res, pages, o, e);
+  fclose(o);
+  fclose(e);
+  if (out) out->assign(ob, on);
+  if (err) err->assign(eb, en);
+  if (out_n) *out_n = on;
+  if (err_n) *err_n = en;
+  free(ob);
+  free(eb);
+  return st;
 }
 }  // namespace
-
-extern "C" uint64_t pw_batch_item_count(const pw_batch* bt) { return bt ? bt->b.log.size() : 0; }
 
 extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
                               const pw_page* pages_host, uint64_t* line, int32_t* status, uint64_t* out_len,
                               uint64_t* err_len, uint64_t* n_items) {
   if (!bt || !n_items) return PW_E_ARG;
-  TextSrc src;
-  src.host = text_host;
   uint64_t k = 0;
   for (const LogItem& it : bt->b.log) {
-    CountCookie co, ce;
-    FILE* o = fopencookie(&co, "w", cookie_io_functions_t{nullptr, count_write, nullptr, nullptr});
-    FILE* e = fopencookie(&ce, "w", cookie_io_functions_t{nullptr, count_write, nullptr, nullptr});
-    if (!o || !e) {
-      if (o) fclose(o);
-      if (e) fclose(e);
-      return PW_E_NOMEM;
+    int32_t st = -1;
+    uint64_t on = 0, en = 0;
+    if (item_plain(bt->b, it, res_host)) {
+      plain_sizes(bt->b, it, res_host, pages_host, on, en);
+    } else {
+      st = item_slow(bt->b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en);
+      if (st == INT_MIN) return PW_E_NOMEM;
     }
-    const int32_t st = emit_item(bt->b, it, src, res_host, pages_host, o, e);
-    fclose(o);
-    fclose(e);
     if (line) line[k] = it.line;
     if (status) status[k] = st;
-    if (out_len) out_len[k] = co.n;
-    if (err_len) err_len[k] = ce.n;
+    if (out_len) out_len[k] = on;
+    if (err_len) err_len[k] = en;
     k++;
     if (st >= 0) break;
   }
@@ -2661,36 +2695,89 @@ extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, cons
 }
 
 // Write the stdout bytes of the batch's items [first, first + n_items) at out_off[k - first] of fd
-// (pwrite: ranks write disjoint ranges of one file) and their stderr bytes back to back into err_buf.
+// (pwrite: ranks write disjoint ranges of one file) and their stderr bytes back to back into
+// err_buf.  Items whose destinations follow each other are assembled into one buffer and written
+// by one pwrite (up to 8 MB), by up to host_threads() threads over contiguous item ranges (a
+// per-item pwrite was the multi-GPU driver's largest host cost: 5.2 s for 3 M records).
 extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
                                     const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off,
                                     uint64_t n_items, char* err_buf, uint64_t err_cap) {
   if (!bt || (n_items && !out_off) || first > bt->b.log.size() || n_items > bt->b.log.size() - first)
     return PW_E_ARG;
-  TextSrc src;
-  src.host = text_host;
-  uint64_t eo = 0;
+  const Batch& b = bt->b;
+  // stderr offsets (a sequential pass: plain items only have soft-clip warnings)
+  std::vector<uint64_t> eoff((size_t)n_items + 1, 0);
+  std::vector<uint8_t> plain((size_t)n_items);
   for (uint64_t j = 0; j < n_items; j++) {
-    const uint64_t k = first + j;
-    PwriteCookie pc{fd, out_off[j]};
-    FILE* o = fopencookie(&pc, "w", cookie_io_functions_t{nullptr, pwrite_write, nullptr, nullptr});
-    char* eb = nullptr;
-    size_t en = 0;
-    FILE* e = open_memstream(&eb, &en);
-    if (!o || !e) {
-      if (o) fclose(o);
-      if (e) fclose(e);
+    const LogItem& it = b.log[(size_t)(first + j)];
+    uint64_t on = 0, en = 0;
+    plain[j] = item_plain(b, it, res_host) ? 1 : 0;
+    if (plain[j]) plain_sizes(b, it, res_host, pages_host, on, en);
+    else if (item_slow(b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en) == INT_MIN)
       return PW_E_NOMEM;
-    }
-    emit_item(bt->b, bt->b.log[(size_t)k], src, res_host, pages_host, o, e);
-    fclose(o);
-    fclose(e);
-    if (en && err_buf && eo + en <= err_cap) memcpy(err_buf + eo, eb, en);
-    eo += en;
-    free(eb);
-    if (pc.bad) return PW_E_IO;
+    eoff[j + 1] = eoff[j] + en;
   }
-  return eo <= err_cap || !err_buf ? PW_OK : PW_E_ARG;
+  if (err_buf && eoff[n_items] > err_cap) return PW_E_ARG;
+  constexpr uint64_t kBuf = 8ull << 20;
+  std::atomic<int> rc{PW_OK};
+  auto work = [&](uint64_t j0, uint64_t j1) {
+    std::vector<uint8_t> buf;
+    buf.reserve(1u << 20);
+    uint64_t d0 = 0;  // destination of buf[0]
+    auto flush = [&]() {
+      for (uint64_t done = 0; done < buf.size();) {
+        const ssize_t w = pwrite(fd, buf.data() + done, buf.size() - done, (off_t)(d0 + done));
+        if (w <= 0) {
+          rc = PW_E_IO;
+          break;
+        }
+        done += (uint64_t)w;
+      }
+      buf.clear();
+    };
+    std::string so, se;
+    for (uint64_t j = j0; j < j1 && rc.load() == PW_OK; j++) {
+      const LogItem& it = b.log[(size_t)(first + j)];
+      if (!buf.empty() && (out_off[j] != d0 + buf.size() || buf.size() >= kBuf)) flush();
+      if (buf.empty()) d0 = out_off[j];
+      if (plain[j]) {
+        const RecHost& rh = b.recs[it.idx];
+        const uint8_t* h = reinterpret_cast<const uint8_t*>(b.hdr.data() + rh.hdr_off);
+        buf.insert(buf.end(), h, h + rh.hdr_len);
+        for_spans(res_host[it.idx], pages_host,
+                  [&](uint64_t lo, uint64_t n) { buf.insert(buf.end(), text_host + lo, text_host + lo + n); });
+        if (rh.n_softclip && err_buf) {
+          char* e = err_buf + eoff[j];
+          const char* ln = b.buf.data() + rh.line_off;
+          const size_t ll = strlen(ln);
+          for (int q = 0; q < rh.n_softclip; q++) {
+            memcpy(e, kSoftclipMsg, sizeof(kSoftclipMsg) - 1);
+            e += sizeof(kSoftclipMsg) - 1;
+            memcpy(e, ln, ll);
+            e += ll;
+            *e++ = '\n';
+          }
+        }
+      } else {
+        if (item_slow(b, it, text_host, res_host, pages_host, &so, &se, nullptr, nullptr) == INT_MIN) {
+          rc = PW_E_NOMEM;
+          break;
+        }
+        buf.insert(buf.end(), so.begin(), so.end());
+        if (err_buf && !se.empty()) memcpy(err_buf + eoff[j], se.data(), se.size());
+      }
+    }
+    if (!buf.empty() && rc.load() == PW_OK) flush();
+  };
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), n_items / 4096));
+  if (T <= 1) {
+    work(0, n_items);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(work, n_items * (uint64_t)t / (uint64_t)T, n_items * (uint64_t)(t + 1) / (uint64_t)T);
+    for (auto& x : th) x.join();
+  }
+  return rc.load();
 }
 
 extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,

@@ -348,7 +348,10 @@ FLAGS = {
 
 def build(name):
     s = open(SRC).read()
-    if name == "head":  # pw_report.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
+    if "=" in name:  # name=path: a saved copy of pw_report.hip built as variant `name`
+        name, path = name.split("=", 1)
+        s = open(path).read()
+    elif name == "head":  # pw_report.hip as committed at git HEAD (the A of an A/B against an uncommitted edit)
         s = subprocess.run(["git", "-C", REPO, "show", "HEAD:pwasm_amd/csrc/pw_report.hip"], check=True,
                            capture_output=True, text=True).stdout
     for a, b in PATCHES.get(name, []):
