@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: optional GPU tests (a -k filter), then alternating same-call kernel-trace sweeps of
 # experiment builds (tools/abl_build/<variant>) under the bench (BENCH_ARGS).
-# Usage: tools/gpu_ab.sh <tag> "<pytest -k expr or ->" <rounds> variant...
+# Usage: profiles/scripts/gpu_ab.sh <tag> "<pytest -k expr or ->" <rounds> variant...
 set -uo pipefail
 TAG=$1; K=$2; R=$3; shift 3
 mkdir -p gpurun_out

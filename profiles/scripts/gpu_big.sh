@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: the large configs on one GPU — cfg3 in full (10M records) and cfg4 (>= 1k
 # Mb-contig records) — bench lines with streamed-hash parity + CPU baseline, then a kernel trace of
-# each (no parity).  Usage: bash tools/gpu_big.sh <tag> [cfg4 scale]
+# each (no parity).  Usage: bash profiles/scripts/gpu_big.sh <tag> [cfg4 scale]
 set -uo pipefail
 TAG=${1:-r3}
 S4=${2:-0.102}

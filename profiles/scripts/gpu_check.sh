@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: GPU parity tests, one bench line (with CPU baseline), then the profile passes.
-# Usage: bash tools/gpu_check.sh <tag>
+# Usage: bash profiles/scripts/gpu_check.sh <tag>
 set -uo pipefail
 TAG=${1:-r1}
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box, during kernel development: a fast parity subset, then the cfg2 bench line and a
-# kernel trace.  Usage: tools/gpu_dev.sh <tag> [pytest -k expr]
+# kernel trace.  Usage: profiles/scripts/gpu_dev.sh <tag> [pytest -k expr]
 set -uo pipefail
 TAG=${1:-dev}
 K=${2:-"kat or edge_mix or modes or cfg2 or long_indels or reverse or error_midway"}

@@ -2,7 +2,7 @@
 # On the GPU box: where cfg3's end-to-end CLI time goes.  The full 10M-record cfg3 PAF, the CLI with
 # PW_PROFILE_HOST=1 (per-batch phases), and the file system's own write rate for the same bytes
 # (16 threads, pwrite of 64 MB blocks), so the CLI's output rate can be read against it.
-# Usage: tools/gpu_e2e3.sh <tag> [scale]
+# Usage: profiles/scripts/gpu_e2e3.sh <tag> [scale]
 set -uo pipefail
 TAG=${1:-e3}; S=${2:-1.0}
 O=gpurun_out/e2e_$TAG

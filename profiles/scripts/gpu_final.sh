@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box: the round's judged artefacts in one call — full GPU suite, smoke, the cfg2 and
 # cfg5 bench lines, then the cfg2 and cfg5 profiles (trace + PMC passes).
-# Usage: bash tools/gpu_final.sh <tag>
+# Usage: bash profiles/scripts/gpu_final.sh <tag>
 set -uo pipefail
 TAG=${1:-final}
 mkdir -p gpurun_out

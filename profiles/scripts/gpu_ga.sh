@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: the GapAssem GPU tests, then the cfg5 bench line and its kernel trace.
-# Usage: bash tools/gpu_ga.sh <tag>
+# Usage: bash profiles/scripts/gpu_ga.sh <tag>
 set -uo pipefail
 TAG=${1:-ga}
 mkdir -p gpurun_out/prof_${TAG}_c5

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: multi-rank rehearsals on ONE GPU (gloo collectives; RCCL needs a GPU per rank)
-# and the cfg3 per-GPU throughput at N=1.  Usage: bash tools/gpu_mgpu.sh <tag>
+# and the cfg3 per-GPU throughput at N=1.  Usage: bash profiles/scripts/gpu_mgpu.sh <tag>
 set -uo pipefail
 TAG=${1:-m}
 mkdir -p gpurun_out

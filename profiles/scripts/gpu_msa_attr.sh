@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: tile_counts attribution (tools/exp_msa_variants.py builds): per variant a kernel
-# trace of the cfg5 bench and one PMC pass of the LDS counters.  Usage: tools/gpu_msa_attr.sh <tag> [variants]
+# trace of the cfg5 bench and one PMC pass of the LDS counters.  Usage: profiles/scripts/gpu_msa_attr.sh <tag> [variants]
 set -uo pipefail
 TAG=${1:-ma}; shift
 VS="${*:-cur noflush nowin noruns rp_lds}"

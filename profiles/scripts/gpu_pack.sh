@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: pack_cs_kernel alone (tools/pack_bench.py) — timing + parity, a kernel trace and
-# PMC passes.  Usage: tools/gpu_pack.sh <tag>
+# PMC passes.  Usage: profiles/scripts/gpu_pack.sh <tag>
 set -uo pipefail
 TAG=${1:-pk}
 O=gpurun_out/pack_$TAG

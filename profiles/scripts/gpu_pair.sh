@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: parity of the two-records-per-wave index kernel, then cfg3 (scale 0.2) kernel
-# traces with and without it.  Usage: tools/gpu_pair.sh <tag>
+# traces with and without it.  Usage: profiles/scripts/gpu_pair.sh <tag>
 set -uo pipefail
 TAG=${1:-pair}
 mkdir -p gpurun_out/pair_$TAG

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: PMC passes (one counter group per run) for the kernels matching a regex.
-# Usage: tools/gpu_pmc.sh <tag> <kernel regex> [bench args...]
+# Usage: profiles/scripts/gpu_pmc.sh <tag> <kernel regex> [bench args...]
 set -uo pipefail
 TAG=${1:-p}; KR=${2:-render_kernel}; shift 2
 mkdir -p gpurun_out/pmc_$TAG

@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the GPU box: GPU parity tests then one bench line (no CPU baseline).  Usage: tools/gpu_quick.sh <tag> [pytest -k expr]
+# On the GPU box: GPU parity tests then one bench line (no CPU baseline).  Usage: profiles/scripts/gpu_quick.sh <tag> [pytest -k expr]
 set -uo pipefail
 TAG=${1:-q}
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: the GPU test suite, the default bench line (cfg2 + the cfg5 sub-object), then the
-# large configs at HEAD (tools/gpu_big.sh: full cfg3, cfg4 >= 1,024 records, kernel traces).
+# large configs at HEAD (profiles/scripts/gpu_big.sh: full cfg3, cfg4 >= 1,024 records, kernel traces).
 # Usage: bash profiles/scripts/gpu_r4.sh <tag> [cfg4 scale] [skip-tests]
 set -uo pipefail
 TAG=${1:-r4}
@@ -13,4 +13,4 @@ if [ "${3:-}" != "skip-tests" ]; then
 fi
 timeout -k 10 400 python3 -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed: $?"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
-bash tools/gpu_big.sh $TAG $S4
+bash profiles/scripts/gpu_big.sh $TAG $S4

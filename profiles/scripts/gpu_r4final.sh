@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box, end of round 4: the GPU test suite, the default bench line (cfg2 + cfg5), the cfg2
 # profile (kernel trace + PMC passes, profiles/run_prof.sh), then the large configs
-# (tools/gpu_big.sh: full cfg3, cfg4 at the given scale, kernel traces).
+# (profiles/scripts/gpu_big.sh: full cfg3, cfg4 at the given scale, kernel traces).
 # Usage: bash profiles/scripts/gpu_r4final.sh <tag> [cfg4 scale] [skip-tests]
 set -uo pipefail
 TAG=${1:-r4f}
@@ -16,4 +16,4 @@ timeout -k 10 400 python3 -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out
 cat gpurun_out/bench_$TAG.json
 bash profiles/run_prof.sh ${TAG}_c2 || exit 1
 bash profiles/run_prof.sh ${TAG}_c5 --config 5 || exit 1
-bash tools/gpu_big.sh $TAG $S4
+bash profiles/scripts/gpu_big.sh $TAG $S4

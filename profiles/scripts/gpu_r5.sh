@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box (round 5): the GPU test suite, the default bench line, and a two-rank rehearsal of
 # `bench.py --gpus 2` (bench.py launches both ranks itself; gloo, both on the one card).
-# Usage: bash tools/gpu_r5.sh <tag> [skip-tests] [skip-rehearsal]
+# Usage: bash profiles/scripts/gpu_r5.sh <tag> [skip-tests] [skip-rehearsal]
 set -uo pipefail
 TAG=${1:-r5}
 mkdir -p gpurun_out

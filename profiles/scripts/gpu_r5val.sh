@@ -1,7 +1,7 @@
 #!/bin/bash
 # On the GPU box (round 5): the GPU test suite, the default bench line, and the full cfg3 bench
 # (10 M records: the pass, the CLI end to end with CRC-32 parity against the chunked oracle).
-# Usage: bash tools/gpu_r5val.sh <tag> [skip-tests]
+# Usage: bash profiles/scripts/gpu_r5val.sh <tag> [skip-tests]
 set -uo pipefail
 TAG=${1:-r5v}
 mkdir -p gpurun_out

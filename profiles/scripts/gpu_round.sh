@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: GPU parity tests, then the cfg2 and cfg5 bench lines (with parity + CPU baseline).
-# Usage: bash tools/gpu_round.sh <tag> [pytest -k expr]
+# Usage: bash profiles/scripts/gpu_round.sh <tag> [pytest -k expr]
 set -uo pipefail
 TAG=${1:-r2}
 K=${2:-}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: PMC passes (one group per run) over the cfg2 bench for the report kernels, then a
-# per-kernel table.  Usage: tools/gpu_rpmc.sh <tag> [kernel regex]
+# per-kernel table.  Usage: profiles/scripts/gpu_rpmc.sh <tag> [kernel regex]
 set -uo pipefail
 TAG=${1:-rp}
 RX=${2:-"pw::(render|index|tctx)_kernel"}

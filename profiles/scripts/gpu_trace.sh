@@ -1,5 +1,5 @@
 #!/bin/bash
-# On the GPU box: kernel-trace stats of a short bench run.  Usage: tools/gpu_trace.sh <tag> [extra bench args]
+# On the GPU box: kernel-trace stats of a short bench run.  Usage: profiles/scripts/gpu_trace.sh <tag> [extra bench args]
 set -uo pipefail
 TAG=${1:-t}; shift
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # On the GPU box: the whole GPU test suite, the default bench line (cfg2 + cfg5 sub-object, CPU
-# baseline), then the cfg2 profile (kernel trace + PMC passes).  Usage: bash tools/gpu_val.sh <tag>
+# baseline), then the cfg2 profile (kernel trace + PMC passes).  Usage: bash profiles/scripts/gpu_val.sh <tag>
 set -uo pipefail
 TAG=${1:-val}
 mkdir -p gpurun_out

@@ -6,7 +6,13 @@ or of the GapAssem calls).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so traffic is taken as
-2*FETCH + WRITE (an upper bound for the narrower, uncalibrated accesses).
+2*FETCH + WRITE.  Round 6 calibrated the factor on the patterns these kernels use
+(profiles/calib/fetch_calib.hip, profiles/r6_calib/calibration.md: 2 GiB buffers, known bytes):
+FETCH_SIZE is exactly 1/2 of the 128-B line fills for coalesced 16 B/lane streams, 4 B and 16 B
+per-lane gathers (one lane per line) and 48-byte per-lane windows alike — every L2 miss fetches a
+whole 128-B line and is tallied at 64 B — so 2*FETCH is the memory-side read traffic of every
+read pattern here (L2 misses: Infinity-Cache hits included).  WRITE_SIZE is exact for streaming
+stores and counts a 32-B sector for each partial-line store.
 
 Occupancy (achieved waves per SIMD, per kernel) = 4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8) /
 (4 * CUs): SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md, SQ PMC units) summed over every
@@ -51,10 +57,12 @@ def main(src, out, bench_args=""):
         "pass_us": sum(k["avg_us"] for k in pw),
         "pmc_per_launch": per,
         "hbm_fetch_bytes_raw": fetch,
+        "per_kernel_bytes": {k: {"read": 2 * c.get("FETCH_SIZE", 0) * 1024, "write": c.get("WRITE_SIZE", 0) * 1024}
+                             for k, c in per.items() if "FETCH_SIZE" in c or "WRITE_SIZE" in c},
         "hbm_write_bytes": write,
         "hbm_bytes_per_launch": 2 * fetch + write,
-        "hbm_bytes_note": "one pass = one launch of every pw:: kernel; 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes, "
-                          "gfx950 FETCH_SIZE halving applied)",
+        "hbm_bytes_note": "one pass = one launch of every pw:: kernel; 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes; "
+                          "the factor 2 calibrated for every read pattern here: profiles/r6_calib/calibration.md)",
     }
     for k, c in per.items():
         if c.get("SQ_LDS_IDX_ACTIVE"):
@@ -76,6 +84,12 @@ def main(src, out, bench_args=""):
         f.write("achieved waves/SIMD: " + ", ".join(f"{k} {v}" for k, v in res["occupancy_waves_per_simd"].items()) + "\n")
         f.write(f"HBM bytes per pass (2*FETCH + WRITE): {res['hbm_bytes_per_launch'] / 1e6:.1f} MB "
                 f"(FETCH {fetch / 1e6:.1f} MB raw, WRITE {write / 1e6:.1f} MB)\n")
+        f.write("\n| kernel | reads (2*FETCH) MB | writes MB | us |\n|---|---|---|---|\n")
+        us = {k["name"]: k["avg_us"] for k in kern}
+        for k, c in sorted(per.items()):
+            if "FETCH_SIZE" in c or "WRITE_SIZE" in c:
+                f.write(f"| {k} | {2 * c.get('FETCH_SIZE', 0) * 1024 / 1e6:.1f} | {c.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f} | "
+                        f"{us.get(k, 0):.1f} |\n")
         for k, c in sorted(per.items()):
             f.write(f"\n## {k} (per launch)\n\n")
             for n, v in sorted(c.items()):

@@ -297,11 +297,10 @@ class OffsetWriter:
             b, text_h, res_h, pages_h, (ln, st, on, en) = ent[0]
             eb = b.write_range(text_h, res_h, pages_h, self.fd, c, off[ln[c:k].astype(np.int64) - lo],
                                int(en[c:k].sum()))
-            p = 0
-            for i in range(c, k):
-                if en[i]:
-                    errs.append((int(ln[i]), eb[p:p + int(en[i])]))
-                    p += int(en[i])
+            nz = c + np.flatnonzero(en[c:k])  # (items with stderr bytes: few, a Python loop over them only)
+            ends = np.cumsum(en[nz].astype(np.int64))
+            for i, e1, n in zip(nz, ends, en[nz]):
+                errs.append((int(ln[i]), eb[int(e1) - int(n):int(e1)]))
             ent[1] = k
         self.pending = [e for e in self.pending if e[1] < len(e[0][4][0])]
         if self.world > 1:  # (every rank's pwrites are done once rank 0 has its stderr)
