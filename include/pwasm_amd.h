@@ -455,6 +455,17 @@ int pw_batch_write_at(const pw_batch* b, const uint8_t* text_host, const pw_aln_
 int pw_batch_write_range(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                          const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off, uint64_t n_items,
                          char* err_buf, uint64_t err_cap);
+/* pw_batch_render_range: the stdout bytes of the items [first, first + n_items) back to back into
+ * out_buf (capacity out_cap: the sum of their pw_batch_items stdout counts) and their stderr bytes
+ * into err_buf.  pw_gather_write: the spans src[src_off[k], + len[k]) in order, written
+ * contiguously into fd from file_off (host threads, large pwrites).  Together the multi-GPU
+ * driver's exchange write: ranks render their items of a window, exchange them (all-to-all) so
+ * that each holds one contiguous byte range of the window, and write that range. */
+int pw_batch_render_range(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
+                          const pw_page* pages_host, uint64_t first, uint64_t n_items, uint8_t* out_buf, uint64_t out_cap,
+                          char* err_buf, uint64_t err_cap);
+int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                    uint64_t n);
 
 /* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
  * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its

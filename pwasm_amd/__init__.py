@@ -183,6 +183,10 @@ _SIGS = {
                                                                  ctypes.c_void_p, ctypes.c_uint64]),
     "pw_batch_write_range": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
                                                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
+    "pw_batch_render_range": (ctypes.c_int, [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
+    "pw_gather_write": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint64]),
     "pw_batch_genomes": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
@@ -357,6 +361,19 @@ class HostBatch:
             raise RuntimeError(f"pw_batch_write_range: {rc}")
         return eb.raw[: int(err_bytes)]
 
+    def render_range(self, text_host, results_host, pages_host, first: int, out_bytes: int, n_items: int,
+                     err_bytes: int):
+        """pw_batch_render_range: (stdout bytes of items [first, first + n_items) back to back as a
+        uint8 array of out_bytes, their stderr bytes)."""
+        out = np.empty(max(int(out_bytes), 1), dtype=np.uint8)
+        eb = ctypes.create_string_buffer(max(int(err_bytes), 1))
+        rc = lib().pw_batch_render_range(self._h, text_host.ctypes.data, results_host.ctypes.data,
+                                         pages_host.ctypes.data, int(first), int(n_items), out.ctypes.data,
+                                         int(out_bytes), eb, int(err_bytes))
+        if rc != 0:
+            raise RuntimeError(f"pw_batch_render_range: {rc}")
+        return out[: int(out_bytes)], eb.raw[: int(err_bytes)]
+
     def array(self, name: str):
         import numpy as np
         v = self.view
@@ -530,6 +547,17 @@ def stage_batch(batch: HostBatch, device: str = "cuda:0") -> dict:
     dev["results"] = torch.empty(max(int(v.n_alns), 1) * ctypes.sizeof(AlnResult), dtype=torch.uint8,
                                  device=device)
     return dev
+
+
+def gather_write(fd: int, file_off: int, src, src_off, lens) -> None:
+    """pw_gather_write: spans src[src_off[k], + lens[k]) in order, written contiguously at file_off."""
+    src_off = np.ascontiguousarray(src_off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    rc = lib().pw_gather_write(int(fd), int(file_off), src.ctypes.data if src.size else None,
+                               src_off.ctypes.data if src_off.size else None, lens.ctypes.data if lens.size else None,
+                               int(lens.size))
+    if rc != 0:
+        raise RuntimeError(f"pw_gather_write: {rc}")
 
 
 def items_merge(paths, out_path=None, err_path=None) -> int:

@@ -2780,6 +2780,122 @@ extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host
   return rc.load();
 }
 
+// The stdout bytes of the items [first, first + n_items) back to back into out_buf and their stderr
+// bytes into err_buf (the multi-GPU driver's exchange write: a rank renders its items of a window,
+// the ranks exchange them so that each holds one contiguous byte range of the file, and each range
+// goes out with large pwrites — pw_gather_write).
+extern "C" int pw_batch_render_range(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
+                                     const pw_page* pages_host, uint64_t first, uint64_t n_items, uint8_t* out_buf,
+                                     uint64_t out_cap, char* err_buf, uint64_t err_cap) {
+  if (!bt || first > bt->b.log.size() || n_items > bt->b.log.size() - first || (n_items && !out_buf && out_cap))
+    return PW_E_ARG;
+  const Batch& b = bt->b;
+  std::vector<uint64_t> ooff((size_t)n_items + 1, 0), eoff((size_t)n_items + 1, 0);
+  std::vector<uint8_t> plain((size_t)n_items);
+  for (uint64_t j = 0; j < n_items; j++) {
+    const LogItem& it = b.log[(size_t)(first + j)];
+    uint64_t on = 0, en = 0;
+    plain[j] = item_plain(b, it, res_host) ? 1 : 0;
+    if (plain[j]) plain_sizes(b, it, res_host, pages_host, on, en);
+    else if (item_slow(b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en) == INT_MIN)
+      return PW_E_NOMEM;
+    ooff[j + 1] = ooff[j] + on;
+    eoff[j + 1] = eoff[j] + en;
+  }
+  if (ooff[n_items] > out_cap || (err_buf && eoff[n_items] > err_cap)) return PW_E_ARG;
+  std::atomic<int> rc{PW_OK};
+  auto work = [&](uint64_t j0, uint64_t j1) {
+    std::string so, se;
+    for (uint64_t j = j0; j < j1; j++) {
+      const LogItem& it = b.log[(size_t)(first + j)];
+      uint8_t* o = out_buf + ooff[j];
+      if (plain[j]) {
+        const RecHost& rh = b.recs[it.idx];
+        memcpy(o, b.hdr.data() + rh.hdr_off, rh.hdr_len);
+        o += rh.hdr_len;
+        for_spans(res_host[it.idx], pages_host, [&](uint64_t lo, uint64_t n) {
+          memcpy(o, text_host + lo, n);
+          o += n;
+        });
+        if (rh.n_softclip && err_buf) {
+          char* e = err_buf + eoff[j];
+          const char* ln = b.buf.data() + rh.line_off;
+          const size_t ll = strlen(ln);
+          for (int q = 0; q < rh.n_softclip; q++) {
+            memcpy(e, kSoftclipMsg, sizeof(kSoftclipMsg) - 1);
+            e += sizeof(kSoftclipMsg) - 1;
+            memcpy(e, ln, ll);
+            e += ll;
+            *e++ = '\n';
+          }
+        }
+      } else {
+        if (item_slow(b, it, text_host, res_host, pages_host, &so, &se, nullptr, nullptr) == INT_MIN) {
+          rc = PW_E_NOMEM;
+          return;
+        }
+        memcpy(o, so.data(), so.size());
+        if (err_buf && !se.empty()) memcpy(err_buf + eoff[j], se.data(), se.size());
+      }
+    }
+  };
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), n_items / 4096));
+  if (T <= 1) {
+    work(0, n_items);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(work, n_items * (uint64_t)t / (uint64_t)T, n_items * (uint64_t)(t + 1) / (uint64_t)T);
+    for (auto& x : th) x.join();
+  }
+  return rc.load();
+}
+
+// Spans src[src_off[k], + len[k]) for k = 0..n-1, in order, written contiguously to fd from
+// file_off: host threads assemble consecutive parts of the range and pwrite each in 8 MB blocks.
+extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
+                               uint64_t n) {
+  if (n && (!src || !src_off || !len)) return PW_E_ARG;
+  std::vector<uint64_t> dst((size_t)n + 1, 0);
+  for (uint64_t k = 0; k < n; k++) dst[k + 1] = dst[k] + len[k];
+  const uint64_t total = dst[n];
+  if (total == 0) return PW_OK;
+  constexpr uint64_t kBlk = 8ull << 20;
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), total / kBlk));
+  std::atomic<int> rc{PW_OK};
+  auto work = [&](int t) {
+    const uint64_t a = total * (uint64_t)t / (uint64_t)T, z = total * (uint64_t)(t + 1) / (uint64_t)T;
+    std::vector<uint8_t> buf((size_t)std::min<uint64_t>(kBlk, z - a));
+    uint64_t k = (uint64_t)(std::upper_bound(dst.begin(), dst.end(), a) - dst.begin()) - 1;  // span holding byte a
+    for (uint64_t x = a; x < z && rc.load() == PW_OK;) {
+      const uint64_t bn = std::min<uint64_t>(kBlk, z - x);
+      uint64_t f = 0;
+      while (f < bn) {  // fill the block from the spans
+        while (dst[k + 1] <= x + f) k++;
+        const uint64_t in = x + f - dst[k], c = std::min<uint64_t>(len[k] - in, bn - f);
+        memcpy(buf.data() + f, src + src_off[k] + in, (size_t)c);
+        f += c;
+      }
+      for (uint64_t done = 0; done < bn;) {
+        const ssize_t w = pwrite(fd, buf.data() + done, (size_t)(bn - done), (off_t)(file_off + x + done));
+        if (w <= 0) {
+          rc = PW_E_IO;
+          break;
+        }
+        done += (uint64_t)w;
+      }
+      x += bn;
+    }
+  };
+  if (T <= 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  return rc.load();
+}
+
 extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
                                  const pw_page* pages_host, int fd, const uint64_t* out_off, uint64_t n_items,
                                  char* err_buf, uint64_t err_cap) {

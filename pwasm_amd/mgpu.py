@@ -217,6 +217,9 @@ class OffsetWriter:
         self.j, self.base, self.code, self.done, self.err = 0, 0, 0, False, None
         self.failed = False  # an input error of some rank, all-reduced: the same on every rank
         self.fatal = False  # the run ended at a fatal line (all-reduced window stop: the same on every rank)
+        # world > 1: "exchange" (each rank writes one contiguous range of each window, _exchange_write)
+        # or "pwrite" (each rank pwrites its own items at their offsets); PW_MGPU_WRITE picks
+        self.mode = os.environ.get("PW_MGPU_WRITE", "exchange")
         self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item], ...] in line order
         self.tmp_out = None
         if out_path is None:  # stdout: assembled in a file, streamed out by rank 0 window by window
@@ -273,6 +276,8 @@ class OffsetWriter:
                 sys.stderr.flush()
             self.code, self.done, self.failed = 1, True, True
             return
+        # per line of the window: its stdout bytes * 256 + (owner rank + 1), summed over the ranks (one
+        # owner per line): the byte counts, and the owners the exchange write needs
         lens = np.zeros(hi - lo, dtype=np.int64)
         spans, owner = [], -1
         for ent in self.pending:
@@ -281,27 +286,37 @@ class OffsetWriter:
             spans.append((c, k))
             if k > c and int(ln[k - 1]) == stop:
                 owner = int(st[k - 1])
-            lens[ln[c:k].astype(np.int64) - lo] = on[c:k].astype(np.int64)
+            lens[ln[c:k].astype(np.int64) - lo] = on[c:k].astype(np.int64) * 256 + (self.rank + 1)
         if self.world > 1:
             tl = torch.from_numpy(lens).to(self.dv)
             dist.all_reduce(tl, op=dist.ReduceOp.SUM)
             lens = tl.cpu().numpy()
+        own = (lens & 255).astype(np.int64) - 1  # (-1: a line no rank has an item for)
+        lens >>= 8
         off = np.empty(hi - lo + 1, dtype=np.int64)
         off[0] = self.base
         np.cumsum(lens, out=off[1:])
         off[1:] += self.base
         errs = []
+        exch = self.world > 1 and self.mode == "exchange"
+        mine = []
         for ent, (c, k) in zip(self.pending, spans):
             if k == c:
                 continue
             b, text_h, res_h, pages_h, (ln, st, on, en) = ent[0]
-            eb = b.write_range(text_h, res_h, pages_h, self.fd, c, off[ln[c:k].astype(np.int64) - lo],
-                               int(en[c:k].sum()))
+            if exch:  # this rank's items of the window, rendered back to back (line order)
+                out, eb = b.render_range(text_h, res_h, pages_h, c, int(on[c:k].sum()), k - c, int(en[c:k].sum()))
+                mine.append(out)
+            else:
+                eb = b.write_range(text_h, res_h, pages_h, self.fd, c, off[ln[c:k].astype(np.int64) - lo],
+                                   int(en[c:k].sum()))
             nz = c + np.flatnonzero(en[c:k])  # (items with stderr bytes: few, a Python loop over them only)
             ends = np.cumsum(en[nz].astype(np.int64))
             for i, e1, n in zip(nz, ends, en[nz]):
                 errs.append((int(ln[i]), eb[int(e1) - int(n):int(e1)]))
             ent[1] = k
+        if exch:
+            self._exchange_write(lens, own, off, mine)
         self.pending = [e for e in self.pending if e[1] < len(e[0][4][0])]
         if self.world > 1:  # (every rank's pwrites are done once rank 0 has its stderr)
             allerr = [None] * self.world if self.rank == 0 else None
@@ -327,6 +342,47 @@ class OffsetWriter:
             self.code = int(self._reduce([owner], dist.ReduceOp.MAX if self.world > 1 else None)[0])
             self.done = True
             self.fatal = True
+
+    def _exchange_write(self, lens, own, off, mine):
+        """Exchange write of one window (world > 1): the window's bytes are cut into one contiguous
+        range per rank at line boundaries; every rank sends each of its rendered items to the rank
+        whose range holds it (all_to_all_single: RCCL over xGMI with the nccl backend), and each
+        rank writes its whole range with large pwrites (pw_gather_write) — instead of one pwrite per
+        item, which serialised the ranks on the output file's inode lock (a rank's lines are
+        interleaved with every other rank's: lines are routed by target genome)."""
+        import torch
+        import torch.distributed as dist
+
+        import pwasm_amd as pw
+        n, W, r = len(lens), self.world, self.rank
+        start = off[:-1] - off[0]
+        total = int(off[-1] - off[0])
+        cut = np.searchsorted(start, [total * q // W for q in range(W)], side="left").astype(np.int64)
+        cut = np.append(cut, n)
+        cut[0] = 0
+        idx = np.flatnonzero(own == r)
+        dest = np.searchsorted(cut[1:], idx, side="right")
+        send = np.bincount(dest, weights=lens[idx], minlength=W).astype(np.int64)
+        a, z = int(cut[r]), int(cut[r + 1])
+        rng = a + np.flatnonzero(lens[a:z] > 0)
+        o_r = own[rng]
+        recv = np.bincount(o_r, weights=lens[rng], minlength=W).astype(np.int64)
+        buf = np.concatenate(mine) if mine else np.zeros(0, np.uint8)
+        if buf.size != int(send.sum()):
+            raise RuntimeError("mgpu: rendered window bytes disagree with the item counts")
+        st = torch.from_numpy(buf).to(self.dv)
+        rt = torch.empty(int(recv.sum()), dtype=torch.uint8, device=self.dv)
+        dist.all_to_all_single(rt, st, [int(x) for x in recv], [int(x) for x in send])
+        got = rt.cpu().numpy()
+        if rng.size:
+            l_r = lens[rng]
+            base = np.concatenate([[0], np.cumsum(recv)[:-1]])
+            src = np.empty(rng.size, dtype=np.int64)
+            for q in range(W):  # (a source's items arrive in line order)
+                m = o_r == q
+                lq = l_r[m]
+                src[m] = base[q] + np.cumsum(lq) - lq
+            pw.gather_write(self.fd, int(off[a]), got, src, l_r)
 
     def close(self):
         """Finish every window; -> the exit code of the single-process run."""

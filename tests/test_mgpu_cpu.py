@@ -115,9 +115,9 @@ def _paf_with_everything(tmp_path, fatal):
     return fa, str(p)
 
 
-def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None):
+def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None, mode="exchange"):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PW_MGPU_WRITE=mode)
     fd = os.open(errf, os.O_WRONLY | os.O_CREAT | os.O_TRUNC)
     os.dup2(fd, 2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -154,9 +154,11 @@ def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,fatal,window", [(2, False, None), (2, True, None), (3, True, None), (2, False, 7),
-                                                (3, True, 5)])
-def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window):
+@pytest.mark.parametrize("world,fatal,window,mode", [(2, False, None, "exchange"), (2, True, None, "exchange"),
+                                                     (3, True, None, "exchange"), (2, False, 7, "exchange"),
+                                                     (3, True, 5, "exchange"), (3, False, 7, "exchange"),
+                                                     (2, True, 5, "pwrite"), (3, False, None, "pwrite")])
+def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window, mode):
     """mgpu's scalable host path on the CPU (gloo): each rank reads 1/N of the PAF by byte range
     (pw_paf_split), lines are exchanged by target genome (all_to_all_single), packed in several
     batches per rank (the q~t dedupe state carried over), and written at offsets from an
@@ -175,7 +177,7 @@ def test_exchange_and_offset_write_gloo(built, tmp_path, world, fatal, window):
     port = _port()
     out = tmp_path / "got.out"
     ps = [ctx.Process(target=_exchange_rank, args=(r, world, port, fa, paf, str(out), str(tmp_path / f"e{r}"), q,
-                                                   window))
+                                                   window, mode))
           for r in range(world)]
     for p in ps:
         p.start()

@@ -9,7 +9,7 @@ VS="$*"
 [ -z "$VS" ] && VS=$(ls tools/abl_build)
 for v in $VS; do
   export PWASM_LIB=$PWD/tools/abl_build/$v/lib/libpwasm_amd.so
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/sw_$TAG/$v -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 2 ${BENCH_ARGS:-} > gpurun_out/sw_${TAG}_$v.json 2> gpurun_out/sw_${TAG}_$v.err || { echo "variant $v failed: $?"; tail -5 gpurun_out/sw_${TAG}_$v.err; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/sw_$TAG/$v -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-cfg3 --steps 10 --warmup 2 ${BENCH_ARGS:---no-gapassem} > gpurun_out/sw_${TAG}_$v.json 2> gpurun_out/sw_${TAG}_$v.err || { echo "variant $v failed: $?"; tail -5 gpurun_out/sw_${TAG}_$v.err; exit 1; }
   f=$(find gpurun_out/sw_$TAG/$v -name "*kernel_stats.csv" | head -1)
   par=$(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d.get('parity'), round(d['roofline']['kernel_ms'],4))" gpurun_out/sw_${TAG}_$v.json)
   echo "== $v parity/kernel_ms: $par"
