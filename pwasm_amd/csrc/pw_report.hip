@@ -219,23 +219,6 @@ __device__ __forceinline__ uint8_t litb(const RecFast& r, uint32_t i) {
   const uint32_t o = i - r.ls0;
   return (uint8_t)((o < 4 ? r.lit0 : r.lit1) >> (8 * (o & 3)));
 }
-// tctx_kernel's record: literal bytes [lb, lb + 20) in registers — the event's own and its
-// neighbours' (a slow target context crosses the S / insertion ops within 5 bases of the event,
-// whose literal bytes lie up to 8 before the event's; with only the event's 8 bytes in registers
-// those were one dependent global load per byte)
-struct RecT : Rec {
-  uint32_t lb;     // literal index of lq[0]'s first byte
-  uint32_t lq[5];
-};
-__device__ __forceinline__ uint8_t litb(const RecT& r, uint32_t i) {
-  const uint32_t o = i - r.lb;
-  if (o < 20u) {
-    const uint32_t k = o >> 2;
-    const uint32_t w = k == 0 ? r.lq[0] : (k == 1 ? r.lq[1] : (k == 2 ? r.lq[2] : (k == 3 ? r.lq[3] : r.lq[4])));
-    return (uint8_t)(w >> (8 * (o & 3)));
-  }
-  return lit_global(r.lits, i);
-}
 __device__ __forceinline__ uint32_t opword(const Rec& r, uint32_t j) {
   const unsigned o = (unsigned)((int)j - r.op_lo);
   return o < r.op_n ? r.opw[o] : r.ops[j];
@@ -506,8 +489,8 @@ struct Cursor {
   int ts, qs;
   uint32_t ls, w;
 };
-template <class S, class R>
-__device__ __forceinline__ void emit_tseq(S& k, const R& r, Cursor c, int p0, int p1, int base) {
+template <class S>
+__device__ __forceinline__ void emit_tseq(S& k, const Rec& r, Cursor c, int p0, int p1, int base) {
   while (c.ts > p0 && c.j > 0) {  // step back to the op holding p0
     c.j--;
     c.w = opword(r, c.j);
@@ -693,8 +676,8 @@ __device__ __forceinline__ void emit_tctx_fast(S& k, const R& r, uint32_t typ, i
 
 // The tctx field by walking the op stream (setTContext, pafreport.cpp:120-128; revCompl :631;
 // abbreviation first5[len-10]last5, :918-927).
-template <class S, class R>
-__device__ __forceinline__ void emit_tctx_walk(S& k, const R& r, uint32_t typ, int n, uint32_t j, uint32_t wd,
+template <class S>
+__device__ __forceinline__ void emit_tctx_walk(S& k, const Rec& r, uint32_t typ, int n, uint32_t j, uint32_t wd,
                                                int qs, int ts, uint32_t ls) {
   const TGeom g = tgeom(r.T, typ, n, ts);
   Cursor cur;
@@ -1842,10 +1825,6 @@ __device__ __forceinline__ IdxBlk block_of(const Work& W, const pw_aln_desc& d, 
   return B;
 }
 
-// kH16: the batch keeps 16-byte event records (W.hot_pbits != 0), which do not carry an event's
-// first literal bytes — the per-op literal words are then not loaded (one dword for the '*' op's
-// query base instead of a byte and three dwords: index is bound by its vector-memory units)
-template <bool kH16>
 __device__ __forceinline__ void index_record(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
                                              LDS IndexWave* w, uint32_t ai, int lane, const RecPre& pre,
                                              const IdxBlk& B) {
@@ -1931,16 +1910,10 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
       const int qp = d.offset + qs[k];
       const int qc = qp < 0 ? 0 : (qp >= L ? (L > 0 ? L - 1 : 0) : qp);
       qref[k] = R[rev ? (L > 0 ? L - 1 - qc : 0) : qc];
-      if constexpr (kH16) {  // (the '*' op's cs query base, byte ls + 1, from one dword)
-        const uint32_t lq = ls[k] + 1u;
-        qlit[k] = (uint8_t)(lits32[lq >> 2] >> (8 * (lq & 3u)));
-        lw[k][0] = lw[k][1] = lw[k][2] = 0u;
-      } else {
-        const uint32_t la = ls[k] >> 2;
+      qlit[k] = A.lits[ls[k] + 1];
+      const uint32_t la = ls[k] >> 2;
 #pragma unroll
-        for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
-        qlit[k] = (uint8_t)(__builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], ls[k] & 3u) >> 8);
-      }
+      for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
     }
     // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads
     uint64_t subm[2], hm[2];
@@ -1982,15 +1955,13 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
     }
     // every event head's first 8 literal bytes, for both halves now: a load first consumed after
     // the first half's Hot stores would make the compiler wait for those stores too (vmcnt(0))
-    uint32_t hl0[2] = {0u, 0u}, hl1[2] = {0u, 0u};
-    if constexpr (!kH16) {
+    uint32_t hl0[2], hl1[2];
 #pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const uint32_t sh = ls[k] & 3u;
-        hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
-        hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
-        asm volatile("" : "+v"(hl0[k]), "+v"(hl1[k]));  // (kept here, not sunk into the store branch)
-      }
+    for (int k = 0; k < 2; k++) {
+      const uint32_t sh = ls[k] & 3u;
+      hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
+      hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
+      asm volatile("" : "+v"(hl0[k]), "+v"(hl1[k]));  // (kept here, not sunk into the store branch)
     }
     // ---- events of this segment: creation index, S-run length, target context
     const uint32_t n0 = (uint32_t)__popcll(hm[0]);
@@ -2159,7 +2130,6 @@ __device__ __forceinline__ void index_record(const pw_report_args& A, const Work
 // index_kernel's (and index_pair_kernel's) end: blocks 1.. of the long records, spread over all
 // wavefronts (a record of 1-5 Mb walked by one wave would be the whole kernel's critical path), and
 // the padding slots of the last chunk (empty)
-template <bool kH16>
 __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
                                                   LDS IndexWave* w, int lane, int wv, uint32_t stride, bool planned,
                                                   uint32_t bid) {
@@ -2174,7 +2144,7 @@ __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const
       rec_pre_ready(A, p, lane);
       IdxBlk B = block_of(W, p.d, i - k, (p.d.n_ops + kBlkOps - 1) / kBlkOps, k, lane);
       B.prev_sub = (A.ops[p.d.op_begin + B.sb0 - 1] >> 30) == PW_OP_SUB;
-      index_record<kH16>(A, W, tp, w, bai, lane, p, B);
+      index_record(A, W, tp, w, bai, lane, p, B);
     }
   }
   const uint64_t pad0 = A.n_ev_slots, pad1 = W.n_chunks * kWave;
@@ -2185,7 +2155,6 @@ __device__ __forceinline__ void index_long_blocks(const pw_report_args& A, const
     }
 }
 
-template <bool kH16>
 __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
@@ -2222,7 +2191,7 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
         if (base != kNoBlk)
           B = block_of(W, cur.d, base, (cur.d.n_ops + kBlkOps - 1) / kBlkOps, 0u, lane);
       }
-      index_record<kH16>(A, W, tp, w, ai, lane, cur, B);
+      index_record(A, W, tp, w, ai, lane, cur, B);
       // (first consumed here, where the record's segment loads have already waited for them:
       // consumed at the top of the next iteration, the wait would also cover this record's stores)
       rec_pre_ready(A, nxt, lane);
@@ -2232,7 +2201,7 @@ __global__ __launch_bounds__(kWave* kWaves, kIndexOcc) void index_kernel(pw_repo
       dn = dnn;
     }
   }
-  index_long_blocks<kH16>(A, W, tp, w, lane, wv, stride, planned, bid);
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned, bid);
 }
 
 // ------------------------------------------------------------------ index_kernel, two short records per wave
@@ -2280,7 +2249,6 @@ __device__ __forceinline__ void pair_head(const pw_report_args& A, uint32_t ri, 
 }
 
 // the two records of a pair unit (record ri of this lane's half; valid = it exists)
-template <bool kH16>
 __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
                                            LDS IndexWave* w, uint32_t ai, bool valid, int lane, const PairHead& P) {
   const int hl = lane & 31, half = lane >> 5;
@@ -2328,16 +2296,10 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
     const int qp = d.offset + qs[k];
     const int qc = qp < 0 ? 0 : (qp >= L ? (L > 0 ? L - 1 : 0) : qp);
     qref[k] = R[rev ? (L > 0 ? L - 1 - qc : 0) : qc];
-    if constexpr (kH16) {  // (16-byte records: no literal words, the '*' op's query base from one dword)
-      const uint32_t lq = ls[k] + 1u;
-      qlit[k] = (uint8_t)(lits32[lq >> 2] >> (8 * (lq & 3u)));
-      lw[k][0] = lw[k][1] = lw[k][2] = 0u;
-    } else {
-      const uint32_t la = ls[k] >> 2;
+    qlit[k] = A.lits[ls[k] + 1];
+    const uint32_t la = ls[k] >> 2;
 #pragma unroll
-      for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
-      qlit[k] = (uint8_t)(__builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], ls[k] & 3u) >> 8);
-    }
+    for (int q = 0; q < 3; q++) lw[k][q] = lits32[la + q];
   }
   // ---- base check of every '*' op (pafreport.cpp:550-554) and event heads, per half
   uint32_t subm[2], hm[2];
@@ -2368,14 +2330,12 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
     }
   }
   wave_sync();
-  uint32_t hl0[2] = {0u, 0u}, hl1[2] = {0u, 0u};
-  if constexpr (!kH16) {
+  uint32_t hl0[2], hl1[2];
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const uint32_t sh = ls[k] & 3u;
-      hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
-      hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
-    }
+  for (int k = 0; k < 2; k++) {
+    const uint32_t sh = ls[k] & 3u;
+    hl0[k] = __builtin_amdgcn_alignbyte(lw[k][1], lw[k][0], sh);
+    hl1[k] = __builtin_amdgcn_alignbyte(lw[k][2], lw[k][1], sh);
   }
   // ---- events (none after a mismatch: the record ends at its first one)
   const bool ok = bad_idx == INT_MAX;
@@ -2477,7 +2437,6 @@ __device__ __forceinline__ void index_pair(const pw_report_args& A, const Work& 
 }
 
 // one record of a unit that is not a pair (index_kernel's per-record step, without its prefetch)
-template <bool kH16>
 __device__ __forceinline__ void index_one(const pw_report_args& A, const Work& W, const LDS SmallTables* tab,
                                           LDS IndexWave* w, uint32_t ai, int lane, bool planned) {
   RecPre p;
@@ -2488,10 +2447,9 @@ __device__ __forceinline__ void index_one(const pw_report_args& A, const Work& W
     const uint32_t base = W.rec_blk[ai];
     if (base != kNoBlk) B = block_of(W, p.d, base, (p.d.n_ops + kBlkOps - 1) / kBlkOps, 0u, lane);
   }
-  index_record<kH16>(A, W, tab, w, ai, lane, p, B);
+  index_record(A, W, tab, w, ai, lane, p, B);
 }
 
-template <bool kH16>
 __global__ __launch_bounds__(kWave* kWaves, kPairOcc) void index_pair_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ IndexWave iw[kWaves];
@@ -2523,16 +2481,16 @@ __global__ __launch_bounds__(kWave* kWaves, kPairOcc) void index_pair_kernel(pw_
       if (n_a <= kPairOps && (!b_ok || n_b <= kPairOps)) {
         PairHead nxt;  // (the next unit's heads in flight while this pair is decoded)
         pair_head(A, nx, hl, nxt);
-        index_pair<kH16>(A, W, tp, w, ai, valid, lane, cur);
+        index_pair(A, W, tp, w, ai, valid, lane, cur);
         cur = nxt;
       } else {  // (no head prefetch across the single-record path: it holds index_record's registers)
 #pragma unroll 1
-        for (uint32_t x = 2 * u; x < 2 * u + (b_ok ? 2u : 1u); x++) index_one<kH16>(A, W, tp, w, x, lane, planned);
+        for (uint32_t x = 2 * u; x < 2 * u + (b_ok ? 2u : 1u); x++) index_one(A, W, tp, w, x, lane, planned);
         pair_head(A, nx, hl, cur);
       }
     }
   }
-  index_long_blocks<kH16>(A, W, tp, w, lane, wv, stride, planned, bid);
+  index_long_blocks(A, W, tp, w, lane, wv, stride, planned, bid);
 }
 
 // ------------------------------------------------------------------ long records: plan + carries
@@ -3272,8 +3230,7 @@ struct TcIn {
   Cold cd;           // the walk's start: record, head op, query / target position (index_kernel)
   uint32_t qi_off_lo, qi_off_hi;
   int32_t L;
-  uint32_t lq[5];          // literal dwords from lb (RecT)
-  uint32_t lb;
+  uint32_t lw0, lw1, lw2;  // literal dwords from ls & ~3 (16-byte records)
   uint32_t op_begin, n_ops;
   int32_t offset, t_len;
   v4u qv[kTcQ / 16];
@@ -3299,19 +3256,17 @@ __device__ __forceinline__ void tc_load2(const pw_report_args& A, const Work& W,
     x.qi_off_lo = (uint32_t)(qo >> 4);
     x.qi_off_hi = 0;
     x.L = A.qlen[qi];
+    const uint32_t ls = x.a.x == kNoEv ? 0u : x.a.w;
+    const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + (ls >> 2);
+    x.lw0 = l32[0];
+    x.lw1 = l32[1];
+    x.lw2 = l32[2];
   } else {
     x.qi_off_lo = x.b.x;
     x.qi_off_hi = 0;
     x.L = (int32_t)x.b.y;
+    x.lw0 = x.lw1 = x.lw2 = 0u;
   }
-  // literal bytes from 8 before the event's (dword-aligned; lits are readable PW_DEV_PAD bytes past
-  // their end): [lb, lb + 20) covers [ls - 8, ls + 9) once ls >= 8
-  const uint32_t ls = x.a.x == kNoEv ? 0u : x.a.w;
-  const uint32_t base = (ls >> 2) >= 2u ? (ls >> 2) - 2u : 0u;
-  x.lb = 4u * base;
-  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(A.lits) + base;
-#pragma unroll
-  for (int q = 0; q < 5; q++) x.lq[q] = l32[q];
 }
 __device__ __forceinline__ int tc_qp(const Work& W, const TcIn& x) {
   return W.hot_pbits ? (int32_t)hot16_qp(W, x.a.y) : (int32_t)x.a.y;
@@ -3340,7 +3295,7 @@ __device__ __forceinline__ void tc_load3(const pw_report_args& A, TcIn& x, const
 // the event's target context, walked over the staged windows, stored as its 32-byte tx record
 __device__ __forceinline__ void tc_event(const pw_report_args& A, const Work& W, const LDS SmallTables* tp,
                                          LDS TctxLane* me, const TcIn& x) {
-  RecT r;
+  Rec r;
   r.R = A.qseq + ((uint64_t)x.qi_off_lo << 4);
   r.L = x.L;
   const uint32_t fn = x.a.x;
@@ -3353,15 +3308,20 @@ __device__ __forceinline__ void tc_event(const pw_report_args& A, const Work& W,
   r.T = x.t_len;
   r.n_ops = x.n_ops;
   r.acgt = false;
-  // literal bytes [ls - 8, ls + 9) in registers (RecT); op words and forward query bytes around
-  // the event are staged in LDS
+  // the event's first 8 literal bytes are in registers; op words and forward query bytes
+  // around the event are staged in LDS
   const uint32_t ls = fn == kNoEv ? 0u : x.a.w;
-#pragma unroll
-  for (int q = 0; q < 5; q++) r.lq[q] = x.lq[q];
-  r.lb = x.lb;
-  r.lit0 = r.lit1 = 0u;
+  uint32_t l0, l1;
+  if (W.hot_pbits) {
+    lit8(ls, x.lw0, x.lw1, x.lw2, l0, l1);
+  } else {
+    l0 = x.b.z;
+    l1 = x.b.w;
+  }
+  r.lit0 = l0;
+  r.lit1 = l1;
   r.ls0 = ls;
-  r.ln = 0;
+  r.ln = 8;
   r.lw = nullptr;
   r.l_lo = 0;
   r.l_n = 0;
@@ -3709,15 +3669,13 @@ extern "C" int pw_report_events_after(const pw_report_args* args, void* stream, 
   // mostly short records (a gene panel): two per wavefront (index_pair_kernel); its grid is two
   // full rounds at the 4 waves/SIMD it runs at (sweep on cfg3 at 0.2: 8 per CU 1,421-1,436 us,
   // 4 / 12 1,427 / 1,421, 10 — index_kernel's, 2.5 rounds here — 1,474-1,481, 16 1,458)
-  if (args->n_short && (uint64_t)args->n_short * 4 >= (uint64_t)args->n_alns * 3) {
-    const dim3 pg((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 8u) + W.ns_grid);
-    if (W.hot_pbits) hipLaunchKernelGGL(pw::index_pair_kernel<true>, pg, dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-    else hipLaunchKernelGGL(pw::index_pair_kernel<false>, pg, dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-  } else if (W.hot_pbits) {
-    hipLaunchKernelGGL(pw::index_kernel<true>, dim3((uint32_t)ig + W.ns_grid), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-  } else {
-    hipLaunchKernelGGL(pw::index_kernel<false>, dim3((uint32_t)ig + W.ns_grid), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
-  }
+  if (args->n_short && (uint64_t)args->n_short * 4 >= (uint64_t)args->n_alns * 3)
+    hipLaunchKernelGGL(pw::index_pair_kernel,
+                       dim3((uint32_t)std::min<uint64_t>(((args->n_alns + 1) / 2 + nwave - 1) / nwave, (uint64_t)ncu * 8u) +
+                            W.ns_grid),
+                       dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
+  else
+    hipLaunchKernelGGL(pw::index_kernel, dim3((uint32_t)ig + W.ns_grid), dim3(pw::kWave * pw::kWaves), 0, st, *args, W);
   if (W.n_chunks) {
     uint64_t tg = (W.n_chunks * pw::kWave + 255) / 256 / pw::kWaves + 1;
     if (tg > (uint64_t)ncu * 4u) tg = (uint64_t)ncu * 4u;
