@@ -478,7 +478,8 @@ def main(argv=None) -> int:
     out_path = opts.get("o") or None
     writer = OffsetWriter(n_total, out_path, world, rank, dv, extra.get("tmpdir"))
     stream = torch.cuda.current_stream()
-    gtabs = {}
+    want_tab = "genome-table" in extra
+    gname, gacc = {}, np.zeros((1024, 3), np.uint64)  # target name -> row of the summed per-genome table
     th = None
     if cuts:
         th = threading.Thread(target=make, args=(0, None))
@@ -496,17 +497,24 @@ def main(argv=None) -> int:
         dev = pw.stage_batch(b, device)
         prof.mark("stage")
         pw.run_report(b, dev, stream.cuda_stream)
-        rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
-        launch_genome_table(dev, rows, gt, stream.cuda_stream)
+        if want_tab:  # (the per-genome tables only when asked for: --genome-table)
+            rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
+            launch_genome_table(dev, rows, gt, stream.cuda_stream)
         if prof.on:
             stream.synchronize()
             prof.mark("gpu pass")
         text_h, res_h, pages_h = pw.fetch_outputs(dev)  # (synchronises the stream)
         prof.mark("fetch")
-        r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
-        for nm, row in zip(names, r):  # per-genome rows of all batches, summed by target
-            acc = gtabs.setdefault(nm, np.zeros(3, np.uint64))
-            acc += np.array([row[0:4].view("<u4")[0], row[4:8].view("<u4")[0], row[8:16].view("<u8")[0]], np.uint64)
+        if want_tab:  # per-genome rows of all batches, summed by target (vectorised: 50k targets a batch at cfg3)
+            r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
+            gidx = np.fromiter((gname.setdefault(nm, len(gname)) for nm in names), dtype=np.int64, count=len(names))
+            if len(gname) > gacc.shape[0]:
+                gacc = np.concatenate([gacc, np.zeros((max(len(gname), 2 * gacc.shape[0]) - gacc.shape[0], 3), np.uint64)])
+            vals = np.stack([r[:, 0:4].copy().view("<u4").ravel().astype(np.uint64),
+                             r[:, 4:8].copy().view("<u4").ravel().astype(np.uint64),
+                             r[:, 8:16].copy().view("<u8").ravel()], axis=1) if len(names) else np.zeros((0, 3), np.uint64)
+            np.add.at(gacc, gidx, vals)
+            prof.mark("genome rows")
         items = b.items(text_h, res_h, pages_h)
         writer.add((b, text_h, res_h, pages_h, items))
         del dev, b
@@ -521,6 +529,7 @@ def main(argv=None) -> int:
     if th is not None and th.is_alive():
         th.join()
     made.clear()
+    gtabs = {nm: gacc[i] for nm, i in gname.items()}
     code = finish_run(writer, err, gtabs, extra, world, rank, device)
     prof.mark("finish")
     prof.report()
