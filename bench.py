@@ -379,14 +379,22 @@ def report_leg(args, config, world, rank, dev_name):
                 cpu = {"value": n_or / el, "unit": "events/s", "cores": 1, "kind": "port",
                        "sample": f"the whole benchmarked batch ({v.n_alns} records, {n_or} events, {el:.1f} s, "
                                  f"oracle/pafreport_oracle pinned to one core)"}
-            # end to end: the drop-in CLI (PAF text in, report file out) on the same input
+            # end to end: the drop-in CLI (PAF text in, report file out) on the same input, three
+            # runs after a sync (the oracle and parity legs before it leave ~0.6 GB of dirty page
+            # cache, whose writeback throttled the CLI's writes: 0.19 vs 0.49 s on one box), the
+            # median reported, every run listed
             cli_out = os.path.join(tmp, "cli.txt")
-            t0 = time.perf_counter()
-            p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", cli_out],
-                               stderr=subprocess.PIPE)
-            cli_s = time.perf_counter() - t0
-            cli_ok = p.returncode == 0 and filecmp.cmp(cli_out, want, shallow=False)
-            e2e = {"cli_wall_s": round(cli_s, 3), "events_per_s": n_or / cli_s, "parity": "ok" if cli_ok else "FAIL",
+            runs, cli_ok = [], True
+            for _ in range(3):
+                os.sync()
+                t0 = time.perf_counter()
+                p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", cli_out],
+                                   stderr=subprocess.PIPE)
+                runs.append(time.perf_counter() - t0)
+                cli_ok = cli_ok and p.returncode == 0 and filecmp.cmp(cli_out, want, shallow=False)
+            cli_s = sorted(runs)[1]
+            e2e = {"cli_wall_s": round(cli_s, 3), "cli_wall_runs_s": [round(x, 3) for x in runs],
+                   "events_per_s": n_or / cli_s, "parity": "ok" if cli_ok else "FAIL",
                    "cmd": f"pafreport {' '.join(flags_cli)} -r q.fa a.paf -o report.txt (PAF text -> report file, "
                           f"{os.path.getsize(paf)} B in, {os.path.getsize(want)} B out)",
                    "phases": cli_phases(flags_cli, fa, paf, os.path.join(tmp, "cli2.txt"))}
@@ -784,6 +792,7 @@ def cli_phases(flags_cli, fa, paf, outp):
     state), from wall-clock epochs the CLI prints; `wall_s` is this run's own wall clock."""
     import re
     env = {**os.environ, "PW_PROFILE_HOST": "1"}
+    os.sync()
     t_spawn = time.time()
     p = subprocess.run([str(REPO / "pwasm_amd/bin/pafreport"), *flags_cli, "-r", fa, paf, "-o", outp],
                        stderr=subprocess.PIPE, env=env)
