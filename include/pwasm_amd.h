@@ -466,6 +466,10 @@ int pw_batch_render_range(const pw_batch* b, const uint8_t* text_host, const pw_
                           char* err_buf, uint64_t err_cap);
 int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
                     uint64_t n);
+/* pw_batch_cuts: a rank's received lines ('\n'-ended, n bytes) cut into batches of at most target
+ * bytes (at least one line) at line ends: out[4k .. 4k + 3] = byte lo, hi, line lo, hi of batch k;
+ * returns the batch count (0 when more than cap). */
+uint64_t pw_batch_cuts(const uint8_t* text, uint64_t n, uint64_t target, uint64_t* out, uint64_t cap);
 
 /* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
  * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its

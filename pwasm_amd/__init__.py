@@ -187,6 +187,8 @@ _SIGS = {
                                                                      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
     "pw_gather_write": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint64]),
+    "pw_batch_cuts": (ctypes.c_uint64, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_uint64]),
     "pw_batch_genomes": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,

@@ -2403,10 +2403,23 @@ extern "C" int pw_items_merge(const char* const* paths, uint32_t n, const char* 
 // lines -> nobody, though they are counted: every line keeps its index in the range).
 struct pw_split {
   uint64_t n_lines = 0;
-  std::vector<std::string> bytes;               // per owner: its lines, each ended by '\n'
-  std::vector<std::vector<uint32_t>> local;     // per owner: the lines' indices in the range
+  uint32_t nshards = 1;
+  std::vector<char> data;  // the range's bytes
+  // per host thread (a sub-range cut after a '\n'): its lines (start, length, owner; owner
+  // nshards = a comment line, nobody's) and per owner its bytes / lines
+  struct Part {
+    std::vector<uint64_t> start;
+    std::vector<uint32_t> len;
+    std::vector<uint32_t> owner;
+    std::vector<uint64_t> nbytes, nlines;
+    uint64_t first = 0;  // index in the range of its first line
+  };
+  std::vector<Part> parts;
 };
 
+// Two passes: pw_paf_split reads the range (host threads) and finds every line and its owner;
+// pw_split_get copies one owner's lines straight into the caller's buffers (host threads, each at
+// its part's offset) — no per-owner strings and no merge pass.
 extern "C" pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uint32_t nshards, char* errbuf,
                                   size_t errlen) {
   auto fail = [&](const std::string& m) -> pw_split* {
@@ -2441,45 +2454,47 @@ extern "C" pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uin
   };
   const uint64_t start = line_start_at(lo), end = line_start_at(hi);
   pw_split* sp = new pw_split();
-  sp->bytes.resize(nshards);
-  sp->local.resize(nshards);
-  std::vector<char> data((size_t)(end - start) + 1);
-  for (uint64_t got = 0; got < end - start;) {
-    const ssize_t k = pread(fd, data.data() + got, (size_t)(end - start - got), (off_t)(start + got));
-    if (k <= 0) {
-      close(fd);
+  sp->nshards = nshards;
+  const size_t n = (size_t)(end - start);
+  sp->data.resize(n + 1);
+  const int nt = std::max(1, std::min<int>(host_threads(), (int)(n >> 20) + 1));
+  {  // the range, read by the host threads in slices
+    std::atomic<bool> bad{false};
+    parallel_for(nt, [&](int t) {
+      const size_t a = n * (size_t)t / (size_t)nt, z = n * (size_t)(t + 1) / (size_t)nt;
+      for (size_t got = a; got < z;) {
+        const ssize_t k = pread(fd, sp->data.data() + got, z - got, (off_t)(start + got));
+        if (k <= 0) {
+          bad = true;
+          return;
+        }
+        got += (size_t)k;
+      }
+    });
+    close(fd);
+    if (bad) {
       delete sp;
       return fail(strf("cannot read %s", paf));
     }
-    got += (uint64_t)k;
   }
-  close(fd);
-  const size_t n = (size_t)(end - start);
   // threads take sub-ranges cut after a '\n' (line splitting is local to such a cut)
-  const int nt = std::max(1, std::min<int>(host_threads(), (int)(n >> 20) + 1));
   std::vector<size_t> cut((size_t)nt + 1, n);
   cut[0] = 0;
+  const char* s = sp->data.data();
   for (int t = 1; t < nt; t++) {
     size_t x = n * (size_t)t / (size_t)nt;
     if (x < cut[(size_t)t - 1]) x = cut[(size_t)t - 1];
-    const char* q = x < n ? (const char*)memchr(data.data() + x, '\n', n - x) : nullptr;
-    cut[(size_t)t] = q ? (size_t)(q - data.data()) + 1 : n;
+    const char* q = x < n ? (const char*)memchr(s + x, '\n', n - x) : nullptr;
+    cut[(size_t)t] = q ? (size_t)(q - s) + 1 : n;
   }
-  struct Part {
-    std::vector<std::string> bytes;
-    std::vector<std::vector<uint32_t>> local;
-    uint64_t lines = 0;
-  };
-  std::vector<Part> parts((size_t)nt);
+  sp->parts.resize((size_t)nt);
   parallel_for(nt, [&](int t) {
-    Part& pt = parts[(size_t)t];
-    pt.bytes.resize(nshards);
-    pt.local.resize(nshards);
-    const char* s = data.data();
+    pw_split::Part& pt = sp->parts[(size_t)t];
+    pt.nbytes.assign(nshards, 0);
+    pt.nlines.assign(nshards, 0);
     const size_t a = cut[(size_t)t], b = cut[(size_t)t + 1];
     const bool has_cr = memchr(s + a, '\r', b - a) != nullptr;
     size_t p = a;
-    std::vector<std::pair<size_t, size_t>> ls;  // this sub-range's lines
     while (p < b) {
       size_t e;
       if (!has_cr) {
@@ -2490,18 +2505,12 @@ extern "C" pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uin
         while (e < b && s[e] != '\n' && s[e] != '\r') e++;
       }
       if (e == b && e == p) break;
-      ls.push_back({p, e});
-      size_t nx = e + 1;
-      if (e < b && s[e] == '\r' && e + 1 < b && s[e + 1] == '\n') nx = e + 2;
-      p = nx;
-    }
-    pt.lines = ls.size();
-    for (size_t i = 0; i < ls.size(); i++) {
-      const char* l = s + ls[i].first;
-      const size_t ln = ls[i].second - ls[i].first;
-      if (ln > 0 && l[0] == '#') continue;
+      const char* l = s + p;
+      const size_t ln = e - p;
       uint32_t owner = 0;
-      if (nshards > 1) {
+      if (ln > 0 && l[0] == '#') {
+        owner = nshards;  // (a comment line: counted, nobody's)
+      } else if (nshards > 1) {
         const char* t5 = nullptr;
         size_t t5n = 0;
         int tabs = 0;
@@ -2516,34 +2525,61 @@ extern "C" pw_split* pw_paf_split(const char* paf, uint64_t lo, uint64_t hi, uin
           }
         owner = tabs >= 6 ? crc32_ieee(t5, t5n) % nshards : 0u;
       }
-      pt.bytes[owner].append(l, ln);
-      pt.bytes[owner].push_back('\n');
-      pt.local[owner].push_back((uint32_t)i);  // (rebased below)
+      pt.start.push_back(p);
+      pt.len.push_back((uint32_t)ln);
+      pt.owner.push_back(owner);
+      if (owner < nshards) {
+        pt.nbytes[owner] += ln + 1;
+        pt.nlines[owner]++;
+      }
+      size_t nx = e + 1;
+      if (e < b && s[e] == '\r' && e + 1 < b && s[e + 1] == '\n') nx = e + 2;
+      p = nx;
     }
   });
   uint64_t base = 0;
-  for (auto& pt : parts) {
-    for (uint32_t o = 0; o < nshards; o++) {
-      sp->bytes[o] += pt.bytes[o];
-      for (uint32_t x : pt.local[o]) sp->local[o].push_back((uint32_t)(base + x));
-    }
-    base += pt.lines;
+  for (auto& pt : sp->parts) {
+    pt.first = base;
+    base += pt.start.size();
   }
   sp->n_lines = base;
   return sp;
 }
 extern "C" uint64_t pw_split_lines(const pw_split* sp) { return sp ? sp->n_lines : 0; }
 extern "C" uint64_t pw_split_bytes(const pw_split* sp, uint32_t owner) {
-  return sp && owner < sp->bytes.size() ? sp->bytes[owner].size() : 0;
+  uint64_t v = 0;
+  if (sp && owner < sp->nshards)
+    for (const auto& pt : sp->parts) v += pt.nbytes[owner];
+  return v;
 }
 extern "C" uint64_t pw_split_count(const pw_split* sp, uint32_t owner) {
-  return sp && owner < sp->local.size() ? sp->local[owner].size() : 0;
+  uint64_t v = 0;
+  if (sp && owner < sp->nshards)
+    for (const auto& pt : sp->parts) v += pt.nlines[owner];
+  return v;
 }
 extern "C" int pw_split_get(const pw_split* sp, uint32_t owner, char* bytes, uint32_t* local_lines) {
-  if (!sp || owner >= sp->bytes.size()) return PW_E_ARG;
-  if (bytes && !sp->bytes[owner].empty()) memcpy(bytes, sp->bytes[owner].data(), sp->bytes[owner].size());
-  if (local_lines && !sp->local[owner].empty())
-    memcpy(local_lines, sp->local[owner].data(), sp->local[owner].size() * 4);
+  if (!sp || owner >= sp->nshards) return PW_E_ARG;
+  const size_t np = sp->parts.size();
+  std::vector<uint64_t> bo(np + 1, 0), lo(np + 1, 0);  // each part's offsets in the outputs
+  for (size_t t = 0; t < np; t++) {
+    bo[t + 1] = bo[t] + sp->parts[t].nbytes[owner];
+    lo[t + 1] = lo[t] + sp->parts[t].nlines[owner];
+  }
+  parallel_for((int)np, [&](int t) {
+    const pw_split::Part& pt = sp->parts[(size_t)t];
+    uint64_t b = bo[(size_t)t], k = lo[(size_t)t];
+    for (size_t i = 0; i < pt.start.size(); i++) {
+      if (pt.owner[i] != owner) continue;
+      if (bytes) {
+        memcpy(bytes + b, sp->data.data() + pt.start[i], pt.len[i]);
+        bytes[b + pt.len[i]] = '\n';
+      }
+      b += (uint64_t)pt.len[i] + 1;
+      if (local_lines) local_lines[k] = (uint32_t)(pt.first + i);
+      k++;
+    }
+  });
   return PW_OK;
 }
 extern "C" void pw_split_free(pw_split* sp) { delete sp; }
@@ -2894,6 +2930,54 @@ extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, co
     for (auto& x : th) x.join();
   }
   return rc.load();
+}
+
+// Cuts of a rank's received lines ('\n'-ended, n bytes) into batches of at most `target` bytes (at
+// least one line) ending at line ends: out[4k .. 4k + 3] = byte lo, hi, line lo, hi of batch k;
+// returns the number of batches (cap: the entries out holds; more -> 0).  The lines of each batch
+// are counted by host threads (memchr).
+extern "C" uint64_t pw_batch_cuts(const uint8_t* text, uint64_t n, uint64_t target, uint64_t* out, uint64_t cap) {
+  if (!out || (n && !text)) return 0;
+  if (target == 0) target = 1;
+  std::vector<uint64_t> b;  // batch ends
+  for (uint64_t b0 = 0; b0 < n;) {
+    uint64_t b1;
+    if (b0 + target > n) {
+      b1 = n;
+    } else {  // the last '\n' in [b0, b0 + target - 1), else the end of the first line
+      const void* q = target > 1 ? memrchr(text + b0, '\n', (size_t)(target - 1)) : nullptr;
+      if (q) {
+        b1 = (uint64_t)((const uint8_t*)q - text) + 1;
+      } else {
+        const void* f = memchr(text + b0, '\n', (size_t)(n - b0));
+        b1 = f ? (uint64_t)((const uint8_t*)f - text) + 1 : n;
+      }
+    }
+    b.push_back(b1);
+    b0 = b1;
+  }
+  if (b.size() > cap) return 0;
+  std::vector<uint64_t> lines(b.size(), 0);
+  parallel_for((int)b.size(), [&](int k) {
+    const uint64_t lo = k ? b[(size_t)k - 1] : 0, hi = b[(size_t)k];
+    uint64_t c = 0;
+    for (const uint8_t* p = text + lo; p < text + hi;) {
+      const void* f = memchr(p, '\n', (size_t)(text + hi - p));
+      if (!f) break;
+      c++;
+      p = (const uint8_t*)f + 1;
+    }
+    lines[(size_t)k] = c;
+  });
+  uint64_t l0 = 0;
+  for (size_t k = 0; k < b.size(); k++) {
+    out[4 * k] = k ? b[k - 1] : 0;
+    out[4 * k + 1] = b[k];
+    out[4 * k + 2] = l0;
+    l0 += lines[k];
+    out[4 * k + 3] = l0;
+  }
+  return b.size();
 }
 
 extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,

@@ -177,19 +177,23 @@ def exchange(paf, world, rank, device, backend):
 
 
 def batch_cuts(text, line_no, target):
-    """Sub-batches of about `target` bytes ending at line ends -> [(byte lo, hi, line lo, hi)]."""
-    n = text.size
+    """Sub-batches of at most `target` bytes (at least one line) ending at line ends -> [(byte lo,
+    hi, line lo, hi)] (pw_batch_cuts: memchr scans, lines counted by host threads; numpy's
+    flatnonzero over the whole text took 0.8 s at cfg3)."""
+    import pwasm_amd as pw
+    text = np.ascontiguousarray(text)
+    if text.dtype != np.uint8:
+        raise TypeError("batch_cuts: text must be uint8")
+    n = int(text.size)
     if n == 0:
         return []
-    ends = np.flatnonzero(text == 10) + 1  # one past each line's '\\n'
-    cuts, b0, l0 = [], 0, 0
-    while b0 < n:
-        k = int(np.searchsorted(ends, b0 + target, side="left"))
-        k = min(max(k, l0 + 1), ends.size) - 1  # last line of this batch
-        b1 = int(ends[k])
-        cuts.append((b0, b1, l0, k + 1))
-        b0, l0 = b1, k + 1
-    return cuts
+    cap = n // max(int(target), 1) + 2
+    while True:
+        out = np.zeros(4 * cap, dtype=np.uint64)
+        k = int(pw.lib().pw_batch_cuts(text.ctypes.data, n, max(int(target), 1), out.ctypes.data, cap))
+        if k:
+            return [tuple(int(x) for x in out[4 * i:4 * i + 4]) for i in range(k)]
+        cap *= 4  # (lines longer than target: more batches than n / target)
 
 
 class OffsetWriter:
