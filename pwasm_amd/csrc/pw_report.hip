@@ -3359,7 +3359,7 @@ __device__ __forceinline__ void tc_event(const pw_report_args& A, const Work& W,
   dtx[0] = t0;
   dtx[1] = t1;
 }
-__global__ __launch_bounds__(kWave* kWaves, 4) void tctx_kernel(pw_report_args A, Work W) {
+__global__ __launch_bounds__(kWave* kWaves) void tctx_kernel(pw_report_args A, Work W) {
   __shared__ SmallTables tab;
   __shared__ __attribute__((aligned(16))) TctxWave tw[kWaves];
   LDS SmallTables* tp = (LDS SmallTables*)&tab;
@@ -3371,93 +3371,81 @@ __global__ __launch_bounds__(kWave* kWaves, 4) void tctx_kernel(pw_report_args A
   const uint64_t n_groups = (W.n_chunks * kWave + 255) / 256;
   const uint32_t* f32 = reinterpret_cast<const uint32_t*>(W.sflag);
   const uint64_t nf32 = W.n_chunks * kWave / 4;
+  // the next group's flag words load one group ahead (clamped index, masked when consumed)
   const uint64_t gstride = (uint64_t)gridDim.x * kWaves;
-  // flagged slots queue up in the wave's list across its groups and are processed up to 192 at a
-  // time (every lane has an event except in the wave's last batch): the walk runs once per 64
-  // events, not once per group (~40 flagged slots per 256 at cfg2)
+  uint64_t gi = (uint64_t)blockIdx.x * kWaves + wv;
+  const uint64_t flast = nf32 ? nf32 - 1 : 0;
+  uint32_t fnext = nf32 ? f32[gi * kWave + lane < nf32 ? gi * kWave + lane : flast] : 0u;
+  // flagged slots queue up in the wave's list across its groups and are processed 64 at a time
+  // (every lane has an event except in the wave's last batch): the walk runs once per 64 events,
+  // not once per group (~40 flagged slots per 256 at cfg2)
   uint32_t nl = 0;  // entries in the list (wave-uniform)
-  // A batch takes up to 192 entries: lane l the events of entries l, 64 + l and 128 + l.  Their
-  // loads are pipelined across the walks (round 6): the first two events' records load together,
-  // level by level (Hot / Cold, then the query table / descriptor / literal words), the third
-  // event's first level behind them and its second level during the first walk; each event's
-  // windows (third level) load after the walk before it — so a wave's 192 events cost three walks
-  // and five load levels, where batches of 128 took two chains of three levels for 129-256 events.
+  // A batch takes up to 128 entries: lane l the events of entries l and 64 + l.  Both events'
+  // records load together, level by level (Hot / Cold, then the query table / descriptor /
+  // literal words); the second event's wait in registers while the first one is walked, so a
+  // wave's second 64 events cost one level of loads (their windows) and a walk, not a whole chain.
   auto batch = [&](uint32_t nb) {
-    const bool has1 = (uint32_t)lane < nb, has2 = (uint32_t)lane + kWave < nb, has3 = (uint32_t)lane + 2 * kWave < nb;
+    const bool has1 = (uint32_t)lane < nb, has2 = (uint32_t)lane + kWave < nb;
     // (unconditional loads: a lane without an entry reads entry 0's records)
-    const uint64_t s1 = w->list[has1 ? lane : 0], s2 = w->list[has2 ? kWave + lane : 0],
-                   s3 = w->list[has3 ? 2 * kWave + lane : 0];
-    TcIn x1, x2, x3;
+    const uint64_t s1 = w->list[has1 ? lane : 0], s2 = w->list[has2 ? kWave + lane : 0];
+    TcIn x1, x2;
     tc_load1(W, s1, x1);
     tc_load1(W, s2, x2);
     tc_load2(A, W, x1);
     tc_load2(A, W, x2);
-    tc_load1(W, s3, x3);
     tc_load3(A, x1, W);
     if (has1) tc_event(A, W, tp, me, x1);
+    // (the second event's windows load after the first walk: held across it, they pushed the
+    // kernel past 128 VGPRs)
     if (nb > (uint32_t)kWave) {  // (uniform)
-      tc_load2(A, W, x3);
       tc_load3(A, x2, W);
       if (has2) tc_event(A, W, tp, me, x2);
-      if (nb > 2u * kWave) {  // (uniform)
-        tc_load3(A, x3, W);
-        if (has3) tc_event(A, W, tp, me, x3);
-      }
     }
   };
-  // the entries after the first nb move to the front of the list
-  auto take = [&](uint32_t nb) {
-    batch(nb);
-    const uint32_t rest = nl - nb;
-    uint32_t mv[3];
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const uint32_t i = (uint32_t)(lane + kWave * k);
-      mv[k] = i < rest ? w->list[nb + i] : 0u;
-    }
-    wave_sync();
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const uint32_t i = (uint32_t)(lane + kWave * k);
-      if (i < rest) w->list[i] = mv[k];
-    }
-    nl = rest;
-    wave_sync();
-  };
-  constexpr uint32_t kTcBatch = 3 * kWave;
-  // the wave's groups in rounds of kTcRound, every flag word of a round loaded at once (round 6:
-  // a cfg2 wave has <= 5 groups, which were one dependent load each)
-  constexpr int kTcRound = 4;
-  const uint64_t flast = nf32 ? nf32 - 1 : 0;
-  for (uint64_t g0 = (uint64_t)blockIdx.x * kWaves + wv; g0 < n_groups; g0 += (uint64_t)kTcRound * gstride) {
-    uint32_t fw[kTcRound];
-#pragma unroll
-    for (int q = 0; q < kTcRound; q++) {
-      const uint64_t fi = (g0 + (uint64_t)q * gstride) * kWave + lane;
-      fw[q] = nf32 ? f32[fi < nf32 ? fi : flast] : 0u;
-      fw[q] = fi < nf32 ? fw[q] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < kTcRound; q++) {
-      const uint64_t gi = g0 + (uint64_t)q * gstride;
-      if (gi >= n_groups) break;
-      const uint32_t f4 = fw[q] & 0x01010101u;
-      const uint32_t cnt = (uint32_t)__popc(f4);
-      const uint32_t incl = wave_incl_scan(cnt, lane);
-      const uint32_t total = wave_last(incl);
-      if (total == 0) continue;
-      while (nl + total > 5u * kWave) take(nl < kTcBatch ? nl : kTcBatch);  // (only groups of > 128 flagged slots)
-      uint32_t o = nl + incl - cnt;
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if ((f4 >> (8 * k)) & 1u) w->list[o++] = (uint32_t)(gi * 256 + (uint64_t)(4 * lane + k));
-      nl += total;
+  for (; gi < n_groups; gi += gstride) {
+    const uint64_t fi = gi * kWave + lane;
+    uint32_t fcur = fnext;
+    asm volatile("" : "+v"(fcur));
+    const uint64_t fin = fi + gstride * kWave;
+    fnext = nf32 ? f32[fin < nf32 ? fin : flast] : 0u;
+    const uint32_t f4 = (fi < nf32 ? fcur : 0u) & 0x01010101u;
+    const uint32_t cnt = (uint32_t)__popc(f4);
+    const uint32_t incl = wave_incl_scan(cnt, lane);
+    const uint32_t total = wave_last(incl);
+    if (total == 0) continue;
+    if (nl + total > 5u * kWave) {  // (uniform; only groups of > 192 flagged slots)
+      batch(nl);
+      nl = 0;
       wave_sync();
-      while (nl >= kTcBatch) take(kTcBatch);
+    }
+    uint32_t o = nl + incl - cnt;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if ((f4 >> (8 * q)) & 1u) w->list[o++] = (uint32_t)(gi * 256 + (uint64_t)(4 * lane + q));
+    nl += total;
+    wave_sync();
+    while (nl >= (uint32_t)(2 * kWave)) {
+      batch((uint32_t)(2 * kWave));
+      // the entries after the batch move to the front (<= 4 per lane)
+      const uint32_t rest = nl - (uint32_t)(2 * kWave);
+      uint32_t mv[4];
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = (uint32_t)(lane + kWave * k);
+        mv[k] = i < rest ? w->list[2 * kWave + i] : 0u;
+      }
+      wave_sync();
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = (uint32_t)(lane + kWave * k);
+        if (i < rest) w->list[i] = mv[k];
+      }
+      nl = rest;
+      wave_sync();
     }
   }
-  while (nl) take(nl < kTcBatch ? nl : kTcBatch);
+  if (nl) batch(nl);
 }
 
 // ------------------------------------------------------------------ fixup_kernel

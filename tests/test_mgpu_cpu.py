@@ -245,3 +245,76 @@ def test_input_error_on_one_rank_ends_every_rank(tmp_path, world, fail_rank):
                     if not ln.startswith(noise))
     assert err0 == (b"Error: invalid FASTA file q.fa !\n" if fail_rank is not None else b"")
     assert gt.exists() == (fail_rank is None)
+
+
+# ---------------------------------------------------------------- host helpers of the write paths (round 6)
+def _old_batch_cuts(text, target):
+    """The pre-round-6 numpy form of mgpu.batch_cuts (every line end indexed)."""
+    n = text.size
+    ends = np.flatnonzero(text == 10) + 1
+    cuts, b0, l0 = [], 0, 0
+    while b0 < n:
+        k = int(np.searchsorted(ends, b0 + target, side="left"))
+        k = min(max(k, l0 + 1), ends.size) - 1
+        b1 = int(ends[k])
+        cuts.append((b0, b1, l0, k + 1))
+        b0, l0 = b1, k + 1
+    return cuts
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_batch_cuts_c_matches_numpy(built, seed):
+    """pw_batch_cuts (memchr scans, threaded line counts) cuts exactly where the numpy form did:
+    batches of at most `target` bytes, at least one line, at line ends."""
+    rng = np.random.default_rng(seed)
+    for _ in range(200):
+        lens = rng.integers(1, 60, int(rng.integers(1, 80)))
+        text = np.concatenate([np.append(np.full(int(x), 65, np.uint8), np.uint8(10)) for x in lens]).astype(np.uint8)
+        for t in (1, 2, 3, 7, 30, 100, 10 ** 6):
+            assert mgpu.batch_cuts(text, None, t) == _old_batch_cuts(text, t)
+    assert mgpu.batch_cuts(np.zeros(0, np.uint8), None, 10) == []
+
+
+def test_gather_write_spans(built, tmp_path):
+    """pw_gather_write: spans of a source in order, written contiguously at an offset (threads,
+    8 MB blocks: a 20 MB case crosses blocks and threads)."""
+    rng = np.random.default_rng(4)
+    src = rng.integers(0, 256, 24 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 5000, 8000).astype(np.uint64)
+    offs = rng.integers(0, src.size - 5000, lens.size).astype(np.uint64)
+    want = b"".join(src[int(o):int(o) + int(n)].tobytes() for o, n in zip(offs, lens))
+    p = tmp_path / "g.bin"
+    p.write_bytes(b"x" * 100)
+    fd = os.open(p, os.O_WRONLY)
+    try:
+        pw.gather_write(fd, 37, src, offs, lens)
+    finally:
+        os.close(fd)
+    got = p.read_bytes()
+    assert got[:37] == b"x" * 37 and got[37:37 + len(want)] == want
+
+
+def test_render_range_equals_write_range(built, tmp_path):
+    """pw_batch_render_range's bytes back to back are what pw_batch_write_range pwrites at the items'
+    offsets (plain items, messages, dedupe warnings; zero results: header-only records)."""
+    from test_shard import _with_duplicates_and_comments
+    from conftest import synth_paf
+    fa, paf = synth_paf(tmp_path, 0, seed=43)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 2)
+    b = pw.HostBatch(fa, dup, 0)
+    n = int(b.view.n_alns)
+    res = np.zeros(max(n, 1) * 48, np.uint8)
+    z = np.zeros(16, np.uint8)
+    ln, st, on, en = b.items(z, res, z)
+    k = len(ln)
+    out, eb = b.render_range(z, res, z, 0, int(on.sum()), k, int(en.sum()))
+    offs = np.concatenate([[0], np.cumsum(on.astype(np.int64))[:-1]]).astype(np.uint64)
+    p = tmp_path / "w.bin"
+    p.write_bytes(b"")
+    fd = os.open(p, os.O_WRONLY)
+    try:
+        eb2 = b.write_range(z, res, z, fd, 0, offs, int(en.sum()))
+    finally:
+        os.close(fd)
+    assert bytes(out) == p.read_bytes() and eb == eb2
+    assert k > 10 and int(en.sum()) > 0
