@@ -492,7 +492,6 @@ struct TileLds {
   uint32_t tab[6 * kCntW];                 // [field][swizzled column]
   uint32_t win[kCntWaves][kWin / 4];       // per-wave base windows
   uint32_t bmap[kCntWaves][64];            // per-wave gap-column bitmaps
-  v2u bpx[kCntWaves][64];                  // per-wave (bitmap dword, gap columns before it)
   uint32_t sel[16];                        // v_perm selectors: 4-bit gap mask -> byte picks
 };
 // LDS slot of column c: rotated within its 32 columns by its 32-column block index, so the adds
@@ -634,9 +633,7 @@ __device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
 __device__ __forceinline__ void cnt_flush(uint32_t (&acc)[32], LDS uint32_t* tab, int lane) {
 #pragma unroll
   for (int m = 0; m < 32; m++) {
-    // (acc[m] = column 256 (m / 4) + 4 lane + m % 4: lane l owns the column quads 64 q + l; for one m
-    // the 32 lanes of an access group then hit 32 distinct banks through cnt_swz)
-    const int x = cnt_swz(256 * (m >> 2) + 4 * lane + (m & 3));
+    const int x = cnt_swz(32 * lane + m);  // (acc[m] = column 32 lane + m)
 #pragma unroll
     for (int f = 0; f < 6; f++) {
       atomicAdd((uint32_t*)&tab[f * kCntW + x], (acc[m] >> (5 * f)) & 31u);
@@ -815,40 +812,36 @@ __global__ __launch_bounds__(64 * kCntWaves, 4) void tile_counts(const pw_msa_ar
           if (lane < 8) w4[128 + lane] = w2;
         }
         wave_sync();
-        {  // (bitmap dword, gap columns before it) per dword: lane l's quads read them below
-          const uint32_t bmv = bm[lane];
-          const int pc = __popc(bmv);
-          lp->bpx[wv][lane] = (v2u){bmv, (uint32_t)(wave_scan_incl(pc) - pc)};
-        }
-        wave_sync();
-        // Lane l owns the column quads Q = 64 q + l (round 6; the columns 4Q .. 4Q + 3): for one q
-        // the 64 lanes read consecutive window dwords, where lanes owning 32 consecutive columns each
-        // read 8 dwords apart — an 8-way LDS bank conflict on every window read.  Quad Q lies in
-        // bitmap dword 8 q + l / 8 at bit 4 (l % 8); its source byte in the window is
-        // base + 4Q - (gap columns before 4Q).
-        const int sh = 4 * (lane & 7);
-        const uint32_t lowm = (1u << sh) - 1u;
-        const int so = (int)((uint32_t)(roff + (uint64_t)ib) & 15u) + 4 * lane;  // (+ 256 q)
+        const uint32_t bmv = bm[lane];
+        const int pc = __popc(bmv);
+        const int excl = wave_scan_incl(pc) - pc;
+        // byte offset in the window of the base in this lane's first clear column
+        const int so = (int)((uint32_t)(roff + (uint64_t)ib) & 15u) + 32 * lane - excl;
         const LDS uint8_t* wb = reinterpret_cast<const LDS uint8_t*>(win);
-        const LDS v2u* bq = lp->bpx[wv] + (lane >> 3);
+        // step q: this lane's column group q (columns 32 lane + 4q ..), its source offset so + 4q -
+        // popc(bitmap bits below 4q).  (Rounds 3-4 rotated each lane's group order so that the 32
+        // lanes of an LDS access group read 32 distinct banks when the row has no gaps; the
+        // rotation's offset and wrap arithmetic cost more than the conflicts it removed: round 5,
+        // tools/exp_msa_variants.py norot, tile_counts 90.5 -> 87.1 us.)
         uint32_t codes[8];
         auto groups = [&](auto edge_c, auto fast_c) {
           constexpr bool kEdge = decltype(edge_c)::value, kFast = decltype(fast_c)::value;
-          uint32_t bad = 0;
+          uint32_t rom = 0, bad = 0;
+          if constexpr (kEdge) {
+            const uint32_t om = outside_mask(lane, a - c0, z - c0 + 1);
+            rom = om;
+          }
 #pragma unroll
           for (int q = 0; q < 8; q++) {
-            const v2u bp = bq[8 * q];
-            const uint32_t nb = (bp.x >> sh) & 15u;
-            const int src = so + 256 * q - (int)(bp.y + (uint32_t)__popc(bp.x & lowm));
+            const uint32_t nb = (bmv >> (4 * q)) & 15u;
+            const int src = so + 4 * q - (q == 0 ? 0 : __popc(bmv & ((1u << (4 * q)) - 1u)));
             const LDS uint32_t* p = reinterpret_cast<const LDS uint32_t*>(wb + (src & ~3));
             const uint32_t s4 = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)src & 3u);
             const uint32_t e4 = __builtin_amdgcn_perm(0x2D2D2D2Du, s4, lp->sel[nb]);
             uint32_t d = 0;
             uint32_t cq = kFast ? bin_codes_fast(e4, d) : bin_codes5(e4);
             if constexpr (kEdge) {  // (columns outside the extent: code none, never "bad")
-              const int x0 = 256 * q + 4 * lane;  // tile column of the quad's first column
-              const int lo4 = min(max(a - c0 - x0, 0), 4), hi4 = min(max(z - c0 + 1 - x0, 0), 4);
-              const uint32_t on = (((1u << lo4) - 1u) | ~((1u << hi4) - 1u)) & 15u;
+              const uint32_t on = (rom >> (4 * q)) & 15u;
               const uint32_t b1 = (on * 0x00204081u) & 0x01010101u;  // 4 bits -> 4 bytes
               const uint32_t bmask = (b1 << 8) - b1;
               cq = (cq & ~bmask) | (bmask & (kCodeNone * 0x01010101u));
