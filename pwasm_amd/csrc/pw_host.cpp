@@ -21,6 +21,8 @@
 #include <atomic>
 #include <chrono>
 #include <future>
+#include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <string_view>
@@ -2742,6 +2744,58 @@ extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, cons
 // err_buf.  Items whose destinations follow each other are assembled into one buffer and written
 // by one pwrite (up to 8 MB), by up to host_threads() threads over contiguous item ranges (a
 // per-item pwrite was the multi-GPU driver's largest host cost: 5.2 s for 3 M records).
+// A file range assembled in images (64 MB) and written with one pwrite per image from a
+// writer thread while host threads fill the next image: writers of one file serialise on its inode
+// lock, so one large pwrite reaches the file system's rate and many concurrent smaller ones do not
+// (the CLI's emit path does the same).  The two images are kept per calling thread
+// across calls (no page faults on every window).
+struct ImageWriter {
+  static uint64_t img_bytes() {  // 64 MB (PW_EMIT_IMG_BYTES: tests)
+    const char* e = getenv("PW_EMIT_IMG_BYTES");
+    return e ? std::max<uint64_t>(1, strtoull(e, nullptr, 10)) : (64ull << 20);
+  }
+  int fd;
+  int ik = 0;
+  std::thread wr;
+  std::atomic<int> rc{PW_OK};
+  explicit ImageWriter(int f) : fd(f) {}
+  ~ImageWriter() { join(); }
+  void join() {
+    if (wr.joinable()) wr.join();
+  }
+  uint8_t* next(uint64_t n) {  // the image to fill (n bytes)
+    static thread_local std::unique_ptr<uint8_t[]> pool[2];
+    static thread_local uint64_t pcap[2] = {0, 0};
+    if (pcap[ik] < n) {
+      pool[ik].reset();
+      pcap[ik] = 0;
+      pool[ik].reset(new (std::nothrow) uint8_t[n]);
+      if (!pool[ik]) return nullptr;
+      pcap[ik] = n;
+    }
+    return pool[ik].get();
+  }
+  void submit(const uint8_t* p, uint64_t n, uint64_t off) {  // write the filled image at off
+    join();
+    if (rc.load() != PW_OK) return;
+    wr = std::thread([this, p, n, off]() {
+      for (uint64_t done = 0; done < n;) {
+        const ssize_t w = pwrite(fd, p + done, (size_t)(n - done), (off_t)(off + done));
+        if (w <= 0) {
+          rc = PW_E_IO;
+          return;
+        }
+        done += (uint64_t)w;
+      }
+    });
+    ik ^= 1;
+  }
+  int finish() {
+    join();
+    return rc.load();
+  }
+};
+
 extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
                                     const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off,
                                     uint64_t n_items, char* err_buf, uint64_t err_cap) {
@@ -2749,7 +2803,7 @@ extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host
     return PW_E_ARG;
   const Batch& b = bt->b;
   // stderr offsets (a sequential pass: plain items only have soft-clip warnings)
-  std::vector<uint64_t> eoff((size_t)n_items + 1, 0);
+  std::vector<uint64_t> eoff((size_t)n_items + 1, 0), osz((size_t)n_items);
   std::vector<uint8_t> plain((size_t)n_items);
   for (uint64_t j = 0; j < n_items; j++) {
     const LogItem& it = b.log[(size_t)(first + j)];
@@ -2758,9 +2812,43 @@ extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host
     if (plain[j]) plain_sizes(b, it, res_host, pages_host, on, en);
     else if (item_slow(b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en) == INT_MIN)
       return PW_E_NOMEM;
+    osz[j] = on;
     eoff[j + 1] = eoff[j] + en;
   }
   if (err_buf && eoff[n_items] > err_cap) return PW_E_ARG;
+  // runs of items whose destinations follow each other, cut at the image size
+  struct Seg {
+    uint64_t j0, j1, d0, n;
+  };
+  std::vector<Seg> segs;
+  const uint64_t kImg = ImageWriter::img_bytes();
+  uint64_t runs = 0;  // contiguity breaks + 1
+  for (uint64_t j = 0; j < n_items; j++) {
+    const bool brk = segs.empty() || out_off[j] != segs.back().d0 + segs.back().n;
+    runs += brk;
+    if (brk || (segs.back().n && segs.back().n + osz[j] > kImg)) segs.push_back({j, j, out_off[j], 0});
+    segs.back().j1 = j + 1;
+    segs.back().n += osz[j];
+  }
+  if (runs && runs * 64 <= n_items) {  // long runs (one rank's window): images
+    ImageWriter iw(fd);
+    for (const Seg& sg : segs) {
+      uint8_t* img = iw.next(sg.n);
+      if (!img) {
+        iw.finish();
+        return PW_E_NOMEM;
+      }
+      const int r = pw_batch_render_range(bt, text_host, res_host, pages_host, first + sg.j0, sg.j1 - sg.j0, img, sg.n,
+                                          err_buf ? err_buf + eoff[sg.j0] : nullptr,
+                                          err_buf ? eoff[sg.j1] - eoff[sg.j0] : 0);
+      if (r != PW_OK) {
+        iw.finish();
+        return r;
+      }
+      iw.submit(img, sg.n, sg.d0);
+    }
+    return iw.finish();
+  }
   constexpr uint64_t kBuf = 8ull << 20;
   std::atomic<int> rc{PW_OK};
   auto work = [&](uint64_t j0, uint64_t j1) {
@@ -2882,7 +2970,7 @@ extern "C" int pw_batch_render_range(const pw_batch* bt, const uint8_t* text_hos
       }
     }
   };
-  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), n_items / 4096));
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), n_items / 256));
   if (T <= 1) {
     work(0, n_items);
   } else {
@@ -2894,7 +2982,8 @@ extern "C" int pw_batch_render_range(const pw_batch* bt, const uint8_t* text_hos
 }
 
 // Spans src[src_off[k], + len[k]) for k = 0..n-1, in order, written contiguously to fd from
-// file_off: host threads assemble consecutive parts of the range and pwrite each in 8 MB blocks.
+// file_off: host threads assemble 64 MB images of the range, a writer thread pwrites each in one
+// call while the next is assembled (ImageWriter).
 extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, const uint64_t* src_off, const uint64_t* len,
                                uint64_t n) {
   if (n && (!src || !src_off || !len)) return PW_E_ARG;
@@ -2902,41 +2991,36 @@ extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, co
   for (uint64_t k = 0; k < n; k++) dst[k + 1] = dst[k] + len[k];
   const uint64_t total = dst[n];
   if (total == 0) return PW_OK;
-  constexpr uint64_t kBlk = 8ull << 20;
-  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), total / kBlk));
-  std::atomic<int> rc{PW_OK};
-  auto work = [&](int t) {
-    const uint64_t a = total * (uint64_t)t / (uint64_t)T, z = total * (uint64_t)(t + 1) / (uint64_t)T;
-    std::vector<uint8_t> buf((size_t)std::min<uint64_t>(kBlk, z - a));
-    uint64_t k = (uint64_t)(std::upper_bound(dst.begin(), dst.end(), a) - dst.begin()) - 1;  // span holding byte a
-    for (uint64_t x = a; x < z && rc.load() == PW_OK;) {
-      const uint64_t bn = std::min<uint64_t>(kBlk, z - x);
-      uint64_t f = 0;
-      while (f < bn) {  // fill the block from the spans
+  ImageWriter iw(fd);
+  const uint64_t kImg = ImageWriter::img_bytes();
+  for (uint64_t x = 0; x < total;) {  // one image per kImg bytes of the range
+    const uint64_t bn = std::min<uint64_t>(kImg, total - x);
+    uint8_t* img = iw.next(bn);
+    if (!img) {
+      iw.finish();
+      return PW_E_NOMEM;
+    }
+    auto fill = [&](uint64_t a, uint64_t z) {  // image bytes [a, z) from the spans
+      uint64_t k = (uint64_t)(std::upper_bound(dst.begin(), dst.end(), x + a) - dst.begin()) - 1;
+      for (uint64_t f = a; f < z;) {
         while (dst[k + 1] <= x + f) k++;
-        const uint64_t in = x + f - dst[k], c = std::min<uint64_t>(len[k] - in, bn - f);
-        memcpy(buf.data() + f, src + src_off[k] + in, (size_t)c);
+        const uint64_t in = x + f - dst[k], c = std::min<uint64_t>(len[k] - in, z - f);
+        memcpy(img + f, src + src_off[k] + in, (size_t)c);
         f += c;
       }
-      for (uint64_t done = 0; done < bn;) {
-        const ssize_t w = pwrite(fd, buf.data() + done, (size_t)(bn - done), (off_t)(file_off + x + done));
-        if (w <= 0) {
-          rc = PW_E_IO;
-          break;
-        }
-        done += (uint64_t)w;
-      }
-      x += bn;
+    };
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), bn >> 20));
+    if (T <= 1) {
+      fill(0, bn);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++) th.emplace_back(fill, bn * (uint64_t)t / (uint64_t)T, bn * (uint64_t)(t + 1) / (uint64_t)T);
+      for (auto& y : th) y.join();
     }
-  };
-  if (T <= 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(work, t);
-    for (auto& x : th) x.join();
+    iw.submit(img, bn, file_off + x);
+    x += bn;
   }
-  return rc.load();
+  return iw.finish();
 }
 
 // Cuts of a rank's received lines ('\n'-ended, n bytes) into batches of at most `target` bytes (at

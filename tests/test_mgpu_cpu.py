@@ -275,9 +275,12 @@ def test_batch_cuts_c_matches_numpy(built, seed):
     assert mgpu.batch_cuts(np.zeros(0, np.uint8), None, 10) == []
 
 
-def test_gather_write_spans(built, tmp_path):
-    """pw_gather_write: spans of a source in order, written contiguously at an offset (threads,
-    8 MB blocks: a 20 MB case crosses blocks and threads)."""
+@pytest.mark.parametrize("img", [None, 1 << 20, 4099])
+def test_gather_write_spans(built, tmp_path, monkeypatch, img):
+    """pw_gather_write: spans of a source in order, written contiguously at an offset (host threads
+    fill 64 MB images, one pwrite each; small images: many images, spans cut between images)."""
+    if img:
+        monkeypatch.setenv("PW_EMIT_IMG_BYTES", str(img))
     rng = np.random.default_rng(4)
     src = rng.integers(0, 256, 24 << 20, dtype=np.uint8)
     lens = rng.integers(0, 5000, 8000).astype(np.uint64)
@@ -294,9 +297,13 @@ def test_gather_write_spans(built, tmp_path):
     assert got[:37] == b"x" * 37 and got[37:37 + len(want)] == want
 
 
-def test_render_range_equals_write_range(built, tmp_path):
+@pytest.mark.parametrize("img", [None, 1000])
+def test_render_range_equals_write_range(built, tmp_path, monkeypatch, img):
     """pw_batch_render_range's bytes back to back are what pw_batch_write_range pwrites at the items'
-    offsets (plain items, messages, dedupe warnings; zero results: header-only records)."""
+    offsets (plain items, messages, dedupe warnings; zero results: header-only records).  Contiguous
+    offsets take the image path (small images: a run cut into many)."""
+    if img:
+        monkeypatch.setenv("PW_EMIT_IMG_BYTES", str(img))
     from test_shard import _with_duplicates_and_comments
     from conftest import synth_paf
     fa, paf = synth_paf(tmp_path, 0, seed=43)
@@ -318,3 +325,34 @@ def test_render_range_equals_write_range(built, tmp_path):
         os.close(fd)
     assert bytes(out) == p.read_bytes() and eb == eb2
     assert k > 10 and int(en.sum()) > 0
+
+
+def test_write_range_scattered_destinations(built, tmp_path):
+    """pw_batch_write_range with every item's destination out of order (the per-thread pwrite path,
+    not the image path): each item's bytes land at its own offset."""
+    from conftest import synth_paf
+    fa, paf = synth_paf(tmp_path, 0, seed=44)
+    b = pw.HostBatch(fa, paf, 0)
+    n = int(b.view.n_alns)
+    res = np.zeros(max(n, 1) * 48, np.uint8)
+    z = np.zeros(16, np.uint8)
+    ln, st, on, en = b.items(z, res, z)
+    k = len(ln)
+    out, eb = b.render_range(z, res, z, 0, int(on.sum()), k, int(en.sum()))
+    on = on.astype(np.int64)
+    src = np.concatenate([[0], np.cumsum(on)[:-1]])
+    order = np.random.default_rng(5).permutation(k)  # item order in the file
+    dst = np.zeros(k, np.int64)
+    dst[order] = np.concatenate([[0], np.cumsum(on[order])[:-1]])
+    p = tmp_path / "s.bin"
+    p.write_bytes(b"")
+    fd = os.open(p, os.O_WRONLY)
+    try:
+        b.write_range(z, res, z, fd, 0, dst.astype(np.uint64), int(en.sum()))
+    finally:
+        os.close(fd)
+    got = p.read_bytes()
+    ob = bytes(out)
+    assert k > 10 and len(got) == len(ob)
+    for j in range(k):
+        assert got[dst[j]:dst[j] + on[j]] == ob[src[j]:src[j] + on[j]]
