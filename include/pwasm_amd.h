@@ -396,6 +396,8 @@ int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_
  * first item with status >= 0, reproduces the single-process output (pwasm_amd/shard.py). */
 int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                          const pw_page* pages_host, const char* path);
+/* Frees the batch: its memory is returned by a background thread (PW_BATCH_FREE_SYNC=1: on the
+ * caller), so the call returns at once; the batch and its array pointers are invalid after it. */
 void pw_batch_free(pw_batch* b);
 /* `pafreport -w`: the multi-FASTA MSA of the batch's last query run (refMSA->writeMSA,
  * pafreport.cpp:382-421, 447-450; GapAssem.cpp:645-753, 1006-1046) from its gap lists — the

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 S=$(date +%s)
 PW_PROFILE_HOST=1 timeout -k 10 580 python3 bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail gpurun_out/bench_$TAG.err; exit 1; }
 echo "bench wall $(( $(date +%s) - S )) s"
-grep "mgpu rank\|e2e\]" gpurun_out/bench_$TAG.err
+grep "mgpu \|e2e\]" gpurun_out/bench_$TAG.err
 python3 -c "
 import json; d=json.load(open('gpurun_out/bench_$TAG.json'))
 print('value', d['value'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'], 'parity', d['parity'])

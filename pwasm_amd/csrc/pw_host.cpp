@@ -20,6 +20,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <future>
 #include <memory>
 #include <new>
@@ -356,6 +357,12 @@ int host_threads() {
   if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = CPU_COUNT(&cs);
   if (n <= 0) n = (int)std::thread::hardware_concurrency();
   return std::max(1, std::min(n, 16));
+}
+// wall clock for the PW_PROFILE_HOST lines
+static double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+static bool host_prof() {
+  static const bool on = getenv("PW_PROFILE_HOST") && *getenv("PW_PROFILE_HOST") && strcmp(getenv("PW_PROFILE_HOST"), "0");
+  return on;
 }
 
 template <class F>
@@ -2603,12 +2610,14 @@ extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, u
     return nullptr;
   };
   if (!fasta || (len && !text) || (n_lines && !line_no)) return fail("bad arguments");
+  const double t0 = now_s();
   pw_batch* bt = new pw_batch();
   std::string err;
   if (!bt->q.load(fasta, err)) {
     delete bt;
     return fail(err);
   }
+  const double t1 = now_s();
   struct stat st;
   const long long fsize = (stat(fasta, &st) == 0) ? (long long)st.st_size : -1;
   bool gene = flags & 1u, full = flags & 2u, fc = flags & 4u, fn = flags & 8u;
@@ -2628,16 +2637,46 @@ extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, u
   }
   Batch& b = bt->b;
   b.buf.resize((size_t)len + 1);
-  if (len) memcpy(b.buf.data(), text, (size_t)len);
   b.buf[(size_t)len] = '\0';
-  char* s = b.buf.data();
-  size_t p = 0;
-  while (p < len) {
-    const char* q = (const char*)memchr(s + p, '\n', (size_t)len - p);
-    const size_t e = q ? (size_t)(q - s) : (size_t)len;
-    b.lines.push_back({p, (uint32_t)(e - p)});
-    s[e] = '\0';
-    p = e + 1;
+  {  // copy + line split by host threads over byte ranges that start at line starts
+    char* s = b.buf.data();
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), len >> 22));
+    std::vector<uint64_t> cut((size_t)T + 1, len);
+    cut[0] = 0;
+    for (int t = 1; t < T; t++) {
+      uint64_t c = std::max(cut[t - 1], len * (uint64_t)t / (uint64_t)T);
+      if (c > 0 && c < len) {  // the line start at or after c
+        const char* q = (const char*)memchr(text + c - 1, '\n', (size_t)(len - c + 1));
+        c = q ? (uint64_t)(q - text) + 1 : len;
+      }
+      cut[t] = c;
+    }
+    std::vector<std::vector<LineRef>> part((size_t)T);
+    auto work = [&](int t) {
+      const uint64_t a = cut[t], z = cut[t + 1];
+      if (z <= a) return;
+      memcpy(s + a, text + a, (size_t)(z - a));
+      auto& ls = part[t];
+      ls.reserve((size_t)((z - a) / 256 + 16));
+      for (uint64_t p = a; p < z;) {
+        const char* q = (const char*)memchr(s + p, '\n', (size_t)(z - p));
+        const uint64_t e = q ? (uint64_t)(q - s) : z;
+        ls.push_back({p, (uint32_t)(e - p)});
+        s[e] = '\0';  // (e == len: the terminator already there)
+        p = e + 1;
+      }
+    };
+    if (T <= 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++) th.emplace_back(work, t);
+      for (auto& x : th) x.join();
+    }
+    size_t nl = 0;
+    for (auto& v : part) nl += v.size();
+    b.lines.reserve(nl);
+    for (auto& v : part) b.lines.append(v.data(), v.size());
   }
   if (b.lines.size() != n_lines) {
     delete bt;
@@ -2645,8 +2684,13 @@ extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, u
   }
   b.line_no.resize((size_t)n_lines);
   if (n_lines) memcpy(b.line_no.data(), line_no, (size_t)n_lines * 8);
+  const double t2 = now_s();
   if (n_lines) bt->pk.pack(b);
+  const double t3 = now_s();
   bt->alg_in = alg_bytes(b, bt->q, skip);
+  if (host_prof())
+    fprintf(stderr, "[from_buffer] %llu lines: queries %.3f s, copy + split %.3f s, pack %.3f s, alg bytes %.3f s\n",
+            (unsigned long long)n_lines, t1 - t0, t2 - t1, t3 - t2, now_s() - t3);
   return bt;
 }
 
@@ -2739,11 +2783,95 @@ extern "C" int pw_batch_items(const pw_batch* bt, const uint8_t* text_host, cons
   return PW_OK;
 }
 
-// Write the stdout bytes of the batch's items [first, first + n_items) at out_off[k - first] of fd
-// (pwrite: ranks write disjoint ranges of one file) and their stderr bytes back to back into
-// err_buf.  Items whose destinations follow each other are assembled into one buffer and written
-// by one pwrite (up to 8 MB), by up to host_threads() threads over contiguous item ranges (a
-// per-item pwrite was the multi-GPU driver's largest host cost: 5.2 s for 3 M records).
+namespace {
+
+// Plain flags and the back-to-back stdout / stderr offsets (ooff / eoff: n + 1 entries) of the items
+// [first, first + n) of a finished batch: one sequential pass (about 12 ns an item).
+int plan_items(const Batch& b, uint64_t first, uint64_t n, const uint8_t* text, const pw_aln_result* res,
+               const pw_page* pages, std::vector<uint8_t>& plain, std::vector<uint64_t>& ooff,
+               std::vector<uint64_t>& eoff) {
+  plain.assign((size_t)n, 0);
+  ooff.assign((size_t)n + 1, 0);
+  eoff.assign((size_t)n + 1, 0);
+  for (uint64_t j = 0; j < n; j++) {
+    const LogItem& it = b.log[(size_t)(first + j)];
+    uint64_t on = 0, en = 0;
+    plain[j] = item_plain(b, it, res) ? 1 : 0;
+    if (plain[j]) plain_sizes(b, it, res, pages, on, en);
+    else if (item_slow(b, it, text, res, pages, nullptr, nullptr, &on, &en) == INT_MIN)
+      return PW_E_NOMEM;
+    ooff[j + 1] = ooff[j] + on;
+    eoff[j + 1] = eoff[j] + en;
+  }
+  return PW_OK;
+}
+
+// Item j's stdout bytes at o and its stderr bytes at e (null: dropped).
+int render_item(const Batch& b, const LogItem& it, bool plain, const uint8_t* text, const pw_aln_result* res,
+                const pw_page* pages, uint8_t* o, char* e, std::string& so, std::string& se) {
+  if (plain) {
+    const RecHost& rh = b.recs[it.idx];
+    memcpy(o, b.hdr.data() + rh.hdr_off, rh.hdr_len);
+    o += rh.hdr_len;
+    for_spans(res[it.idx], pages, [&](uint64_t lo, uint64_t n) {
+      memcpy(o, text + lo, n);
+      o += n;
+    });
+    if (rh.n_softclip && e) {
+      const char* ln = b.buf.data() + rh.line_off;
+      const size_t ll = strlen(ln);
+      for (int q = 0; q < rh.n_softclip; q++) {
+        memcpy(e, kSoftclipMsg, sizeof(kSoftclipMsg) - 1);
+        e += sizeof(kSoftclipMsg) - 1;
+        memcpy(e, ln, ll);
+        e += ll;
+        *e++ = '\n';
+      }
+    }
+    return PW_OK;
+  }
+  if (item_slow(b, it, text, res, pages, &so, &se, nullptr, nullptr) == INT_MIN) return PW_E_NOMEM;
+  memcpy(o, so.data(), so.size());
+  if (e && !se.empty()) memcpy(e, se.data(), se.size());
+  return PW_OK;
+}
+
+// The items [j0, j1) of a plan rendered back to back: item j's stdout bytes at out + ooff[j] - ooff[j0],
+// its stderr bytes at err + eoff[j] - eoff[j0] (null: dropped); host threads over item ranges of
+// about equal bytes.
+int render_items(const Batch& b, uint64_t first, const std::vector<uint8_t>& plain, const std::vector<uint64_t>& ooff,
+                 const std::vector<uint64_t>& eoff, uint64_t j0, uint64_t j1, const uint8_t* text,
+                 const pw_aln_result* res, const pw_page* pages, uint8_t* out, char* err) {
+  std::atomic<int> rc{PW_OK};
+  auto work = [&](uint64_t a, uint64_t z) {
+    std::string so, se;
+    for (uint64_t j = a; j < z; j++) {
+      const int r = render_item(b, b.log[(size_t)(first + j)], plain[j] != 0, text, res, pages,
+                                out + (ooff[j] - ooff[j0]), err ? err + (eoff[j] - eoff[j0]) : nullptr, so, se);
+      if (r != PW_OK) {
+        rc = r;
+        return;
+      }
+    }
+  };
+  const uint64_t n = j1 - j0, bytes = ooff[j1] - ooff[j0];
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)host_threads(), n / 64, bytes >> 18}));
+  if (T <= 1) {
+    work(j0, j1);
+  } else {  // cuts at equal byte shares
+    std::vector<uint64_t> cut((size_t)T + 1, j1);
+    cut[0] = j0;
+    for (int t = 1; t < T; t++)
+      cut[t] = (uint64_t)(std::lower_bound(ooff.begin() + (ptrdiff_t)j0, ooff.begin() + (ptrdiff_t)j1,
+                                           ooff[j0] + bytes * (uint64_t)t / (uint64_t)T) - ooff.begin());
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      if (cut[t + 1] > cut[t]) th.emplace_back(work, cut[t], cut[t + 1]);
+    for (auto& x : th) x.join();
+  }
+  return rc.load();
+}
+
 // A file range assembled in images (64 MB) and written with one pwrite per image from a
 // writer thread while host threads fill the next image: writers of one file serialise on its inode
 // lock, so one large pwrite reaches the file system's rate and many concurrent smaller ones do not
@@ -2758,10 +2886,15 @@ struct ImageWriter {
   int ik = 0;
   std::thread wr;
   std::atomic<int> rc{PW_OK};
+  double waited = 0;  // seconds spent waiting for the writer thread
   explicit ImageWriter(int f) : fd(f) {}
   ~ImageWriter() { join(); }
   void join() {
-    if (wr.joinable()) wr.join();
+    if (wr.joinable()) {
+      const double t = now_s();
+      wr.join();
+      waited += now_s() - t;
+    }
   }
   uint8_t* next(uint64_t n) {  // the image to fill (n bytes)
     static thread_local std::unique_ptr<uint8_t[]> pool[2];
@@ -2796,26 +2929,26 @@ struct ImageWriter {
   }
 };
 
+}  // namespace
+
+// Write the stdout bytes of the batch's items [first, first + n_items) at out_off[k - first] of fd
+// (pwrite: ranks write disjoint ranges of one file) and their stderr bytes back to back into
+// err_buf.  Runs of items whose destinations follow each other (a rank's whole window with one
+// rank) go out as 64 MB images through ImageWriter; scattered destinations (ranks' lines
+// interleaved, PW_MGPU_WRITE=pwrite) are assembled per host thread into buffers of up to 8 MB, one
+// pwrite each (a per-item pwrite was the multi-GPU driver's largest host cost: 5.2 s for 3 M records).
 extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host, const pw_aln_result* res_host,
                                     const pw_page* pages_host, int fd, uint64_t first, const uint64_t* out_off,
                                     uint64_t n_items, char* err_buf, uint64_t err_cap) {
   if (!bt || (n_items && !out_off) || first > bt->b.log.size() || n_items > bt->b.log.size() - first)
     return PW_E_ARG;
   const Batch& b = bt->b;
-  // stderr offsets (a sequential pass: plain items only have soft-clip warnings)
-  std::vector<uint64_t> eoff((size_t)n_items + 1, 0), osz((size_t)n_items);
-  std::vector<uint8_t> plain((size_t)n_items);
-  for (uint64_t j = 0; j < n_items; j++) {
-    const LogItem& it = b.log[(size_t)(first + j)];
-    uint64_t on = 0, en = 0;
-    plain[j] = item_plain(b, it, res_host) ? 1 : 0;
-    if (plain[j]) plain_sizes(b, it, res_host, pages_host, on, en);
-    else if (item_slow(b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en) == INT_MIN)
-      return PW_E_NOMEM;
-    osz[j] = on;
-    eoff[j + 1] = eoff[j] + en;
-  }
+  const double t0 = now_s();
+  std::vector<uint8_t> plain;
+  std::vector<uint64_t> ooff, eoff;
+  if (int r = plan_items(b, first, n_items, text_host, res_host, pages_host, plain, ooff, eoff)) return r;
   if (err_buf && eoff[n_items] > err_cap) return PW_E_ARG;
+  const double t1 = now_s();
   // runs of items whose destinations follow each other, cut at the image size
   struct Seg {
     uint64_t j0, j1, d0, n;
@@ -2824,30 +2957,35 @@ extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host
   const uint64_t kImg = ImageWriter::img_bytes();
   uint64_t runs = 0;  // contiguity breaks + 1
   for (uint64_t j = 0; j < n_items; j++) {
+    const uint64_t on = ooff[j + 1] - ooff[j];
     const bool brk = segs.empty() || out_off[j] != segs.back().d0 + segs.back().n;
     runs += brk;
-    if (brk || (segs.back().n && segs.back().n + osz[j] > kImg)) segs.push_back({j, j, out_off[j], 0});
+    if (brk || (segs.back().n && segs.back().n + on > kImg)) segs.push_back({j, j, out_off[j], 0});
     segs.back().j1 = j + 1;
-    segs.back().n += osz[j];
+    segs.back().n += on;
   }
   if (runs && runs * 64 <= n_items) {  // long runs (one rank's window): images
     ImageWriter iw(fd);
+    double fill = 0;
+    int r = PW_OK;
     for (const Seg& sg : segs) {
       uint8_t* img = iw.next(sg.n);
       if (!img) {
-        iw.finish();
-        return PW_E_NOMEM;
+        r = PW_E_NOMEM;
+        break;
       }
-      const int r = pw_batch_render_range(bt, text_host, res_host, pages_host, first + sg.j0, sg.j1 - sg.j0, img, sg.n,
-                                          err_buf ? err_buf + eoff[sg.j0] : nullptr,
-                                          err_buf ? eoff[sg.j1] - eoff[sg.j0] : 0);
-      if (r != PW_OK) {
-        iw.finish();
-        return r;
-      }
+      const double f0 = now_s();
+      r = render_items(b, first, plain, ooff, eoff, sg.j0, sg.j1, text_host, res_host, pages_host, img,
+                       err_buf ? err_buf + eoff[sg.j0] : nullptr);
+      fill += now_s() - f0;
+      if (r != PW_OK) break;
       iw.submit(img, sg.n, sg.d0);
     }
-    return iw.finish();
+    const int w = iw.finish();
+    if (host_prof())
+      fprintf(stderr, "[host write_range] %llu items, %.1f MB in %zu images: plan %.3f s, fill %.3f s, writer wait %.3f s, total %.3f s\n",
+              (unsigned long long)n_items, ooff[n_items] / 1e6, segs.size(), t1 - t0, fill, iw.waited, now_s() - t0);
+    return r != PW_OK ? r : w;
   }
   constexpr uint64_t kBuf = 8ull << 20;
   std::atomic<int> rc{PW_OK};
@@ -2868,34 +3006,16 @@ extern "C" int pw_batch_write_range(const pw_batch* bt, const uint8_t* text_host
     };
     std::string so, se;
     for (uint64_t j = j0; j < j1 && rc.load() == PW_OK; j++) {
-      const LogItem& it = b.log[(size_t)(first + j)];
+      const uint64_t on = ooff[j + 1] - ooff[j];
       if (!buf.empty() && (out_off[j] != d0 + buf.size() || buf.size() >= kBuf)) flush();
       if (buf.empty()) d0 = out_off[j];
-      if (plain[j]) {
-        const RecHost& rh = b.recs[it.idx];
-        const uint8_t* h = reinterpret_cast<const uint8_t*>(b.hdr.data() + rh.hdr_off);
-        buf.insert(buf.end(), h, h + rh.hdr_len);
-        for_spans(res_host[it.idx], pages_host,
-                  [&](uint64_t lo, uint64_t n) { buf.insert(buf.end(), text_host + lo, text_host + lo + n); });
-        if (rh.n_softclip && err_buf) {
-          char* e = err_buf + eoff[j];
-          const char* ln = b.buf.data() + rh.line_off;
-          const size_t ll = strlen(ln);
-          for (int q = 0; q < rh.n_softclip; q++) {
-            memcpy(e, kSoftclipMsg, sizeof(kSoftclipMsg) - 1);
-            e += sizeof(kSoftclipMsg) - 1;
-            memcpy(e, ln, ll);
-            e += ll;
-            *e++ = '\n';
-          }
-        }
-      } else {
-        if (item_slow(b, it, text_host, res_host, pages_host, &so, &se, nullptr, nullptr) == INT_MIN) {
-          rc = PW_E_NOMEM;
-          break;
-        }
-        buf.insert(buf.end(), so.begin(), so.end());
-        if (err_buf && !se.empty()) memcpy(err_buf + eoff[j], se.data(), se.size());
+      const size_t at = buf.size();
+      buf.resize(at + on);
+      const int r = render_item(b, b.log[(size_t)(first + j)], plain[j] != 0, text_host, res_host, pages_host,
+                                buf.data() + at, err_buf ? err_buf + eoff[j] : nullptr, so, se);
+      if (r != PW_OK) {
+        rc = r;
+        break;
       }
     }
     if (!buf.empty() && rc.load() == PW_OK) flush();
@@ -2921,64 +3041,11 @@ extern "C" int pw_batch_render_range(const pw_batch* bt, const uint8_t* text_hos
   if (!bt || first > bt->b.log.size() || n_items > bt->b.log.size() - first || (n_items && !out_buf && out_cap))
     return PW_E_ARG;
   const Batch& b = bt->b;
-  std::vector<uint64_t> ooff((size_t)n_items + 1, 0), eoff((size_t)n_items + 1, 0);
-  std::vector<uint8_t> plain((size_t)n_items);
-  for (uint64_t j = 0; j < n_items; j++) {
-    const LogItem& it = b.log[(size_t)(first + j)];
-    uint64_t on = 0, en = 0;
-    plain[j] = item_plain(b, it, res_host) ? 1 : 0;
-    if (plain[j]) plain_sizes(b, it, res_host, pages_host, on, en);
-    else if (item_slow(b, it, text_host, res_host, pages_host, nullptr, nullptr, &on, &en) == INT_MIN)
-      return PW_E_NOMEM;
-    ooff[j + 1] = ooff[j] + on;
-    eoff[j + 1] = eoff[j] + en;
-  }
+  std::vector<uint8_t> plain;
+  std::vector<uint64_t> ooff, eoff;
+  if (int r = plan_items(b, first, n_items, text_host, res_host, pages_host, plain, ooff, eoff)) return r;
   if (ooff[n_items] > out_cap || (err_buf && eoff[n_items] > err_cap)) return PW_E_ARG;
-  std::atomic<int> rc{PW_OK};
-  auto work = [&](uint64_t j0, uint64_t j1) {
-    std::string so, se;
-    for (uint64_t j = j0; j < j1; j++) {
-      const LogItem& it = b.log[(size_t)(first + j)];
-      uint8_t* o = out_buf + ooff[j];
-      if (plain[j]) {
-        const RecHost& rh = b.recs[it.idx];
-        memcpy(o, b.hdr.data() + rh.hdr_off, rh.hdr_len);
-        o += rh.hdr_len;
-        for_spans(res_host[it.idx], pages_host, [&](uint64_t lo, uint64_t n) {
-          memcpy(o, text_host + lo, n);
-          o += n;
-        });
-        if (rh.n_softclip && err_buf) {
-          char* e = err_buf + eoff[j];
-          const char* ln = b.buf.data() + rh.line_off;
-          const size_t ll = strlen(ln);
-          for (int q = 0; q < rh.n_softclip; q++) {
-            memcpy(e, kSoftclipMsg, sizeof(kSoftclipMsg) - 1);
-            e += sizeof(kSoftclipMsg) - 1;
-            memcpy(e, ln, ll);
-            e += ll;
-            *e++ = '\n';
-          }
-        }
-      } else {
-        if (item_slow(b, it, text_host, res_host, pages_host, &so, &se, nullptr, nullptr) == INT_MIN) {
-          rc = PW_E_NOMEM;
-          return;
-        }
-        memcpy(o, so.data(), so.size());
-        if (err_buf && !se.empty()) memcpy(err_buf + eoff[j], se.data(), se.size());
-      }
-    }
-  };
-  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)host_threads(), n_items / 256));
-  if (T <= 1) {
-    work(0, n_items);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++) th.emplace_back(work, n_items * (uint64_t)t / (uint64_t)T, n_items * (uint64_t)(t + 1) / (uint64_t)T);
-    for (auto& x : th) x.join();
-  }
-  return rc.load();
+  return render_items(b, first, plain, ooff, eoff, 0, n_items, text_host, res_host, pages_host, out_buf, err_buf);
 }
 
 // Spans src[src_off[k], + len[k]) for k = 0..n-1, in order, written contiguously to fd from
@@ -2993,6 +3060,7 @@ extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, co
   if (total == 0) return PW_OK;
   ImageWriter iw(fd);
   const uint64_t kImg = ImageWriter::img_bytes();
+  const double t0 = now_s();
   for (uint64_t x = 0; x < total;) {  // one image per kImg bytes of the range
     const uint64_t bn = std::min<uint64_t>(kImg, total - x);
     uint8_t* img = iw.next(bn);
@@ -3020,7 +3088,10 @@ extern "C" int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, co
     iw.submit(img, bn, file_off + x);
     x += bn;
   }
-  return iw.finish();
+  const int r = iw.finish();
+  if (host_prof())
+    fprintf(stderr, "[host gather_write] %.1f MB: writer wait %.3f s, total %.3f s\n", total / 1e6, iw.waited, now_s() - t0);
+  return r;
 }
 
 // Cuts of a rank's received lines ('\n'-ended, n bytes) into batches of at most `target` bytes (at
@@ -3077,6 +3148,47 @@ extern "C" int pw_batch_write_at(const pw_batch* bt, const uint8_t* text_host, c
   return pw_batch_write_range(bt, text_host, res_host, pages_host, fd, 0, out_off, n_items, err_buf, err_cap);
 }
 
-extern "C" void pw_batch_free(pw_batch* bt) { delete bt; }
+// Batches are freed by a reaper thread: releasing one returns ~1 GB of buffers to the system (about
+// 75 ms of unmapping at cfg3's 256 MB batches), which the multi-GPU driver's window loop otherwise
+// waited for once per batch.  PW_BATCH_FREE_SYNC=1 frees on the caller.  The reaper is detached: a
+// batch still queued at exit is left to process teardown.
+namespace {
+struct BatchReaper {
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<pw_batch*> q;
+  bool started = false;
+  void put(pw_batch* bt) {
+    std::unique_lock<std::mutex> lk(m);
+    if (!started) {
+      started = true;
+      std::thread([this]() {
+        for (;;) {
+          std::vector<pw_batch*> batch;
+          {
+            std::unique_lock<std::mutex> l2(m);
+            cv.wait(l2, [this]() { return !q.empty(); });
+            batch.swap(q);
+          }
+          for (pw_batch* b : batch) delete b;
+        }
+      }).detach();
+    }
+    q.push_back(bt);
+    cv.notify_one();
+  }
+};
+BatchReaper* reaper() {
+  static BatchReaper* r = new BatchReaper;  // (never destroyed: the detached thread may outlive statics)
+  return r;
+}
+}  // namespace
+
+extern "C" void pw_batch_free(pw_batch* bt) {
+  if (!bt) return;
+  static const bool sync = getenv("PW_BATCH_FREE_SYNC") && atoi(getenv("PW_BATCH_FREE_SYNC")) != 0;
+  if (sync) delete bt;
+  else reaper()->put(bt);
+}
 
 extern "C" const char* pw_version(void) { return "pwasm_amd 0.1 (gfx950)"; }

@@ -224,7 +224,7 @@ class OffsetWriter:
         # world > 1: "exchange" (each rank writes one contiguous range of each window, _exchange_write)
         # or "pwrite" (each rank pwrites its own items at their offsets); PW_MGPU_WRITE picks
         self.mode = os.environ.get("PW_MGPU_WRITE", "exchange")
-        self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item], ...] in line order
+        self.pending = []  # [[(b, text_h, res_h, pages_h, items), next item, release], ...] in line order
         self.tmp_out = None
         if out_path is None:  # stdout: assembled in a file, streamed out by rank 0 window by window
             if rank == 0:
@@ -241,6 +241,7 @@ class OffsetWriter:
             dist.barrier()
         self.fd = os.open(out_path, os.O_WRONLY)
         self.rd = open(self.tmp_out, "rb") if self.tmp_out and rank == 0 else None
+        self.prof = _Phases(rank, "window")  # PW_PROFILE_HOST: the steps of _window, summed
 
     def _reduce(self, vals, op):
         import torch
@@ -250,8 +251,10 @@ class OffsetWriter:
             dist.all_reduce(t, op=op)
         return t.cpu().numpy()
 
-    def add(self, out):
-        self.pending.append([out, 0])
+    def add(self, out, release=None):
+        """A finished batch's outputs; release() is called once all its items are written (the
+        host text buffer goes back to its pool)."""
+        self.pending.append([out, 0, release])
 
     def advance(self, covered):
         """This rank has the items of all its lines < covered (n_total: all it will ever have)."""
@@ -262,13 +265,16 @@ class OffsetWriter:
         import torch
         import torch.distributed as dist
         lo, hi = self.j * self.W, min((self.j + 1) * self.W, self.n_total)
+        self.prof.mark("(outside)")
         fatal = self.BIG
-        for (_, _, _, _, (ln, st, _, _)), c in self.pending:
+        for ent in self.pending:
+            (_, _, _, _, (ln, st, _, _)), c = ent[0], ent[1]
             sel = (ln[c:] < hi) & (st[c:] >= 0)
             if sel.any():
                 fatal = min(fatal, int(ln[c:][sel][0]))
         MIN = dist.ReduceOp.MIN if self.world > 1 else None
         stop, ok = (int(x) for x in self._reduce([fatal, 0 if self.err else 1], MIN))
+        self.prof.mark("stop reduce")
         if not ok:  # an input error on some rank: the first one in rank order, printed by rank 0
             errs = [self.err]
             if self.world > 1:
@@ -285,7 +291,7 @@ class OffsetWriter:
         lens = np.zeros(hi - lo, dtype=np.int64)
         spans, owner = [], -1
         for ent in self.pending:
-            (_, _, _, _, (ln, st, on, en)), c = ent
+            (_, _, _, _, (ln, st, on, en)), c = ent[0], ent[1]
             k = c + int(np.searchsorted(ln[c:], min(hi, stop + 1) if stop != self.BIG else hi, side="left"))
             spans.append((c, k))
             if k > c and int(ln[k - 1]) == stop:
@@ -301,6 +307,7 @@ class OffsetWriter:
         off[0] = self.base
         np.cumsum(lens, out=off[1:])
         off[1:] += self.base
+        self.prof.mark("offsets")
         errs = []
         exch = self.world > 1 and self.mode == "exchange"
         mine = []
@@ -319,9 +326,17 @@ class OffsetWriter:
             for i, e1, n in zip(nz, ends, en[nz]):
                 errs.append((int(ln[i]), eb[int(e1) - int(n):int(e1)]))
             ent[1] = k
+        self.prof.mark("render/write")
         if exch:
             self._exchange_write(lens, own, off, mine)
-        self.pending = [e for e in self.pending if e[1] < len(e[0][4][0])]
+        keep = []
+        for e in self.pending:
+            if e[1] < len(e[0][4][0]):
+                keep.append(e)
+            elif e[2] is not None:
+                e[2]()
+        self.pending = keep
+        self.prof.mark("exchange write/drop")
         if self.world > 1:  # (every rank's pwrites are done once rank 0 has its stderr)
             allerr = [None] * self.world if self.rank == 0 else None
             dist.gather_object(errs, allerr, dst=0)
@@ -340,6 +355,7 @@ class OffsetWriter:
             for _, e in errs:
                 sys.stderr.buffer.write(e)
             sys.stderr.buffer.flush()
+        self.prof.mark("stderr/stdout")
         self.base = int(off[-1])
         self.j += 1
         if stop != self.BIG:  # the exit code is the fatal item's (its owner's status)
@@ -391,6 +407,7 @@ class OffsetWriter:
     def close(self):
         """Finish every window; -> the exit code of the single-process run."""
         self.advance(self.n_total)
+        self.prof.report()
         os.close(self.fd)
         if self.rd is not None:
             self.rd.close()
@@ -409,6 +426,7 @@ def write_items_at(outs, n_total, out_path, world, rank, dv, tmpdir=None, window
 
 
 def main(argv=None) -> int:
+    import queue
     import threading
 
     import torch
@@ -480,7 +498,36 @@ def main(argv=None) -> int:
             made[k] = e
 
     out_path = opts.get("o") or None
+    # (no more text buffers than this rank has batches: at N = 8 a rank has ~2 batches of cfg3)
+    hostbufs = HostTextPool(min(int(os.environ.get("PW_MGPU_HOST_SLOTS", "4")), max(1, len(cuts))))
     writer = OffsetWriter(n_total, out_path, world, rank, dv, extra.get("tmpdir"))
+    # ---- 3. the writer thread: each finished batch is handed over with the line its rank has
+    # covered, and the windows that completes are written (offsets, render + pwrite, stderr) while
+    # this thread stages / runs / fetches the next batch.  The writer's collectives (window
+    # reductions, the exchange write) are the only ones between exchange() and finish_run, so their
+    # order is the same on every rank.
+    wq = queue.Queue(maxsize=int(os.environ.get("PW_MGPU_WRITE_QUEUE", "2")))
+    werr = []
+
+    def write_loop():
+        if device.startswith("cuda"):
+            torch.cuda.set_device(device)
+        while True:
+            job = wq.get()
+            if job is None:
+                return
+            out, release, covered = job
+            if werr:
+                release()
+                continue
+            try:
+                writer.add(out, release)
+                if covered is not None:
+                    writer.advance(covered)
+            except BaseException as e:  # (re-raised by the main thread)
+                werr.append(e)
+    wth = threading.Thread(target=write_loop, name="pw-mgpu-writer", daemon=True)
+    wth.start()
     stream = torch.cuda.current_stream()
     want_tab = "genome-table" in extra
     gname, gacc = {}, np.zeros((1024, 3), np.uint64)  # target name -> row of the summed per-genome table
@@ -507,8 +554,15 @@ def main(argv=None) -> int:
         if prof.on:
             stream.synchronize()
             prof.mark("gpu pass")
-        text_h, res_h, pages_h = pw.fetch_outputs(dev)  # (synchronises the stream)
-        prof.mark("fetch")
+        slot = []
+
+        def take(n):
+            prof.mark("fetch results/pages")
+            t = hostbufs.take(n, slot)
+            prof.mark("fetch alloc")
+            return t
+        text_h, res_h, pages_h = pw.fetch_outputs(dev, take)  # (synchronises the stream)
+        prof.mark("fetch text")
         if want_tab:  # per-genome rows of all batches, summed by target (vectorised: 50k targets a batch at cfg3)
             r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
             gidx = np.fromiter((gname.setdefault(nm, len(gname)) for nm in names), dtype=np.int64, count=len(names))
@@ -520,16 +574,19 @@ def main(argv=None) -> int:
             np.add.at(gacc, gidx, vals)
             prof.mark("genome rows")
         items = b.items(text_h, res_h, pages_h)
-        writer.add((b, text_h, res_h, pages_h, items))
-        del dev, b
+        fatal = bool((items[1] >= 0).any())  # a fatal item: nothing after it is reached
+        covered = None if fatal else (int(line_no[cuts[k + 1][2]]) if k + 1 < len(cuts) else n_total)
         prof.mark("items")
-        if (items[1] >= 0).any():  # a fatal item: nothing after it is reached
+        wq.put(((b, text_h, res_h, pages_h, items), (lambda i=slot[0]: hostbufs.give(i)), covered))
+        del dev, b
+        prof.mark("writer queue wait")
+        if fatal or werr or writer.done:  # (done: the run ended at a window every rank has processed)
             break
-        # ---- 3. the windows this rank's lines so far complete: offsets, pwrites, stderr
-        writer.advance(int(line_no[cuts[k + 1][2]]) if k + 1 < len(cuts) else n_total)
-        prof.mark("write windows")
-        if writer.done:  # the run ended at a window every rank has processed: nothing later is written
-            break
+    wq.put(None)
+    wth.join()
+    prof.mark("writer drain")
+    if werr:
+        raise werr[0]
     if th is not None and th.is_alive():
         th.join()
     made.clear()
@@ -540,13 +597,66 @@ def main(argv=None) -> int:
     return code
 
 
+class HostTextPool:
+    """Reused pinned host buffers for the batches' report text (fetch_outputs): a fresh pageable
+    array per batch cost a page fault per 4 KB on the copy and an unmap of ~1 GB when the batch was
+    dropped.  A buffer is busy from take() until its batch's items are all written (give(), called
+    by OffsetWriter from the writer thread); when every slot is busy take() falls back to a pageable
+    tensor.  The first take() sizes a slot at 1.5x its request and allocates the other slots at that
+    size on a helper thread (pinning ~1.5 GB takes ~0.3 s), so later batches find them ready.
+    Without a GPU (tests) the buffers are ordinary host memory."""
+
+    def __init__(self, slots=4):
+        import threading
+        self.bufs, self.busy = [None] * max(0, slots), [False] * max(0, slots)
+        self.pre = None  # the helper thread allocating the other slots
+
+    def _alloc(self, n):
+        import torch
+        return torch.empty(int(n), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+
+    def take(self, n, slot_out):
+        import threading
+        n = int(n)
+        first = all(b is None for b in self.bufs)
+        if not first and self.pre is not None:
+            self.pre.join()
+            self.pre = None
+        free = [i for i, b in enumerate(self.busy) if not b]
+        fit = [i for i in free if self.bufs[i] is not None and self.bufs[i].numel() >= n]
+        if fit:
+            i = fit[0]
+        elif free:
+            i = free[0]
+            cap = n + n // 2 + (1 << 20)
+            self.bufs[i] = None  # (release the smaller one first)
+            self.bufs[i] = self._alloc(cap)
+            if first and len(self.bufs) > 1:
+                def pre():
+                    for j in range(len(self.bufs)):
+                        if self.bufs[j] is None:
+                            self.bufs[j] = self._alloc(cap)
+                self.pre = threading.Thread(target=pre, daemon=True)
+                self.pre.start()
+        else:
+            slot_out.append(None)
+            return self._alloc(n)
+        self.busy[i] = True
+        slot_out.append(i)
+        return self.bufs[i][:n]
+
+    def give(self, i):
+        if i is not None:
+            self.busy[i] = False
+
+
 class _Phases:
     """PW_PROFILE_HOST=1: wall time per phase of main() (summed over batches), one stderr line per rank."""
 
-    def __init__(self, rank):
+    def __init__(self, rank, what="rank"):
         import time
         self.on = bool(os.environ.get("PW_PROFILE_HOST"))
-        self.rank, self.t, self.acc, self.clock = rank, time.perf_counter(), {}, time.perf_counter
+        self.rank, self.t, self.acc, self.clock, self.what = rank, time.perf_counter(), {}, time.perf_counter, what
 
     def mark(self, name):
         if self.on:
@@ -556,7 +666,7 @@ class _Phases:
 
     def report(self):
         if self.on:
-            print(f"[mgpu rank {self.rank}] " + ", ".join(f"{k} {v:.3f} s" for k, v in self.acc.items()),
+            print(f"[mgpu {self.what} {self.rank}] " + ", ".join(f"{k} {v:.3f} s" for k, v in self.acc.items()),
                   file=sys.stderr, flush=True)
 
 

@@ -142,12 +142,19 @@ def _exchange_rank(rank, world, port, fa, paf, out_path, errf, q, window=None, m
             code = mgpu.write_items_at(outs, n_total, out_path, world, rank, "cpu")
         else:  # windows of a few lines, each batch handed over before the windows it completes
             w = mgpu.OffsetWriter(n_total, out_path, world, rank, "cpu", window=window)
+            pool, released = mgpu.HostTextPool(2), []  # (the text buffers of main(): released once written)
             for k, o in enumerate(outs):
-                w.add(o)
+                slot = []
+                t = pool.take(16, slot)
+                t.zero_()
+                w.add((o[0], t.numpy()) + o[2:], lambda i=slot[0], k=k: (released.append(k), pool.give(i)))
                 w.advance(int(o[4][0][-1]) + 1 if len(o[4][0]) else 0)
+                assert released == sorted(released) and len(released) <= k + 1
             # (finish_run closes the writer; a run ended by a fatal line writes no genome table)
             gtab = {f"t{rank}".encode(): np.array([1, 2, 3], np.uint64)}
             code = mgpu.finish_run(w, None, gtab, {"genome-table": out_path + ".gt"}, world, rank, "cpu")
+            if not w.fatal:  # every batch's buffer went back to the pool
+                assert released == list(range(len(outs))), (released, len(outs))
         q.put((rank, code, n_total, [int(x) for x in line_no]))
         dist.barrier()
     finally:
@@ -356,3 +363,45 @@ def test_write_range_scattered_destinations(built, tmp_path):
     assert k > 10 and len(got) == len(ob)
     for j in range(k):
         assert got[dst[j]:dst[j] + on[j]] == ob[src[j]:src[j] + on[j]]
+
+
+def test_host_text_pool():
+    """HostTextPool: a free slot large enough is reused, a small free slot is regrown, and with every
+    slot busy take() falls back to a fresh tensor (no slot: give(None) is a no-op)."""
+    p = mgpu.HostTextPool(2)
+    s = []
+    a = p.take(100, s)  # slot 0; slot 1 allocated at the same size on the helper thread
+    b = p.take(50, s)
+    c = p.take(10, s)
+    assert s == [0, 1, None] and a.numel() == 100 and b.numel() == 50 and c.numel() == 10
+    assert p.bufs[0].numel() == p.bufs[1].numel() >= 150
+    p.give(1)
+    p.give(None)
+    d = p.take(40, s)  # slot 1 fits
+    assert s[-1] == 1 and d.data_ptr() == b.data_ptr()
+    p.give(0)
+    e = p.take(1 << 22, s)  # slot 0 too small: regrown
+    assert s[-1] == 0 and e.numel() == 1 << 22
+
+
+def test_from_buffer_threaded_split_matches_files(built, tmp_path):
+    """pw_batch_from_buffer copies and splits its lines on host threads (byte ranges snapped to line
+    starts, > 4 MB): the packed batch equals pw_batch_from_files on the same PAF (arrays, and the
+    items of a zero-results pass)."""
+    from conftest import synth_paf
+    fa, paf = synth_paf(tmp_path, 2, seed=7, scale=0.3)
+    raw = open(paf, "rb").read()
+    assert len(raw) > (12 << 20)
+    text = np.frombuffer(raw, np.uint8)
+    line_no = np.arange(raw.count(b"\n"), dtype=np.uint64)
+    flags = pw.FLAG_G | pw.FLAG_C
+    a = pw.HostBatch(fa, paf, flags)
+    b = pw.HostBatch.from_buffer(fa, text, line_no, flags, None)
+    for name in ("desc", "ops", "lits", "qseq", "qoff", "qlen"):
+        assert np.array_equal(a.array(name), b.array(name)), name
+    n = int(a.view.n_alns)
+    res = np.zeros(max(n, 1) * 48, np.uint8)
+    z = np.zeros(16, np.uint8)
+    ia, ib = a.items(z, res, z), b.items(z, res, z)
+    for x, y in zip(ia, ib):
+        assert np.array_equal(x, y)
