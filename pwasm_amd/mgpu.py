@@ -607,7 +607,6 @@ class HostTextPool:
     Without a GPU (tests) the buffers are ordinary host memory."""
 
     def __init__(self, slots=4):
-        import threading
         self.bufs, self.busy = [None] * max(0, slots), [False] * max(0, slots)
         self.pre = None  # the helper thread allocating the other slots
 
@@ -617,6 +616,8 @@ class HostTextPool:
 
     def take(self, n, slot_out):
         import threading
+
+        import torch
         n = int(n)
         first = all(b is None for b in self.bufs)
         if not first and self.pre is not None:
@@ -638,9 +639,9 @@ class HostTextPool:
                             self.bufs[j] = self._alloc(cap)
                 self.pre = threading.Thread(target=pre, daemon=True)
                 self.pre.start()
-        else:
+        else:  # (pageable: pinning a one-off buffer costs more than its copy saves)
             slot_out.append(None)
-            return self._alloc(n)
+            return torch.empty(n, dtype=torch.uint8)
         self.busy[i] = True
         slot_out.append(i)
         return self.bufs[i][:n]
