@@ -396,6 +396,9 @@ int pw_batch_write_report(const pw_batch* b, const uint8_t* text_host, const pw_
  * first item with status >= 0, reproduces the single-process output (pwasm_amd/shard.py). */
 int pw_batch_write_items(const pw_batch* b, const uint8_t* text_host, const pw_aln_result* res_host,
                          const pw_page* pages_host, const char* path);
+/* pw_batch_from_buffer flag: keep the cs strings as text for pw_runner_run to pack on the GPU
+ * (pw_pack_cs_batch, as the CLI does); without it the host packs the op words and literals. */
+#define PW_BATCH_GPU_PACK 32u
 /* Frees the batch: its memory is returned by a background thread (PW_BATCH_FREE_SYNC=1: on the
  * caller), so the call returns at once; the batch and its array pointers are invalid after it. */
 void pw_batch_free(pw_batch* b);
@@ -473,6 +476,22 @@ int pw_gather_write(int fd, uint64_t file_off, const uint8_t* src, const uint64_
  * returns the batch count (0 when more than cap). */
 uint64_t pw_batch_cuts(const uint8_t* text, uint64_t n, uint64_t target, uint64_t* out, uint64_t cap);
 
+/* Batch runner (the multi-GPU driver's per-rank device state): the CLI's device
+ * session behind the ABI — the batch's query set and next-stop table uploaded once on the current
+ * device (pw_runner_create), then per batch of that query set pw_runner_run: the cs strings packed
+ * on the GPU (batches made with PW_BATCH_GPU_PACK; the host descriptors are completed from the
+ * packer's totals), the report pass on the runner's stream, results and pages copied back; it
+ * returns the page count and the used text bytes, and pw_runner_fetch copies the results
+ * (n_res = the batch's records), the pages and the text (text_cap >= text_used) out.
+ * pw_runner_genome_rows: the batch's per-genome rows (pw_batch_genomes_get's genome_of / t_aln) from
+ * the results still on the device.  Errors: PW_E_ARG (wrong sizes, another query set), PW_E_HIP. */
+typedef struct pw_runner pw_runner;
+pw_runner* pw_runner_create(const pw_batch* b, char* errbuf, size_t errlen);
+int pw_runner_run(pw_runner* r, pw_batch* b, uint64_t* n_pages, uint64_t* text_used);
+int pw_runner_fetch(pw_runner* r, pw_aln_result* res, uint64_t n_res, pw_page* pages, uint64_t n_pages, uint8_t* text,
+                    uint64_t text_cap);
+void pw_runner_free(pw_runner* r);
+
 /* Per-genome coverage / event tables: genome = target sequence (PAF column 6).  Host: number of
  * distinct targets of a batch (+ bytes of their NUL-terminated names), then per record its
  * genome index (first-appearance order) and aligned target bases.  Device: one row per genome
@@ -487,6 +506,9 @@ uint32_t pw_batch_genomes(pw_batch* b, uint64_t* names_bytes);
 int pw_batch_genomes_get(const pw_batch* b, uint32_t* genome_of, int32_t* t_aln, char* names);
 int pw_genome_table(const pw_aln_result* results, const uint32_t* genome_of, const int32_t* t_aln, uint32_t n_alns,
                     pw_genome_row* rows, uint32_t n_genomes, void* stream);
+/* (the batch runner above: the rows of its last batch, into host memory) */
+int pw_runner_genome_rows(pw_runner* r, const uint32_t* genome_of, const int32_t* t_aln, uint32_t n_alns,
+                          uint32_t n_genomes, pw_genome_row* rows);
 
 const char* pw_version(void);
 

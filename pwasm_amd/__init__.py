@@ -29,6 +29,7 @@ DEV_PAD = 256  # readable bytes required past the end of the device query / lite
 
 # pafreport mode flags for pw_batch_from_files (same meaning as -G/-F/-C/-N)
 FLAG_G, FLAG_F, FLAG_C, FLAG_N, FLAG_W = 1, 2, 4, 8, 16
+FLAG_GPU_PACK = 32  # pw_batch_from_buffer: cs strings packed on the GPU by pw_runner_run (PW_BATCH_GPU_PACK)
 
 
 class AlnDesc(ctypes.Structure):
@@ -193,6 +194,14 @@ _SIGS = {
     "pw_batch_genomes_get": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "pw_genome_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    "pw_runner_create": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "pw_runner_run": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "pw_runner_fetch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]),
+    "pw_runner_genome_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                             ctypes.c_uint32, ctypes.c_void_p]),
+    "pw_runner_free": (None, [ctypes.c_void_p]),
 }
 
 _lib = None
@@ -575,6 +584,64 @@ def items_merge(paths, out_path=None, err_path=None) -> int:
 
 
 GENOME_ROW = 16  # sizeof(pw_genome_row)
+
+
+class Runner:
+    """pw_runner: the CLI's device session for the batches of one query set (queries and the
+    next-stop table uploaded once on the current device; device buffers reused; cs strings of
+    FLAG_GPU_PACK batches packed on the GPU).  run(batch) -> (pages, text bytes); fetch(text, ...)
+    -> (text, results, pages) as numpy, the text copied into `text` (a host uint8 tensor / array
+    of at least that many bytes, e.g. a pinned buffer)."""
+
+    def __init__(self, batch: HostBatch):
+        err = ctypes.create_string_buffer(512)
+        self._h = lib().pw_runner_create(batch._h, err, len(err))
+        if not self._h:
+            raise RuntimeError("pw_runner_create: " + err.value.decode(errors="replace"))
+        self._n = 0
+
+    def run(self, batch: HostBatch):
+        npg, used = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = lib().pw_runner_run(self._h, batch._h, ctypes.byref(npg), ctypes.byref(used))
+        if rc != 0:
+            raise RuntimeError(f"pw_runner_run: {rc}")
+        self._n = int(batch.view.n_alns)
+        return int(npg.value), int(used.value)
+
+    def fetch(self, text, n_pages: int, used: int):
+        res = np.empty(max(self._n, 1) * ctypes.sizeof(AlnResult), np.uint8)
+        pages = np.empty(max(n_pages, 1) * ctypes.sizeof(Page), np.uint8)
+        tp = text.data_ptr() if hasattr(text, "data_ptr") else text.ctypes.data
+        cap = text.numel() if hasattr(text, "numel") else text.size
+        rc = lib().pw_runner_fetch(self._h, res.ctypes.data, self._n, pages.ctypes.data, n_pages, tp if used else None,
+                                   cap)
+        if rc != 0:
+            raise RuntimeError(f"pw_runner_fetch: {rc}")
+        t = text.numpy() if hasattr(text, "numpy") else text
+        return t[:max(used, 1)], res, pages
+
+    def genome_rows(self, batch: HostBatch):
+        """(rows as uint8 [n_genomes * 16], target names) of the last run batch."""
+        gof, taln, names = batch.genomes()
+        rows = np.zeros(max(len(names), 1) * GENOME_ROW, np.uint8)
+        n = int(batch.view.n_alns)
+        rc = lib().pw_runner_genome_rows(self._h, np.ascontiguousarray(gof, np.uint32).ctypes.data if n else None,
+                                         np.ascontiguousarray(taln, np.int32).ctypes.data if n else None, n, len(names),
+                                         rows.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"pw_runner_genome_rows: {rc}")
+        return rows[: len(names) * GENOME_ROW], names
+
+    def close(self):
+        if self._h:
+            lib().pw_runner_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def version() -> str:

@@ -2631,6 +2631,9 @@ extern "C" pw_batch* pw_batch_from_buffer(const char* fasta, const char* text, u
   bt->pk.opt.skip_codan = skip;
   bt->pk.opt.single_query_gene = (bt->q.ids.size() == 1 && !full);
   bt->pk.opt.msa = false;
+  // PW_BATCH_GPU_PACK: the cs strings stay text for pw_runner_run to pack on the GPU (the CLI's
+  // default; PW_PACK_HOST=1 keeps the host packer)
+  bt->pk.opt.gpu_pack = (flags & PW_BATCH_GPU_PACK) && !(getenv("PW_PACK_HOST") && atoi(getenv("PW_PACK_HOST")) != 0);
   if (prev) {  // the next batch of the same input: the q~t pairs seen so far move over
     bt->pk.alnpairs = std::move(prev->pk.alnpairs);
     bt->pk.n_lines = prev->pk.n_lines;
@@ -3183,6 +3186,93 @@ BatchReaper* reaper() {
   return r;
 }
 }  // namespace
+
+// ----------------------------------------------------------------- batch runner
+// The CLI's device state (Device: queries and next-stop table uploaded once, device buffers grown
+// and reused across batches, GPU cs packing) behind the C ABI for the multi-GPU driver: a batch
+// runs on the runner's stream, its results / pages come back to host vectors here, and the used
+// text is copied into the caller's (pinned) buffer by pw_runner_fetch.
+struct pw_runner {
+  Device dev;
+  bool skip_codan = false;
+  size_t q_len = 0, q_n = 0;
+  std::vector<pw_aln_result> res;
+  std::vector<pw_page> pages;
+  uint64_t used = 0;
+  bool have = false;  // a finished batch whose outputs are here
+  DevBuf<uint32_t> gof;
+  DevBuf<int32_t> taln;
+  DevBuf<pw_genome_row> grows;
+};
+
+extern "C" pw_runner* pw_runner_create(const pw_batch* bt, char* errbuf, size_t errlen) {
+  if (!bt) {
+    if (errbuf && errlen) snprintf(errbuf, errlen, "bad arguments");
+    return nullptr;
+  }
+  pw_runner* r = new pw_runner();
+  r->skip_codan = bt->skip_codan;
+  r->q_len = bt->q.seq.size();
+  r->q_n = bt->q.len.size();
+  if (!r->dev.init(bt->q, bt->skip_codan)) {  // (Device::init prints the cause)
+    delete r;
+    if (errbuf && errlen) snprintf(errbuf, errlen, "device initialisation failed");
+    return nullptr;
+  }
+  return r;
+}
+
+extern "C" int pw_runner_run(pw_runner* r, pw_batch* bt, uint64_t* n_pages, uint64_t* text_used) {
+  if (!r || !bt || !n_pages || !text_used) return PW_E_ARG;
+  // (the runner's query set: the batch must come from the same FASTA and mode)
+  if (bt->skip_codan != r->skip_codan || bt->q.seq.size() != r->q_len || bt->q.len.size() != r->q_n) return PW_E_ARG;
+  r->have = false;
+  if (!r->dev.run(bt->b, bt->q, bt->skip_codan, nullptr, r->res, r->pages)) return PW_E_HIP;
+  const uint64_t tcap = pw_report_text_bytes(bt->b.n_events_max, bt->b.text_total);
+  uint64_t used = 0;
+  if (!bt->b.desc.empty())
+    for (const pw_page& pg : r->pages)
+      if (pg.len && pg.off + pg.len > used) used = pg.off + pg.len;
+  r->used = used < tcap ? used : tcap;
+  r->have = true;
+  *n_pages = r->pages.size();
+  *text_used = r->used;
+  return PW_OK;
+}
+
+extern "C" int pw_runner_fetch(pw_runner* r, pw_aln_result* res, uint64_t n_res, pw_page* pages, uint64_t n_pages,
+                               uint8_t* text, uint64_t text_cap) {
+  if (!r || !r->have || n_res != r->res.size() || n_pages != r->pages.size() || text_cap < r->used ||
+      (n_res && !res) || (n_pages && !pages) || (r->used && !text))
+    return PW_E_ARG;
+  if (n_res) memcpy(res, r->res.data(), n_res * sizeof(pw_aln_result));
+  if (n_pages) memcpy(pages, r->pages.data(), n_pages * sizeof(pw_page));
+  // (on the runner's stream; every path reaches ~57 GB/s alone on the box: tools/d2h_probe.py)
+  if (r->used && (hipMemcpyAsync(text, r->dev.text.p, r->used, hipMemcpyDeviceToHost, r->dev.stream) != hipSuccess ||
+                  hipStreamSynchronize(r->dev.stream) != hipSuccess))
+    return PW_E_HIP;
+  return PW_OK;
+}
+
+extern "C" int pw_runner_genome_rows(pw_runner* r, const uint32_t* genome_of, const int32_t* t_aln, uint32_t n_alns,
+                                     uint32_t n_genomes, pw_genome_row* rows) {
+  if (!r || !r->have || n_alns != r->res.size() || (n_alns && (!genome_of || !t_aln)) || (n_genomes && !rows))
+    return PW_E_ARG;
+  if (n_genomes == 0) return PW_OK;
+  hipStream_t st = r->dev.stream;
+  if (!r->gof.ensure(n_alns + 1) || !r->taln.ensure(n_alns + 1) || !r->grows.ensure(n_genomes)) return PW_E_NOMEM;
+  if (n_alns && (hipMemcpyAsync(r->gof.p, genome_of, (size_t)n_alns * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                 hipMemcpyAsync(r->taln.p, t_aln, (size_t)n_alns * 4, hipMemcpyHostToDevice, st) != hipSuccess))
+    return PW_E_HIP;
+  const int rc = pw_genome_table(r->dev.res.p, r->gof.p, r->taln.p, n_alns, r->grows.p, n_genomes, st);
+  if (rc != PW_OK) return rc;
+  if (hipMemcpyAsync(rows, r->grows.p, (size_t)n_genomes * sizeof(pw_genome_row), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return PW_E_HIP;
+  return PW_OK;
+}
+
+extern "C" void pw_runner_free(pw_runner* r) { delete r; }
 
 extern "C" void pw_batch_free(pw_batch* bt) {
   if (!bt) return;

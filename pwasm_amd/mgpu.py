@@ -475,6 +475,11 @@ def main(argv=None) -> int:
         return 1
     flags = ((pw.FLAG_G if "G" in opts else 0) | (pw.FLAG_F if "F" in opts else 0) |
              (pw.FLAG_C if "C" in opts else 0) | (pw.FLAG_N if "N" in opts else 0))
+    # the batches run through a pw_runner (the CLI's device session: cs strings packed on the GPU,
+    # device buffers reused); PW_MGPU_RUNNER=0: staged through torch tensors, host-packed
+    use_runner = os.environ.get("PW_MGPU_RUNNER", "1") != "0"
+    if use_runner:
+        flags |= pw.FLAG_GPU_PACK
     dv = device if backend != "gloo" else "cpu"
 
     prof = _Phases(rank)
@@ -532,6 +537,7 @@ def main(argv=None) -> int:
     want_tab = "genome-table" in extra
     gname, gacc = {}, np.zeros((1024, 3), np.uint64)  # target name -> row of the summed per-genome table
     th = None
+    runner = None
     if cuts:
         th = threading.Thread(target=make, args=(0, None))
         th.start()
@@ -545,26 +551,41 @@ def main(argv=None) -> int:
         if k + 1 < len(cuts):
             th = threading.Thread(target=make, args=(k + 1, b))
             th.start()
-        dev = pw.stage_batch(b, device)
-        prof.mark("stage")
-        pw.run_report(b, dev, stream.cuda_stream)
-        if want_tab:  # (the per-genome tables only when asked for: --genome-table)
-            rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
-            launch_genome_table(dev, rows, gt, stream.cuda_stream)
-        if prof.on:
-            stream.synchronize()
-            prof.mark("gpu pass")
         slot = []
-
-        def take(n):
-            prof.mark("fetch results/pages")
-            t = hostbufs.take(n, slot)
+        dev = None
+        if use_runner:
+            if runner is None:
+                runner = pw.Runner(b)
+            npg, used = runner.run(b)  # (GPU cs packing, the pass, results and pages back)
+            prof.mark("gpu pack + pass")
+            t = hostbufs.take(max(used, 1), slot)
             prof.mark("fetch alloc")
-            return t
-        text_h, res_h, pages_h = pw.fetch_outputs(dev, take)  # (synchronises the stream)
-        prof.mark("fetch text")
+            text_h, res_h, pages_h = runner.fetch(t, npg, used)
+            prof.mark("fetch text")
+            if want_tab:  # (the per-genome tables only when asked for: --genome-table)
+                rows_h, names = runner.genome_rows(b)
+        else:
+            dev = pw.stage_batch(b, device)
+            prof.mark("stage")
+            pw.run_report(b, dev, stream.cuda_stream)
+            if want_tab:
+                rows, names, gt = genome_rows(b, dev, stream.cuda_stream)
+                launch_genome_table(dev, rows, gt, stream.cuda_stream)
+            if prof.on:
+                stream.synchronize()
+                prof.mark("gpu pass")
+
+            def take(n):
+                prof.mark("fetch results/pages")
+                t = hostbufs.take(n, slot)
+                prof.mark("fetch alloc")
+                return t
+            text_h, res_h, pages_h = pw.fetch_outputs(dev, take)  # (synchronises the stream)
+            prof.mark("fetch text")
+            if want_tab:
+                rows_h = rows.cpu().numpy()
         if want_tab:  # per-genome rows of all batches, summed by target (vectorised: 50k targets a batch at cfg3)
-            r = rows.cpu().numpy().view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
+            r = rows_h.view(np.uint8).reshape(-1, 16) if len(names) else np.zeros((0, 16), np.uint8)
             gidx = np.fromiter((gname.setdefault(nm, len(gname)) for nm in names), dtype=np.int64, count=len(names))
             if len(gname) > gacc.shape[0]:
                 gacc = np.concatenate([gacc, np.zeros((max(len(gname), 2 * gacc.shape[0]) - gacc.shape[0], 3), np.uint64)])
@@ -590,6 +611,8 @@ def main(argv=None) -> int:
     if th is not None and th.is_alive():
         th.join()
     made.clear()
+    if runner is not None:
+        runner.close()
     gtabs = {nm: gacc[i] for nm, i in gname.items()}
     code = finish_run(writer, err, gtabs, extra, world, rank, device)
     prof.mark("finish")

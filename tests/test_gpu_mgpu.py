@@ -96,13 +96,16 @@ def _genome_table_from(paf, report):
     return tab
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_mgpu_matches_single_process(built, tmp_path, world):
+@pytest.mark.parametrize("world,runner", [(2, "1"), (3, "1"), (2, "0")])
+def test_mgpu_matches_single_process(built, tmp_path, world, runner):
+    """runner "1": batches through pw_runner (GPU cs packing, the CLI's device session; the genome
+    rows from its device results); "0": staged through torch tensors with host packing."""
     fa, paf = synth_paf(tmp_path, 0, seed=17)
     dup = _with_duplicates_and_comments(paf, tmp_path, 2)
     out = tmp_path / "r.txt"
     tab = tmp_path / "g.tsv"
-    rc, err = run_mgpu(world, ["-r", fa, dup, "-o", str(out), "--genome-table", str(tab)], tmp_path)
+    rc, err = run_mgpu(world, ["-r", fa, dup, "-o", str(out), "--genome-table", str(tab)], tmp_path,
+                       env={"PW_MGPU_RUNNER": runner})
     orc, oout, oerr = run([ORACLE, "-r", fa, dup])
     assert (rc, out.read_bytes(), err) == (orc, oout, oerr)
     want = _genome_table_from(dup, oout)
@@ -113,9 +116,12 @@ def test_mgpu_matches_single_process(built, tmp_path, world):
     assert got == dict(want)
 
 
-def test_mgpu_fatal_midway(built, tmp_path):
+@pytest.mark.parametrize("kind", ["mismatch", "mismatch_splice", "bounds"])
+def test_mgpu_fatal_midway(built, tmp_path, kind):
+    """A fatal line two thirds in: a base mismatch, an unknown op byte after a flipped base (the GPU
+    packer hands the record back to the host packer for the reference's error), a bounds violation."""
     fa, paf = synth_paf(tmp_path, 0, seed=41)
-    bad = _inject(paf, tmp_path, "mismatch", seed=5)
+    bad = _inject(paf, tmp_path, kind, seed=5)
     out = tmp_path / "r.txt"
     rc, err = run_mgpu(2, ["-r", fa, bad, "-o", str(out)], tmp_path)
     orc, oout, oerr = run([ORACLE, "-r", fa, bad])
