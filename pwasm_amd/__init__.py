@@ -373,10 +373,16 @@ class HostBatch:
         return eb.raw[: int(err_bytes)]
 
     def render_range(self, text_host, results_host, pages_host, first: int, out_bytes: int, n_items: int,
-                     err_bytes: int):
+                     err_bytes: int, out=None):
         """pw_batch_render_range: (stdout bytes of items [first, first + n_items) back to back as a
-        uint8 array of out_bytes, their stderr bytes)."""
-        out = np.empty(max(int(out_bytes), 1), dtype=np.uint8)
+        uint8 array of out_bytes, their stderr bytes).  out: a contiguous uint8 array of at least
+        out_bytes to render into (e.g. a slice of a reused send buffer)."""
+        if out is None:
+            out = np.empty(max(int(out_bytes), 1), dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.size < int(out_bytes):
+            raise ValueError("render_range: out must be a contiguous uint8 array of at least out_bytes")
+        elif out.size == 0:
+            out = np.empty(1, dtype=np.uint8)
         eb = ctypes.create_string_buffer(max(int(err_bytes), 1))
         rc = lib().pw_batch_render_range(self._h, text_host.ctypes.data, results_host.ctypes.data,
                                          pages_host.ctypes.data, int(first), int(n_items), out.ctypes.data,

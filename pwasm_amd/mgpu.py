@@ -242,6 +242,7 @@ class OffsetWriter:
         self.fd = os.open(out_path, os.O_WRONLY)
         self.rd = open(self.tmp_out, "rb") if self.tmp_out and rank == 0 else None
         self.prof = _Phases(rank, "window")  # PW_PROFILE_HOST: the steps of _window, summed
+        self._hb = [None, None]  # exchange write: reused send / receive buffers (_hostbuf)
 
     def _reduce(self, vals, op):
         import torch
@@ -310,14 +311,19 @@ class OffsetWriter:
         self.prof.mark("offsets")
         errs = []
         exch = self.world > 1 and self.mode == "exchange"
-        mine = []
-        for ent, (c, k) in zip(self.pending, spans):
+        if exch:  # this rank's items of the window, rendered back to back (line order) into one send buffer
+            nbs = [int(ent[0][4][2][c:k].sum()) for ent, (c, k) in zip(self.pending, spans)]
+            sbuf = self._hostbuf(0, sum(nbs))
+            pos = 0
+        for i_ent, (ent, (c, k)) in enumerate(zip(self.pending, spans)):
             if k == c:
                 continue
             b, text_h, res_h, pages_h, (ln, st, on, en) = ent[0]
-            if exch:  # this rank's items of the window, rendered back to back (line order)
-                out, eb = b.render_range(text_h, res_h, pages_h, c, int(on[c:k].sum()), k - c, int(en[c:k].sum()))
-                mine.append(out)
+            if exch:
+                nb = nbs[i_ent]
+                _, eb = b.render_range(text_h, res_h, pages_h, c, nb, k - c, int(en[c:k].sum()),
+                                       out=sbuf.numpy()[pos:pos + nb])
+                pos += nb
             else:
                 eb = b.write_range(text_h, res_h, pages_h, self.fd, c, off[ln[c:k].astype(np.int64) - lo],
                                    int(en[c:k].sum()))
@@ -328,7 +334,7 @@ class OffsetWriter:
             ent[1] = k
         self.prof.mark("render/write")
         if exch:
-            self._exchange_write(lens, own, off, mine)
+            self._exchange_write(lens, own, off, sbuf[:pos])
         keep = []
         for e in self.pending:
             if e[1] < len(e[0][4][0]):
@@ -363,7 +369,20 @@ class OffsetWriter:
             self.done = True
             self.fatal = True
 
-    def _exchange_write(self, lens, own, off, mine):
+    def _hostbuf(self, i, n):
+        """Reused host buffer i (0: the rendered items sent, 1: the bytes received) of at least n
+        bytes, as a uint8 tensor slice: pinned when the collectives run on the GPU (the copies to and
+        from the device then need no staging), grown by a quarter when short."""
+        import torch
+        n = int(n)
+        t = self._hb[i]
+        if t is None or t.numel() < max(n, 1):
+            self._hb[i] = None
+            pin = str(self.dv) != "cpu" and torch.cuda.is_available()
+            t = self._hb[i] = torch.empty(max(n + n // 4, 1 << 20), dtype=torch.uint8, pin_memory=pin)
+        return t[:n]
+
+    def _exchange_write(self, lens, own, off, sbuf):
         """Exchange write of one window (world > 1): the window's bytes are cut into one contiguous
         range per rank at line boundaries; every rank sends each of its rendered items to the rank
         whose range holds it (all_to_all_single: RCCL over xGMI with the nccl backend), and each
@@ -387,13 +406,18 @@ class OffsetWriter:
         rng = a + np.flatnonzero(lens[a:z] > 0)
         o_r = own[rng]
         recv = np.bincount(o_r, weights=lens[rng], minlength=W).astype(np.int64)
-        buf = np.concatenate(mine) if mine else np.zeros(0, np.uint8)
-        if buf.size != int(send.sum()):
+        if sbuf.numel() != int(send.sum()):
             raise RuntimeError("mgpu: rendered window bytes disagree with the item counts")
-        st = torch.from_numpy(buf).to(self.dv)
-        rt = torch.empty(int(recv.sum()), dtype=torch.uint8, device=self.dv)
+        nr = int(recv.sum())
+        st = sbuf.to(self.dv, non_blocking=True)  # (gloo: the host tensor itself)
+        rt = torch.empty(nr, dtype=torch.uint8, device=self.dv)
         dist.all_to_all_single(rt, st, [int(x) for x in recv], [int(x) for x in send])
-        got = rt.cpu().numpy()
+        if rt.device.type == "cpu":
+            got = rt.numpy()
+        else:  # into the reused (pinned) receive buffer; the copy waits for the collective
+            rb = self._hostbuf(1, nr)
+            rb.copy_(rt)
+            got = rb.numpy()
         if rng.size:
             l_r = lens[rng]
             base = np.concatenate([[0], np.cumsum(recv)[:-1]])
