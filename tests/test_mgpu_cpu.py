@@ -332,6 +332,10 @@ def test_render_range_equals_write_range(built, tmp_path, monkeypatch, img):
         os.close(fd)
     assert bytes(out) == p.read_bytes() and eb == eb2
     assert k > 10 and int(en.sum()) > 0
+    big = np.full(int(on.sum()) + 64, 0xAB, np.uint8)  # into a caller's buffer (the exchange write's)
+    _, eb3 = b.render_range(z, res, z, 0, int(on.sum()), k, int(en.sum()), out=big[16:16 + int(on.sum())])
+    assert bytes(big[16:16 + int(on.sum())]) == bytes(out) and eb3 == eb
+    assert (big[:16] == 0xAB).all() and (big[16 + int(on.sum()):] == 0xAB).all()
 
 
 def test_write_range_scattered_destinations(built, tmp_path):
