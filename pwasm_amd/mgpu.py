@@ -680,7 +680,11 @@ class HostTextPool:
             self.bufs[i] = None  # (release the smaller one first)
             self.bufs[i] = self._alloc(cap)
             if first and len(self.bufs) > 1:
-                def pre():
+                dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+
+                def pre():  # (on the caller's device: a thread starts on device 0)
+                    if dev is not None:
+                        torch.cuda.set_device(dev)
                     for j in range(len(self.bufs)):
                         if self.bufs[j] is None:
                             self.bufs[j] = self._alloc(cap)
