@@ -128,6 +128,18 @@ def test_mgpu_fatal_midway(built, tmp_path, kind):
     assert (rc, out.read_bytes(), err) == (orc, oout, oerr) and orc == 1
 
 
+@pytest.mark.parametrize("flags", [["-F"], ["-N"], ["-G"], ["-F", "-C"]])
+def test_mgpu_modes(built, tmp_path, flags):
+    """The report modes through the multi-GPU driver's runner path (GPU cs packing in every mode):
+    full-genome, no codon analysis, gene mode, full-genome with codons forced."""
+    fa, paf = synth_paf(tmp_path, 0, seed=23)
+    dup = _with_duplicates_and_comments(paf, tmp_path, 2)
+    out = tmp_path / "r.txt"
+    rc, err = run_mgpu(2, [*flags, "-r", fa, dup, "-o", str(out)], tmp_path)
+    orc, oout, oerr = run([ORACLE, *flags, "-r", fa, dup])
+    assert (rc, out.read_bytes(), err) == (orc, oout, oerr)
+
+
 def test_mgpu_cfg3_shards_gene_mode(built, tmp_path):
     fa, paf = synth_paf(tmp_path, 3, scale=0.002)
     out = tmp_path / "r.txt"
