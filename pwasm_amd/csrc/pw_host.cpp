@@ -3230,9 +3230,12 @@ extern "C" int pw_runner_run(pw_runner* r, pw_batch* bt, uint64_t* n_pages, uint
   if (!r->dev.run(bt->b, bt->q, bt->skip_codan, nullptr, r->res, r->pages)) return PW_E_HIP;
   const uint64_t tcap = pw_report_text_bytes(bt->b.n_events_max, bt->b.text_total);
   uint64_t used = 0;
-  if (!bt->b.desc.empty())
+  if (bt->b.desc.empty()) {  // (no pass ran: the pages Device::run sized are not written)
+    for (pw_page& pg : r->pages) pg = pw_page{0, 0, 0};
+  } else {
     for (const pw_page& pg : r->pages)
       if (pg.len && pg.off + pg.len > used) used = pg.off + pg.len;
+  }
   r->used = used < tcap ? used : tcap;
   r->have = true;
   *n_pages = r->pages.size();
