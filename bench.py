@@ -308,6 +308,12 @@ def report_leg(args, config, world, rank, dev_name):
         tot_events = int(e[0].item())
         tot_records = int(e[1].item())
     e2e_node = None
+    flags_cli = ["-G", "-C"] if flags else []
+    pre_hash = None
+    if sharded and world == 1 and not args.no_parity and not args.no_e2e:
+        # (the benchmarked batch's report is hashed before the end-to-end leg releases its device
+        # buffers; the rank-0 block below reuses the result)
+        pre_hash = hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp)
     if sharded and not args.no_e2e:
         # end to end over the node: pwasm_amd.mgpu (every rank reads 1/N of the PAF, exchanges lines
         # by target genome, packs / runs / writes its own records at their offsets of one report);
@@ -356,14 +362,14 @@ def report_leg(args, config, world, rank, dev_name):
         if config == 2 and args.scale == 1.0 and args.traffic_json and os.path.exists(args.traffic_json):
             prof = json.load(open(args.traffic_json))
         traffic = prof.get("hbm_bytes_per_report_pass", prof.get("hbm_bytes_per_launch"))
-        flags_cli = ["-G", "-C"] if flags else []
         parity, cpu, e2e, gpack = None, None, None, None
         big = config == 4 or v.n_alns > 200000
         if not args.no_parity and world == 1 and big:
             # too large for files on both sides: the report of the benchmarked batch and the
             # CLI's stdout streamed through CRC-32, against the oracle run over byte ranges of
             # the PAF in parallel processes with the CRCs combined (hash_parity)
-            parity, e2e, n_or = hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp)
+            parity, e2e, n_or = pre_hash if pre_hash is not None else hash_parity(pw, batch, dev, flags_cli, fa,
+                                                                                   paf, tmp)
             if n_or != n_events:
                 parity = "FAIL"
         elif not args.no_parity and world == 1:
@@ -755,12 +761,15 @@ def hash_parity(pw, batch, dev, flags_cli, fa, paf, tmp):
         with open(fifo, "rb") as f:
             got["r"] = crc_stream(f)
 
-    th = threading.Thread(target=reader)
+    th = threading.Thread(target=reader, daemon=True)
     th.start()
-    rc = batch.write_report_from(dev, fifo)
-    if rc != 0 and "r" not in got:  # never opened: release the reader
-        open(fifo, "wb").close()
-    th.join()
+    rc = -1
+    try:
+        rc = batch.write_report_from(dev, fifo)
+    finally:
+        if rc != 0 and "r" not in got:  # never opened (or failed first): release the reader
+            open(fifo, "wb").close()
+        th.join()
     batch_ok = rc == 0 and got.get("r") == want[:3]
     # the drop-in CLI writing its report to a local file (-o), timed alone; CRC-checked afterwards
     cli_out = os.path.join(tmp, "cli.txt")
