@@ -75,6 +75,7 @@ def main():
     if plan:  # python3 bench.py --gpus N: start the N ranks (nothing here has touched torch / HIP)
         sys.exit(run_ranks(plan))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_thread_share()
     if args.config is None:
         args.config = 2
     if args.traffic_json is None:  # the newest committed profile of the same command (profiles/run_prof.sh)
@@ -831,6 +832,15 @@ def cli_phases(flags_cli, fa, paf, outp):
     except OSError:
         pass
     return ph or None
+
+
+def rank_thread_share():
+    """Under torchrun (which sets OMP_NUM_THREADS=1 when the caller left it unset) a rank's host
+    pre-pass would run on one thread: with several ranks and no PW_THREADS, give each rank its share
+    of this process's CPUs (at most 16) through PW_THREADS, which the library reads first."""
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")) or 1)
+    if lw > 1 and not os.environ.get("PW_THREADS") and os.environ.get("OMP_NUM_THREADS") == "1":
+        os.environ["PW_THREADS"] = str(max(1, min(16, len(os.sched_getaffinity(0)) // lw)))
 
 
 def host_threads():

@@ -462,6 +462,11 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torchrun sets OMP_NUM_THREADS=1 when the caller left it unset: a rank's host work would run on
+    # one thread; give each rank its share of the CPUs instead (PW_THREADS, read by the library first)
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)) or 1)
+    if lw > 1 and not os.environ.get("PW_THREADS") and os.environ.get("OMP_NUM_THREADS") == "1":
+        os.environ["PW_THREADS"] = str(max(1, min(16, len(os.sched_getaffinity(0)) // lw)))
     backend = os.environ.get("PW_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if world > 1 and not dist.is_initialized():
         # c10d / gloo announce their connections on fd 1: keep that off the report (stdout)

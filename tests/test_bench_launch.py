@@ -89,3 +89,21 @@ def test_scaling_cfg3_keys_same_at_every_n():
     assert eight["value"] / one["value"] > 7 and one["e2e_wall_s"] / eight["e2e_wall_s"] == 5.0
     assert bench.CFG3_KEYS == ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config", "roofline",
                                "e2e")
+
+
+def test_rank_thread_share(monkeypatch):
+    """Several ranks under torchrun's OMP_NUM_THREADS=1: each rank gets its share of the CPUs as
+    PW_THREADS (at most 16); an explicit PW_THREADS, a chosen OMP_NUM_THREADS or one rank: untouched."""
+    import os
+    import bench
+    ncpu = len(os.sched_getaffinity(0))
+    for env, want in [({"LOCAL_WORLD_SIZE": "2", "OMP_NUM_THREADS": "1"}, str(max(1, min(16, ncpu // 2)))),
+                      ({"LOCAL_WORLD_SIZE": "2", "OMP_NUM_THREADS": "4"}, None),
+                      ({"LOCAL_WORLD_SIZE": "2", "OMP_NUM_THREADS": "1", "PW_THREADS": "3"}, "3"),
+                      ({"WORLD_SIZE": "1", "OMP_NUM_THREADS": "1"}, None)]:
+        for k in ("LOCAL_WORLD_SIZE", "WORLD_SIZE", "OMP_NUM_THREADS", "PW_THREADS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        bench.rank_thread_share()
+        assert os.environ.get("PW_THREADS") == want, env
